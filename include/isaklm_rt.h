@@ -1,0 +1,265 @@
+/*
+ * isaklm_rt.h — C-ABI of the MI355X-native path-tracing hot path.
+ *
+ * Drop-in boundary for INDA23PlusPlus/isaklm-raytracer's render path
+ * (SURVEY §8b).  Paths below are relative to /root/reference/isaklm-raytracer
+ * and abbreviated "rt/".
+ *
+ *   reference                                   this ABI
+ *   -------------------------------------------------------------------------
+ *   cudaMalloc / cudaMemcpy on the host path     rt_device_alloc / rt_upload /
+ *     (rt/create_scene.cuh:33-34,62-63,            rt_download / rt_free
+ *      rt/create_kd_tree.cuh:319-324,
+ *      rt/scene.cuh:58-59, rt/screen.cuh:24-45)
+ *   G_Buffer::G_Buffer()  rt/screen.cuh:22-46     rt_gbuffer_create / rt_gbuffer_seeds
+ *   load_mesh()           rt/mesh_loading.cuh:221 rt_host_scene_load_mesh
+ *   create_models()       rt/create_models.cuh:17 rt_host_scene_load_file (scene text file)
+ *   create_kd_tree()      rt/create_kd_tree.cuh:267  rt_build_kd_tree
+ *   create_scene()        rt/create_scene.cuh:18  rt_create_scene
+ *   (new) device re-layout                        rt_scene_prepare
+ *   render()              rt/render.cuh:62        rt_render
+ *   reset_frame<<<>>>     rt/render.cuh:18        (inside rt_render, sample_count==0)
+ *   draw_frame<<<>>>      rt/render.cuh:37        rt_tonemap (into an HBM RGBA8 buffer)
+ *   save_render()         rt/save_render.cuh:25   rt_save_render (PNG, same flip)
+ *
+ * Conventions: every function returns 0 on success and a negative RT_E_*
+ * code otherwise (rt_last_error() describes the last failure of the calling
+ * thread).  Pointers named *_device are HIP device pointers.  The caller owns
+ * every allocation and frees it explicitly (the reference leaks; see
+ * rt/screen.cuh:24-31).  Calls are synchronous unless an RtOptions.stream is
+ * given, in which case rt_render only enqueues.
+ */
+#ifndef ISAKLM_RT_H
+#define ISAKLM_RT_H
+
+#include <stddef.h>
+#include <stdint.h>
+#ifndef __cplusplus
+#include <stdbool.h>
+#endif
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------- reference-layout types (byte-identical) ---------------- */
+
+/* rt/math_library.cuh:71-82 (union {x,u},{y,v}) */
+typedef struct Vec2D { float x, y; } Vec2D;
+/* rt/math_library.cuh:115-131 (union {x,r},{y,g},{z,b}) */
+typedef struct Vec3D { float x, y, z; } Vec3D;
+/* CUDA uchar4, used for texels (rt/scene.cuh:18) */
+typedef struct RtUChar4 { uint8_t x, y, z, w; } RtUChar4;
+
+/* rt/scene.cuh:16-21 */
+typedef struct Texture {
+    RtUChar4 *buffer; /* device RGBA8 texels, NULL = no texture */
+    int width;
+    int height;
+} Texture;
+
+/* rt/scene.cuh:65-74 */
+typedef struct Material {
+    Vec3D albedo;
+    Vec3D emittance;
+    float roughness;
+    float refractive_index;
+    float extinction;
+    bool transparent;
+    Texture texture;
+} Material;
+
+/* rt/scene.cuh:76-82 */
+typedef struct Triangle {
+    Vec3D p1, p2, p3;
+    Vec3D n1, n2, n3;
+    Vec2D uv1, uv2, uv3;
+    Material material;
+} Triangle;
+
+/* rt/scene.cuh:84-100 */
+typedef struct KD_Tree_Node {
+    union { int index_offset; int child_index1; };
+    union { int triangle_count; int child_index2; };
+    uint8_t plane_axis;
+    float plane_offset;
+    bool is_leaf_node;
+} KD_Tree_Node;
+
+/* rt/scene.cuh:102-105 */
+typedef struct Bounding_Box { Vec3D min, max; } Bounding_Box;
+
+/* rt/scene.cuh:107-112 */
+typedef struct KD_Tree {
+    Bounding_Box bounding_box;
+    KD_Tree_Node *nodes;       /* device, pre-order (rt/create_kd_tree.cuh:286-298) */
+    int *triangle_indicies;    /* device (rt/create_kd_tree.cuh:300-312) */
+} KD_Tree;
+
+/* rt/scene.cuh:114-121 */
+typedef struct Scene {
+    Triangle *triangles;       /* device AoS */
+    int triangle_count;
+    int *light_indicies;       /* device */
+    int light_count;
+    KD_Tree kd_tree;
+} Scene;
+
+/* rt/screen.cuh:15-21 (per-pixel SoA device arrays, row-major, row 0 = bottom) */
+typedef struct G_Buffer {
+    Vec3D *frame_buffer;
+    float *squared_luminance;
+    int *sample_count;
+    uint32_t *random_numbers;
+} G_Buffer;
+
+/* rt/camera.cuh:15-26 */
+typedef struct Camera {
+    Vec3D position;
+    float yaw, pitch;
+    float FOV;
+    float aperture_radius;
+} Camera;
+
+#ifdef __cplusplus
+static_assert(sizeof(Vec2D) == 8, "Vec2D");
+static_assert(sizeof(Vec3D) == 12, "Vec3D");
+static_assert(sizeof(Texture) == 16, "Texture");
+static_assert(sizeof(Material) == 56 && offsetof(Material, roughness) == 24 &&
+              offsetof(Material, transparent) == 36 && offsetof(Material, texture) == 40, "Material");
+static_assert(sizeof(Triangle) == 152 && offsetof(Triangle, n1) == 36 && offsetof(Triangle, uv1) == 72 &&
+              offsetof(Triangle, material) == 96, "Triangle");
+static_assert(sizeof(KD_Tree_Node) == 20 && offsetof(KD_Tree_Node, plane_axis) == 8 &&
+              offsetof(KD_Tree_Node, plane_offset) == 12 && offsetof(KD_Tree_Node, is_leaf_node) == 16,
+              "KD_Tree_Node");
+static_assert(sizeof(Bounding_Box) == 24, "Bounding_Box");
+static_assert(sizeof(KD_Tree) == 40, "KD_Tree");
+static_assert(sizeof(Scene) == 72 && offsetof(Scene, light_indicies) == 16 && offsetof(Scene, kd_tree) == 32,
+              "Scene");
+static_assert(sizeof(G_Buffer) == 32, "G_Buffer");
+static_assert(sizeof(Camera) == 28 && offsetof(Camera, FOV) == 20, "Camera");
+#endif
+
+/* ---------------- status codes ---------------- */
+#define RT_OK 0
+#define RT_E_INVALID (-1)   /* bad argument / shape */
+#define RT_E_HIP (-2)       /* HIP runtime failure */
+#define RT_E_IO (-3)        /* file could not be read / written */
+#define RT_E_PARSE (-4)     /* malformed OBJ / .mat / scene file */
+#define RT_E_UNSUPPORTED (-5) /* e.g. KD tree deeper than the traversal stack */
+#define RT_E_NOMEM (-6)
+
+const char *rt_last_error(void);
+const char *rt_version(void);
+
+/* ---------------- device memory (hipMalloc/hipMemcpy stand-ins) ---------------- */
+int rt_device_alloc(void **ptr_device, size_t bytes);
+int rt_free(void *ptr_device);
+int rt_upload(void *dst_device, const void *src_host, size_t bytes);
+int rt_download(void *dst_host, const void *src_device, size_t bytes);
+int rt_memset(void *dst_device, int value, size_t bytes);
+int rt_device_count(int *count);
+int rt_set_device(int device);
+int rt_synchronize(void);
+void rt_host_free(void *ptr_host);  /* frees host arrays returned by this library */
+
+/* ---------------- G_Buffer (rt/screen.cuh:22-46) ---------------- */
+/* outputs [skip, skip+count) of std::mt19937 (default seed 5489) through
+ * uniform_int_distribution<uint32_t>(0, UINT32_MAX), i.e. the raw engine words
+ * (rt/screen.cuh:34-45).  Shard g of an spp-sliced render uses skip = g*W*H. */
+int rt_gbuffer_seeds(uint32_t *host_out, size_t count, uint64_t skip);
+/* allocates the four arrays for width*height pixels, zeroes fb/sq/count
+ * (the reference leaves them uninitialised until reset_frame) and uploads the
+ * seeds */
+int rt_gbuffer_create(int width, int height, uint64_t seed_skip, G_Buffer *out);
+int rt_gbuffer_destroy(G_Buffer *g);
+
+/* ---------------- host scene path ---------------- */
+typedef struct RtHostScene RtHostScene;
+int rt_host_scene_create(RtHostScene **out);
+void rt_host_scene_destroy(RtHostScene *scene);
+/* load_mesh (rt/mesh_loading.cuh:221-440): appends the OBJ's triangles,
+ * materials from the .mat file, re-centred on the mesh AABB and transformed by
+ * `matrix` (column vectors i,j,k = matrix[0..2],[3..5],[6..8]) + `offset`. */
+int rt_host_scene_load_mesh(RtHostScene *scene, const char *obj_path, const char *mat_path,
+                            const float offset[3], const float matrix[9], int smooth_normals);
+/* scene text file: "mesh <obj> <mat> ox oy oz yaw pitch scale smooth" lines
+ * (create_models' rotation_matrix(yaw,pitch)*scale transforms,
+ * rt/create_models.cuh:21-39) and one "camera px py pz yaw pitch fov aperture"
+ * line (rt/main.cu:101-104).  Relative paths resolve against the file's dir. */
+int rt_host_scene_load_file(RtHostScene *scene, const char *scene_path, Camera *camera_out);
+int rt_host_scene_triangles(const RtHostScene *scene, const Triangle **triangles, int *count);
+/* Synthetic scenes for BASELINE.json's configs (the reference's OBJ models
+ * are unpublished): writes OBJ + .mat + scene.txt into out_dir and
+ * returns the scene.txt path.  Names: cornell (cfg 1), cornell_blob (cfg 2),
+ * room2m (cfg 3/4), room2m_glass (cfg 5), room_small (tests). */
+int rt_generate_scene(const char *name, const char *out_dir, char *scene_path_out, size_t cap);
+
+/* create_kd_tree (rt/create_kd_tree.cuh:267-328) on the host: identical tree,
+ * node numbering and index order.  Outputs are host arrays (rt_host_free). */
+int rt_build_kd_tree(const Triangle *host_triangles, int triangle_count, KD_Tree_Node **nodes_out,
+                     int *node_count, int **indices_out, int *index_count, Bounding_Box *bounds_out);
+
+/* create_scene (rt/create_scene.cuh:18-73): uploads triangles, the light list
+ * and the KD tree into a reference-layout device Scene. */
+int rt_create_scene(const RtHostScene *scene, Scene *out, int *node_count, int *index_count);
+int rt_destroy_scene(Scene *scene);
+
+/* ---------------- prepared (MI355X-layout) scene ---------------- */
+typedef struct RtPreparedScene *rt_scene_t;
+/* Re-lays a reference-layout device Scene into the traversal layout (SoA
+ * nodes, precomputed triangle planes).  Bit-preserving: every precomputed
+ * value is the reference's own expression evaluated once. */
+int rt_scene_prepare(const Scene *device_scene, int node_count, int index_count, rt_scene_t *out);
+/* same from host arrays (skips a device round trip) */
+int rt_scene_prepare_host(const Triangle *triangles, int triangle_count, const KD_Tree_Node *nodes,
+                          int node_count, const int *indices, int index_count, const int *lights,
+                          int light_count, Bounding_Box bounds, rt_scene_t *out);
+int rt_scene_release(rt_scene_t scene);
+/* device bytes held by the prepared scene */
+int rt_scene_info(rt_scene_t scene, size_t *device_bytes, int *triangle_count, int *node_count,
+                  int *index_count, int *max_depth);
+
+/* ---------------- render (rt/render.cuh:62-76) ---------------- */
+/* work counters (SURVEY §8d algorithmic bytes) */
+enum {
+    RT_CNT_NODE = 0,   /* KD node fetches */
+    RT_CNT_TRI = 1,    /* triangle tests */
+    RT_CNT_HIT = 2,    /* closest-hit shadings */
+    RT_CNT_TEXEL = 3,  /* texel reads */
+    RT_CNT_NEE = 4,    /* next-event estimations */
+    RT_CNT_SAMPLE = 5, /* samples traced */
+    RT_CNT_SKIP = 6,   /* pixel-passes skipped by the adaptive test */
+    RT_CNT_RAY = 7,    /* trace_ray calls */
+    RT_CNT_WATCHDOG = 8, /* paths cut by the bounce watchdog */
+    RT_CNT_COUNT = 16
+};
+
+typedef struct RtOptions {
+    int width, height;   /* frame (rt/macros.h:3-4: 1920x1080) */
+    int passes;          /* passes per call; the reference runs 1 per render() */
+    int adaptive;        /* 1: rt/path_tracing.cuh:352-376 test; 0: always sample */
+    int min_samples;     /* MIN_SAMPLES (rt/macros.h:13) */
+    float tolerance;     /* MAX_TOLERANCE (rt/macros.h:17) */
+    int max_depth;       /* 0 = unbounded (reference); else max extension rays per path */
+    int kernel;          /* kernel variant, 0 = default */
+    void *stream;        /* hipStream_t; NULL = synchronous on the null stream */
+    unsigned long long *counters_device; /* optional RT_CNT_COUNT u64 counters (adds) */
+} RtOptions;
+
+void rt_default_options(RtOptions *opt);
+/* render(): if sample_count == 0 the frame's fb/sq/count are reset first
+ * (reset_frame; RNG state is kept), then opt->passes passes run, each one
+ * sample for every pixel that passes the adaptive test. */
+int rt_render(rt_scene_t scene, G_Buffer g_buffer, Camera camera, int sample_count, const RtOptions *opt);
+
+/* draw_frame's colour math (rt/render.cuh:37-59): correct_color(fb/count) ->
+ * RGBA8 into a device buffer of width*height*4 bytes, row 0 = bottom. */
+int rt_tonemap(G_Buffer g_buffer, uint8_t *rgba_device, int width, int height, void *stream);
+/* save_render (rt/save_render.cuh:25-67): tonemap, flip vertically, write PNG */
+int rt_save_render(G_Buffer g_buffer, int width, int height, const char *png_path);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ISAKLM_RT_H */

@@ -1,0 +1,73 @@
+"""Builds the in-tree HIP library libisaklm_rt.so for gfx950 (and nothing else).
+
+Host C++ (scene loading, exact KD build, prepare) is compiled by g++, the
+kernels and the C-ABI by hipcc --offload-arch=gfx950; everything with
+-ffp-contract=off so host-precomputed constants and
+GPU arithmetic round identically.  Rebuilds only what changed.
+"""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+BUILD = os.path.join(HERE, "_build")
+LIB = os.path.join(HERE, "libisaklm_rt.so")
+ROOT = os.path.dirname(HERE)
+INCLUDE = os.path.join(ROOT, "include")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+
+HOST_SOURCES = ["host/mesh_loading.cpp", "host/kd_build.cpp", "host/scene_prepare.cpp", "host/misc.cpp",
+                "host/scenes.cpp"]
+HIP_SOURCES = ["path_kernel.hip", "abi.hip"]
+HEADERS = ["rt_libm.h", "rt_vecmath.h", "rt_device.h", "host/rt_host.h"]
+
+COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-I" + INCLUDE, "-I" + CSRC]
+HOST_FLAGS = ["-fopenmp", "-Wall", "-Wno-unused-function"]
+HIP_FLAGS = ["--offload-arch=gfx950", "-fno-gpu-rdc", "-munsafe-fp-atomics", "-Wno-unused-command-line-argument"]
+
+
+def _run(cmd, verbose):
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout + r.stderr)
+        raise RuntimeError("build failed: " + " ".join(cmd[:2]) + " ...")
+    elif verbose and (r.stdout or r.stderr):
+        sys.stderr.write(r.stdout + r.stderr)
+
+
+def _stale(out, deps):
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(verbose=False, extra_hip_flags=()):
+    os.makedirs(BUILD, exist_ok=True)
+    headers = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(INCLUDE, "isaklm_rt.h")]
+    objs = []
+    for src in HOST_SOURCES:
+        s = os.path.join(CSRC, src)
+        o = os.path.join(BUILD, os.path.basename(src) + ".o")
+        if _stale(o, [s] + headers):
+            _run(["g++"] + COMMON + HOST_FLAGS + ["-c", s, "-o", o], verbose)
+        objs.append(o)
+    hipcc = os.path.join(ROCM, "bin", "hipcc")
+    for src in HIP_SOURCES:
+        s = os.path.join(CSRC, src)
+        o = os.path.join(BUILD, os.path.basename(src) + ".o")
+        if _stale(o, [s] + headers) or extra_hip_flags:
+            _run([hipcc] + COMMON + HIP_FLAGS + list(extra_hip_flags) + ["-c", s, "-o", o], verbose)
+        objs.append(o)
+    if _stale(LIB, objs):
+        _run(["g++", "-shared", "-o", LIB] + objs +
+             ["-L" + os.path.join(ROCM, "lib"), "-lamdhip64", "-fopenmp",
+              "-Wl,-rpath," + os.path.join(ROCM, "lib")], verbose)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(verbose=True))

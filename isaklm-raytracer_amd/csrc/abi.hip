@@ -1,0 +1,445 @@
+// abi.hip — implementation of include/isaklm_rt.h (the drop-in boundary).
+//
+// Thin by design: host scene code lives in host/*.cpp, kernels in
+// path_kernel.hip.  Every entry point checks its arguments and every HIP
+// call, returning RT_E_* instead of the reference's silent failures
+// (SURVEY §5 "Failure detection").
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "host/rt_host.h"
+
+int rt_launch_path(const RtDevScene &sc, const RtDevFrame &fr, const RtDevCamera &cam, int stack_depth,
+                   hipStream_t stream);
+int rt_launch_tonemap(const Vec3D *fb, const int *count, RtUChar4 *out, int n, hipStream_t stream);
+
+static thread_local std::string g_error;
+
+void rt_set_error(const char *fmt, ...)
+{
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_error = buf;
+}
+
+#define HIPCHK(expr)                                                                                 \
+    do {                                                                                             \
+        hipError_t e_ = (expr);                                                                      \
+        if (e_ != hipSuccess) {                                                                      \
+            rt_set_error("%s failed: %s", #expr, hipGetErrorString(e_));                             \
+            return RT_E_HIP;                                                                         \
+        }                                                                                            \
+    } while (0)
+
+struct RtPreparedScene {
+    RtDevScene dev;
+    std::vector<void *> allocs;
+    size_t bytes = 0;
+    int ntris = 0, nnodes = 0, nindices = 0, max_depth = 0;
+};
+
+namespace {
+
+template <typename T>
+int upload_vec(RtPreparedScene &s, const std::vector<T> &v, const T **out)
+{
+    void *p = nullptr;
+    size_t n = v.size() * sizeof(T);
+    HIPCHK(hipMalloc(&p, n > 0 ? n : 16));
+    s.allocs.push_back(p);
+    s.bytes += n;
+    if (n) HIPCHK(hipMemcpy(p, v.data(), n, hipMemcpyHostToDevice));
+    *out = (const T *)p;
+    return RT_OK;
+}
+
+void release(RtPreparedScene *s)
+{
+    if (!s) return;
+    for (void *p : s->allocs) (void)hipFree(p);
+    delete s;
+}
+
+int upload_prepared(const rt_host::PreparedHost &h, int ntris, int nindices, rt_scene_t *out)
+{
+    RtPreparedScene *s = new RtPreparedScene();
+    int rc = RT_OK;
+    const uint32_t *nodes = nullptr;
+    const int *leaf = nullptr, *lights = nullptr;
+    const RtF4 *a = nullptr, *b = nullptr, *c = nullptr, *d = nullptr, *sh = nullptr;
+    const float *r = nullptr;
+    const RtDevMaterial *mats = nullptr;
+    if ((rc = upload_vec(*s, h.nodes, &nodes)) || (rc = upload_vec(*s, h.leaf_tris, &leaf)) ||
+        (rc = upload_vec(*s, h.isect_a, &a)) || (rc = upload_vec(*s, h.isect_b, &b)) ||
+        (rc = upload_vec(*s, h.isect_c, &c)) || (rc = upload_vec(*s, h.isect_d, &d)) ||
+        (rc = upload_vec(*s, h.isect_r, &r)) || (rc = upload_vec(*s, h.shade, &sh)) ||
+        (rc = upload_vec(*s, h.materials, &mats)) || (rc = upload_vec(*s, h.lights, &lights))) {
+        release(s);
+        return rc;
+    }
+    RtDevScene &dv = s->dev;
+    dv.nodes = nodes;
+    dv.leaf_tris = leaf;
+    dv.isect_a = a;
+    dv.isect_b = b;
+    dv.isect_c = c;
+    dv.isect_d = d;
+    dv.isect_r = r;
+    dv.shade = sh;
+    dv.materials = mats;
+    dv.lights = lights;
+    dv.light_count = h.light_count;
+    dv.triangle_count = ntris;
+    dv.bmin[0] = h.bounds.min.x; dv.bmin[1] = h.bounds.min.y; dv.bmin[2] = h.bounds.min.z;
+    dv.bmax[0] = h.bounds.max.x; dv.bmax[1] = h.bounds.max.y; dv.bmax[2] = h.bounds.max.z;
+    s->ntris = ntris;
+    s->nnodes = (int)(h.nodes.size() / 2);
+    s->nindices = nindices;
+    s->max_depth = h.max_depth;
+    *out = s;
+    return RT_OK;
+}
+
+} // namespace
+
+extern "C" {
+
+const char *rt_last_error(void) { return g_error.c_str(); }
+const char *rt_version(void) { return "isaklm-raytracer_amd 0.1 (gfx950)"; }
+
+// ---------------- device memory ----------------
+int rt_device_alloc(void **ptr, size_t bytes)
+{
+    if (!ptr) { rt_set_error("rt_device_alloc: null out"); return RT_E_INVALID; }
+    HIPCHK(hipMalloc(ptr, bytes ? bytes : 16));
+    return RT_OK;
+}
+int rt_free(void *ptr)
+{
+    if (ptr) HIPCHK(hipFree(ptr));
+    return RT_OK;
+}
+int rt_upload(void *dst, const void *src, size_t bytes)
+{
+    if (bytes == 0) return RT_OK;
+    if (!dst || !src) { rt_set_error("rt_upload: null pointer"); return RT_E_INVALID; }
+    HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+    return RT_OK;
+}
+int rt_download(void *dst, const void *src, size_t bytes)
+{
+    if (bytes == 0) return RT_OK;
+    if (!dst || !src) { rt_set_error("rt_download: null pointer"); return RT_E_INVALID; }
+    HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+int rt_memset(void *dst, int value, size_t bytes)
+{
+    if (bytes == 0) return RT_OK;
+    HIPCHK(hipMemset(dst, value, bytes));
+    return RT_OK;
+}
+int rt_device_count(int *count)
+{
+    if (!count) return RT_E_INVALID;
+    HIPCHK(hipGetDeviceCount(count));
+    return RT_OK;
+}
+int rt_set_device(int device)
+{
+    HIPCHK(hipSetDevice(device));
+    return RT_OK;
+}
+int rt_synchronize(void)
+{
+    HIPCHK(hipDeviceSynchronize());
+    return RT_OK;
+}
+void rt_host_free(void *p) { free(p); }
+
+// ---------------- G_Buffer ----------------
+int rt_gbuffer_seeds(uint32_t *out, size_t count, uint64_t skip)
+{
+    if (!out && count) { rt_set_error("rt_gbuffer_seeds: null out"); return RT_E_INVALID; }
+    rt_host::mt19937_seeds(out, count, skip);
+    return RT_OK;
+}
+
+int rt_gbuffer_create(int w, int h, uint64_t skip, G_Buffer *g)
+{
+    if (!g || w <= 0 || h <= 0) { rt_set_error("rt_gbuffer_create: bad arguments"); return RT_E_INVALID; }
+    const size_t n = (size_t)w * (size_t)h;
+    memset(g, 0, sizeof *g);
+    std::vector<uint32_t> seeds(n);
+    rt_host::mt19937_seeds(seeds.data(), n, skip);
+    HIPCHK(hipMalloc((void **)&g->frame_buffer, n * sizeof(Vec3D)));
+    HIPCHK(hipMalloc((void **)&g->squared_luminance, n * sizeof(float)));
+    HIPCHK(hipMalloc((void **)&g->sample_count, n * sizeof(int)));
+    HIPCHK(hipMalloc((void **)&g->random_numbers, n * sizeof(uint32_t)));
+    HIPCHK(hipMemset(g->frame_buffer, 0, n * sizeof(Vec3D)));
+    HIPCHK(hipMemset(g->squared_luminance, 0, n * sizeof(float)));
+    HIPCHK(hipMemset(g->sample_count, 0, n * sizeof(int)));
+    HIPCHK(hipMemcpy(g->random_numbers, seeds.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice));
+    return RT_OK;
+}
+
+int rt_gbuffer_destroy(G_Buffer *g)
+{
+    if (!g) return RT_E_INVALID;
+    (void)hipFree(g->frame_buffer);
+    (void)hipFree(g->squared_luminance);
+    (void)hipFree(g->sample_count);
+    (void)hipFree(g->random_numbers);
+    memset(g, 0, sizeof *g);
+    return RT_OK;
+}
+
+// ---------------- host scene ----------------
+int rt_host_scene_create(RtHostScene **out)
+{
+    if (!out) return RT_E_INVALID;
+    *out = new RtHostScene();
+    return RT_OK;
+}
+void rt_host_scene_destroy(RtHostScene *s) { delete s; }
+
+int rt_host_scene_load_mesh(RtHostScene *s, const char *obj, const char *mat, const float offset[3],
+                            const float m[9], int smooth)
+{
+    if (!s || !obj || !mat || !offset || !m) { rt_set_error("rt_host_scene_load_mesh: null argument"); return RT_E_INVALID; }
+    RtM3 M = {rt_v3(m[0], m[1], m[2]), rt_v3(m[3], m[4], m[5]), rt_v3(m[6], m[7], m[8])};
+    return rt_host::load_mesh(*s, obj, mat, rt_v3(offset[0], offset[1], offset[2]), M, smooth != 0);
+}
+
+int rt_host_scene_load_file(RtHostScene *s, const char *path, Camera *cam)
+{
+    if (!s || !path) { rt_set_error("rt_host_scene_load_file: null argument"); return RT_E_INVALID; }
+    return rt_host::load_scene_file(*s, path, cam);
+}
+
+int rt_host_scene_triangles(const RtHostScene *s, const Triangle **tris, int *count)
+{
+    if (!s || !tris || !count) return RT_E_INVALID;
+    *tris = s->tris.data();
+    *count = (int)s->tris.size();
+    return RT_OK;
+}
+
+int rt_build_kd_tree(const Triangle *tris, int n, KD_Tree_Node **nodes_out, int *node_count, int **idx_out,
+                     int *index_count, Bounding_Box *bounds)
+{
+    if (!tris || n <= 0 || !nodes_out || !node_count || !idx_out || !index_count || !bounds) {
+        rt_set_error("rt_build_kd_tree: bad arguments");
+        return RT_E_INVALID;
+    }
+    std::vector<KD_Tree_Node> nodes;
+    std::vector<int> idx;
+    int rc = rt_host::build_kd_tree(tris, n, nodes, idx, *bounds);
+    if (rc) return rc;
+    *nodes_out = (KD_Tree_Node *)malloc(nodes.size() * sizeof(KD_Tree_Node));
+    *idx_out = (int *)malloc((idx.size() ? idx.size() : 1) * sizeof(int));
+    if (!*nodes_out || !*idx_out) { rt_set_error("out of host memory"); return RT_E_NOMEM; }
+    memcpy(*nodes_out, nodes.data(), nodes.size() * sizeof(KD_Tree_Node));
+    memcpy(*idx_out, idx.data(), idx.size() * sizeof(int));
+    *node_count = (int)nodes.size();
+    *index_count = (int)idx.size();
+    return RT_OK;
+}
+
+// create_scene (rt/create_scene.cuh:18-73)
+int rt_create_scene(const RtHostScene *s, Scene *out, int *node_count, int *index_count)
+{
+    if (!s || !out || s->tris.empty()) { rt_set_error("rt_create_scene: bad arguments"); return RT_E_INVALID; }
+    memset(out, 0, sizeof *out);
+    const int n = (int)s->tris.size();
+    std::vector<KD_Tree_Node> nodes;
+    std::vector<int> idx;
+    Bounding_Box bb;
+    int rc = rt_host::build_kd_tree(s->tris.data(), n, nodes, idx, bb);
+    if (rc) return rc;
+    std::vector<int> lights = rt_host::light_list(s->tris.data(), n);
+    HIPCHK(hipMalloc((void **)&out->triangles, (size_t)n * sizeof(Triangle)));
+    HIPCHK(hipMemcpy(out->triangles, s->tris.data(), (size_t)n * sizeof(Triangle), hipMemcpyHostToDevice));
+    out->triangle_count = n;
+    HIPCHK(hipMalloc((void **)&out->light_indicies, (lights.size() + 1) * sizeof(int)));
+    if (!lights.empty())
+        HIPCHK(hipMemcpy(out->light_indicies, lights.data(), lights.size() * sizeof(int), hipMemcpyHostToDevice));
+    out->light_count = (int)lights.size();
+    HIPCHK(hipMalloc((void **)&out->kd_tree.nodes, nodes.size() * sizeof(KD_Tree_Node)));
+    HIPCHK(hipMemcpy(out->kd_tree.nodes, nodes.data(), nodes.size() * sizeof(KD_Tree_Node), hipMemcpyHostToDevice));
+    HIPCHK(hipMalloc((void **)&out->kd_tree.triangle_indicies, (idx.size() + 1) * sizeof(int)));
+    if (!idx.empty())
+        HIPCHK(hipMemcpy(out->kd_tree.triangle_indicies, idx.data(), idx.size() * sizeof(int), hipMemcpyHostToDevice));
+    out->kd_tree.bounding_box = bb;
+    if (node_count) *node_count = (int)nodes.size();
+    if (index_count) *index_count = (int)idx.size();
+    return RT_OK;
+}
+
+int rt_destroy_scene(Scene *s)
+{
+    if (!s) return RT_E_INVALID;
+    (void)hipFree(s->triangles);
+    (void)hipFree(s->light_indicies);
+    (void)hipFree(s->kd_tree.nodes);
+    (void)hipFree(s->kd_tree.triangle_indicies);
+    memset(s, 0, sizeof *s);
+    return RT_OK;
+}
+
+// ---------------- prepared scene ----------------
+int rt_scene_prepare_host(const Triangle *tris, int ntris, const KD_Tree_Node *nodes, int nnodes, const int *idx,
+                          int nidx, const int *lights, int nlights, Bounding_Box bounds, rt_scene_t *out)
+{
+    if (!out) return RT_E_INVALID;
+    rt_host::PreparedHost h;
+    int rc = rt_host::prepare_host(tris, ntris, nodes, nnodes, idx, nidx, lights, nlights, bounds, h);
+    if (rc) return rc;
+    return upload_prepared(h, ntris, nidx, out);
+}
+
+int rt_scene_prepare(const Scene *ds, int node_count, int index_count, rt_scene_t *out)
+{
+    if (!ds || !out || ds->triangle_count <= 0 || node_count <= 0 || index_count < 0 || ds->light_count < 0) {
+        rt_set_error("rt_scene_prepare: bad arguments");
+        return RT_E_INVALID;
+    }
+    std::vector<Triangle> tris((size_t)ds->triangle_count);
+    std::vector<KD_Tree_Node> nodes((size_t)node_count);
+    std::vector<int> idx((size_t)index_count), lights((size_t)ds->light_count);
+    HIPCHK(hipMemcpy(tris.data(), ds->triangles, tris.size() * sizeof(Triangle), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(nodes.data(), ds->kd_tree.nodes, nodes.size() * sizeof(KD_Tree_Node), hipMemcpyDeviceToHost));
+    if (index_count)
+        HIPCHK(hipMemcpy(idx.data(), ds->kd_tree.triangle_indicies, idx.size() * sizeof(int), hipMemcpyDeviceToHost));
+    if (ds->light_count)
+        HIPCHK(hipMemcpy(lights.data(), ds->light_indicies, lights.size() * sizeof(int), hipMemcpyDeviceToHost));
+    return rt_scene_prepare_host(tris.data(), ds->triangle_count, nodes.data(), node_count, idx.data(), index_count,
+                                 lights.data(), ds->light_count, ds->kd_tree.bounding_box, out);
+}
+
+int rt_scene_release(rt_scene_t s)
+{
+    release(s);
+    return RT_OK;
+}
+
+int rt_scene_info(rt_scene_t s, size_t *bytes, int *ntris, int *nnodes, int *nidx, int *max_depth)
+{
+    if (!s) return RT_E_INVALID;
+    if (bytes) *bytes = s->bytes;
+    if (ntris) *ntris = s->ntris;
+    if (nnodes) *nnodes = s->nnodes;
+    if (nidx) *nidx = s->nindices;
+    if (max_depth) *max_depth = s->max_depth;
+    return RT_OK;
+}
+
+// ---------------- render ----------------
+void rt_default_options(RtOptions *o)
+{
+    if (!o) return;
+    memset(o, 0, sizeof *o);
+    o->width = 1920;       // rt/macros.h:3
+    o->height = 1080;      // rt/macros.h:4
+    o->passes = 1;
+    o->adaptive = 1;
+    o->min_samples = 100;  // rt/macros.h:13
+    o->tolerance = 0.05f;  // rt/macros.h:17
+    o->max_depth = 0;
+}
+
+// render (rt/render.cuh:62-76)
+int rt_render(rt_scene_t scene, G_Buffer g, Camera cam, int sample_count, const RtOptions *opt)
+{
+    RtOptions o;
+    if (opt) o = *opt; else rt_default_options(&o);
+    if (!scene || !g.frame_buffer || !g.squared_luminance || !g.sample_count || !g.random_numbers) {
+        rt_set_error("rt_render: null scene or G_Buffer array");
+        return RT_E_INVALID;
+    }
+    if (o.width <= 0 || o.height <= 0 || o.width < 2 || o.passes < 0 || o.min_samples < 0 ||
+        (long long)o.width * o.height > (1LL << 31) - 1) {
+        rt_set_error("rt_render: bad frame size / passes");
+        return RT_E_INVALID;
+    }
+    RtDevFrame fr;
+    fr.fb = g.frame_buffer;
+    fr.sq = g.squared_luminance;
+    fr.count = g.sample_count;
+    fr.rng = g.random_numbers;
+    fr.width = o.width;
+    fr.height = o.height;
+    fr.half_w = o.width / 2;   // SCREEN_W / 2 (integer division)
+    fr.half_h = o.height / 2;
+    fr.passes = o.passes;
+    fr.adaptive = o.adaptive;
+    fr.min_samples = o.min_samples;
+    fr.tolerance = o.tolerance;
+    fr.z_const = rt_adaptive_z(o.tolerance);
+    fr.max_depth = o.max_depth;
+    fr.reset = sample_count == 0;
+    fr.counters = o.counters_device;
+
+    // Camera::rotation() and tanf(FOV / 2) are frame constants (rt/camera.cuh:22-25, :381)
+    RtDevCamera dc;
+    RtM3 R = rt_rotation_matrix(cam.yaw, cam.pitch);
+    dc.R[0] = R.i.x; dc.R[1] = R.i.y; dc.R[2] = R.i.z;
+    dc.R[3] = R.j.x; dc.R[4] = R.j.y; dc.R[5] = R.j.z;
+    dc.R[6] = R.k.x; dc.R[7] = R.k.y; dc.R[8] = R.k.z;
+    dc.pos[0] = cam.position.x; dc.pos[1] = cam.position.y; dc.pos[2] = cam.position.z;
+    dc.tan_half_fov = rt_tanf(cam.FOV / 2);
+    dc.aperture = cam.aperture_radius;
+
+    hipStream_t stream = (hipStream_t)o.stream;
+    if (rt_launch_path(scene->dev, fr, dc, scene->max_depth, stream) != 0) {
+        rt_set_error("rt_render: kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
+        return RT_E_HIP;
+    }
+    if (!o.stream) HIPCHK(hipStreamSynchronize(nullptr));
+    return RT_OK;
+}
+
+int rt_tonemap(G_Buffer g, uint8_t *rgba, int w, int h, void *stream)
+{
+    if (!rgba || !g.frame_buffer || !g.sample_count || w <= 0 || h <= 0) {
+        rt_set_error("rt_tonemap: bad arguments");
+        return RT_E_INVALID;
+    }
+    if (rt_launch_tonemap(g.frame_buffer, g.sample_count, (RtUChar4 *)rgba, w * h, (hipStream_t)stream) != 0) {
+        rt_set_error("rt_tonemap: launch failed");
+        return RT_E_HIP;
+    }
+    if (!stream) HIPCHK(hipStreamSynchronize(nullptr));
+    return RT_OK;
+}
+
+// save_render (rt/save_render.cuh:25-67): tonemap on the GPU, flip rows, PNG
+int rt_save_render(G_Buffer g, int w, int h, const char *path)
+{
+    if (!path || w <= 0 || h <= 0) { rt_set_error("rt_save_render: bad arguments"); return RT_E_INVALID; }
+    const size_t n = (size_t)w * h;
+    uint8_t *d = nullptr;
+    HIPCHK(hipMalloc((void **)&d, n * 4));
+    int rc = rt_tonemap(g, d, w, h, nullptr);
+    std::vector<uint8_t> img(n * 4), flipped(n * 4);
+    if (rc == RT_OK && hipMemcpy(img.data(), d, n * 4, hipMemcpyDeviceToHost) != hipSuccess) {
+        rt_set_error("rt_save_render: download failed");
+        rc = RT_E_HIP;
+    }
+    (void)hipFree(d);
+    if (rc) return rc;
+    for (int y = 0; y < h; ++y) // flipped_pixel_index = (H - y - 1) * W + x  (:55)
+        memcpy(&flipped[(size_t)(h - y - 1) * w * 4], &img[(size_t)y * w * 4], (size_t)w * 4);
+    return rt_host::write_png(path, flipped.data(), w, h);
+}
+
+} // extern "C"

@@ -1,0 +1,54 @@
+// rt_host.h — host-side (CPU) pieces of the render path's boundary:
+// scene loading, exact KD build, seeds, scene preparation, image output.
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "../rt_device.h"
+#include "../rt_vecmath.h"
+
+void rt_set_error(const char *fmt, ...);
+
+struct RtHostScene {
+    std::vector<Triangle> tris;
+};
+
+namespace rt_host {
+
+// load_mesh (rt/mesh_loading.cuh:221-440)
+int load_mesh(RtHostScene &scene, const std::string &obj_path, const std::string &mat_path, Vec3D offset,
+              RtM3 matrix, bool smooth_normals);
+// create_models as data (rt/create_models.cuh:17-43) + camera (rt/main.cu:101-104)
+int load_scene_file(RtHostScene &scene, const std::string &path, Camera *camera_out);
+
+// create_kd_tree (rt/create_kd_tree.cuh:267-328), identical output
+int build_kd_tree(const Triangle *tris, int n, std::vector<KD_Tree_Node> &nodes, std::vector<int> &indices,
+                  Bounding_Box &bounds);
+// light list of create_scene (rt/create_scene.cuh:40-49)
+std::vector<int> light_list(const Triangle *tris, int n);
+
+// std::mt19937 seeds (rt/screen.cuh:34-45)
+void mt19937_seeds(uint32_t *out, size_t count, uint64_t skip);
+
+// host image of the device layout (rt_device.h) before upload
+struct PreparedHost {
+    std::vector<uint32_t> nodes;
+    std::vector<int> leaf_tris;
+    std::vector<RtF4> isect_a, isect_b, isect_c, isect_d;
+    std::vector<float> isect_r;
+    std::vector<RtF4> shade;
+    std::vector<RtDevMaterial> materials;
+    std::vector<int> lights; // light_count + 1
+    int light_count = 0;
+    int max_depth = 0;
+    Bounding_Box bounds;
+};
+int prepare_host(const Triangle *tris, int ntris, const KD_Tree_Node *nodes, int nnodes, const int *indices,
+                 int nindices, const int *lights, int nlights, Bounding_Box bounds, PreparedHost &out);
+
+int write_png(const char *path, const uint8_t *rgba, int width, int height);
+
+} // namespace rt_host

@@ -1,0 +1,175 @@
+// scene_prepare.cpp — reference-layout Scene -> traversal layout (rt_device.h).
+//
+// Bit-preserving: the per-triangle constants are exactly the sub-expressions
+// intersect_triangle / calculate_barycentric_coordinates compute per test
+// (rt/trace_ray.cuh:48-113), evaluated once here with the same operations
+// (-ffp-contract=off), so a test on the GPU sees the same floats.  Nodes are
+// renumbered into pre-order with child1 == node + 1, which is the identity
+// for trees from create_kd_tree (rt/create_kd_tree.cuh:225-258) and keeps
+// traversal order for any other tree.
+#include <string.h>
+
+#include <map>
+#include <string>
+#include <vector>
+
+#include "rt_host.h"
+
+namespace rt_host {
+
+static inline uint32_t fbits(float f)
+{
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    return u;
+}
+static inline float bitsf(uint32_t u)
+{
+    float f;
+    memcpy(&f, &u, 4);
+    return f;
+}
+static inline RtF4 f4(float x, float y, float z, float w) { return RtF4{x, y, z, w}; }
+
+int prepare_host(const Triangle *tris, int ntris, const KD_Tree_Node *nodes, int nnodes, const int *indices,
+                 int nindices, const int *lights, int nlights, Bounding_Box bounds, PreparedHost &out)
+{
+    if (ntris <= 0 || nnodes <= 0 || !tris || !nodes || (nindices > 0 && !indices) || nlights < 0 ||
+        (nlights > 0 && !lights)) {
+        rt_set_error("prepare: invalid scene arrays");
+        return RT_E_INVALID;
+    }
+    if (ntris >= (1 << 30) || nnodes >= (1 << 30) || nindices >= (1 << 30)) {
+        rt_set_error("prepare: scene too large for 30-bit node/leaf fields");
+        return RT_E_UNSUPPORTED;
+    }
+    // --- nodes: pre-order renumbering + validation -----------------------
+    std::vector<int> new_id((size_t)nnodes, -1);
+    std::vector<int> order;
+    order.reserve((size_t)nnodes);
+    struct Item { int node, depth; };
+    std::vector<Item> st;
+    st.push_back({0, 0});
+    int max_depth = 0;
+    while (!st.empty()) {
+        Item it = st.back();
+        st.pop_back();
+        if (it.node < 0 || it.node >= nnodes || new_id[it.node] != -1) {
+            rt_set_error("prepare: KD node %d out of range or shared", it.node);
+            return RT_E_INVALID;
+        }
+        new_id[it.node] = (int)order.size();
+        order.push_back(it.node);
+        const KD_Tree_Node &n = nodes[it.node];
+        if (!n.is_leaf_node) {
+            if (n.plane_axis > 2) {
+                rt_set_error("prepare: node %d has plane axis %d", it.node, (int)n.plane_axis);
+                return RT_E_INVALID;
+            }
+            max_depth = it.depth + 1 > max_depth ? it.depth + 1 : max_depth;
+            st.push_back({n.child_index2, it.depth + 1}); // popped after child1's subtree
+            st.push_back({n.child_index1, it.depth + 1});
+        } else if (n.triangle_count < 0 || n.index_offset < 0 ||
+                   (n.triangle_count > 0 && (long long)n.index_offset + n.triangle_count > nindices)) {
+            rt_set_error("prepare: leaf %d addresses indices out of range", it.node);
+            return RT_E_INVALID;
+        }
+    }
+    if (max_depth > RT_STACK_DEPTH) {
+        rt_set_error("prepare: KD tree depth %d exceeds the traversal stack (%d)", max_depth, RT_STACK_DEPTH);
+        return RT_E_UNSUPPORTED;
+    }
+    out.max_depth = max_depth;
+    out.nodes.assign(2 * order.size(), 0u);
+    for (size_t k = 0; k < order.size(); ++k) {
+        const KD_Tree_Node &n = nodes[order[k]];
+        if (n.is_leaf_node) {
+            out.nodes[2 * k] = (uint32_t)n.index_offset;
+            out.nodes[2 * k + 1] = ((uint32_t)n.triangle_count << 2) | RT_LEAF_TAG;
+        } else {
+            if (new_id[n.child_index1] != (int)k + 1) {
+                rt_set_error("prepare: internal renumbering error");
+                return RT_E_INVALID;
+            }
+            out.nodes[2 * k] = fbits(n.plane_offset);
+            out.nodes[2 * k + 1] = ((uint32_t)new_id[n.child_index2] << 2) | (uint32_t)n.plane_axis;
+        }
+    }
+    out.leaf_tris.assign(indices, indices + nindices);
+    for (int i = 0; i < nindices; ++i)
+        if (indices[i] < 0 || indices[i] >= ntris) {
+            rt_set_error("prepare: triangle index %d out of range", indices[i]);
+            return RT_E_INVALID;
+        }
+
+    // --- materials (deduplicated by value) --------------------------------
+    std::map<std::string, int> mat_ids;
+    std::vector<int> tri_mat((size_t)ntris);
+    out.materials.clear();
+    for (int i = 0; i < ntris; ++i) {
+        const Material &m = tris[i].material;
+        RtDevMaterial d;
+        memset(&d, 0, sizeof d);
+        d.albedo[0] = m.albedo.x; d.albedo[1] = m.albedo.y; d.albedo[2] = m.albedo.z;
+        d.roughness = m.roughness;
+        d.emittance[0] = m.emittance.x; d.emittance[1] = m.emittance.y; d.emittance[2] = m.emittance.z;
+        d.refractive_index = m.refractive_index;
+        d.extinction = m.extinction;
+        d.transparent = m.transparent ? 1 : 0;
+        d.tex = m.texture.buffer;
+        d.tex_width = m.texture.buffer ? m.texture.width : 0;
+        d.tex_height = m.texture.buffer ? m.texture.height : 0;
+        std::string key((const char *)&d, sizeof d);
+        auto it = mat_ids.find(key);
+        if (it == mat_ids.end()) {
+            it = mat_ids.emplace(key, (int)out.materials.size()).first;
+            out.materials.push_back(d);
+        }
+        tri_mat[i] = it->second;
+    }
+
+    // --- per-triangle constants (rt/trace_ray.cuh:48-113) -----------------
+    out.isect_a.resize((size_t)ntris);
+    out.isect_b.resize((size_t)ntris);
+    out.isect_c.resize((size_t)ntris);
+    out.isect_d.resize((size_t)ntris);
+    out.isect_r.resize((size_t)ntris);
+    out.shade.resize(7 * (size_t)ntris);
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < ntris; ++i) {
+        const Triangle &t = tris[i];
+        Vec3D v0 = t.p2 - t.p1;
+        Vec3D v1 = t.p3 - t.p1;
+        Vec3D n = rt_normalize(rt_cross(v0, v1)); // cross(p2 - p1, p3 - p1)
+        float d = rt_dot(n, t.p1);
+        float d00 = rt_dot(v0, v0), d01 = rt_dot(v0, v1), d11 = rt_dot(v1, v1);
+        float rd = 1.0f / (d00 * d11 - d01 * d01);
+        out.isect_a[i] = f4(n.x, n.y, n.z, d);
+        out.isect_b[i] = f4(t.p1.x, t.p1.y, t.p1.z, d00);
+        out.isect_c[i] = f4(v0.x, v0.y, v0.z, d01);
+        out.isect_d[i] = f4(v1.x, v1.y, v1.z, d11);
+        out.isect_r[i] = rd;
+        RtF4 *s = &out.shade[7 * (size_t)i];
+        s[0] = f4(t.p1.x, t.p1.y, t.p1.z, bitsf((uint32_t)tri_mat[i]));
+        s[1] = f4(t.p2.x, t.p2.y, t.p2.z, t.uv1.x);
+        s[2] = f4(t.p3.x, t.p3.y, t.p3.z, t.uv1.y);
+        s[3] = f4(t.n1.x, t.n1.y, t.n1.z, t.uv2.x);
+        s[4] = f4(t.n2.x, t.n2.y, t.n2.z, t.uv2.y);
+        s[5] = f4(t.n3.x, t.n3.y, t.n3.z, t.uv3.x);
+        s[6] = f4(t.uv3.y, 0.0f, 0.0f, 0.0f);
+    }
+
+    // --- lights: one padding entry for the xi == 1.0 draw -----
+    out.lights.assign(lights, lights + nlights);
+    for (int l : out.lights)
+        if (l < 0 || l >= ntris) {
+            rt_set_error("prepare: light index %d out of range", l);
+            return RT_E_INVALID;
+        }
+    out.lights.push_back(nlights > 0 ? lights[nlights - 1] : 0);
+    out.light_count = nlights;
+    out.bounds = bounds;
+    return RT_OK;
+}
+
+} // namespace rt_host

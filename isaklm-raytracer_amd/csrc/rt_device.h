@@ -1,0 +1,80 @@
+// rt_device.h — the MI355X traversal layout of a prepared scene.
+//
+// The reference keeps 152-B AoS triangles with an embedded material and 20-B
+// AoS KD nodes (rt/scene.cuh:65-100).  A ray query there reads 36 of the 152
+// bytes per triangle test and recomputes the plane, cross product, normalize
+// and Cramer denominators each time (rt/trace_ray.cuh:73-113).  Here:
+//
+//  * nodes: 8 B each, pre-order, child1 == node+1 implicit
+//      inner:  x = plane_offset bits, y = (child2 << 2) | axis      (axis 0..2)
+//      leaf:   x = index_offset,      y = (triangle_count << 2) | 3
+//  * per-triangle intersection constants, SoA float4 streams indexed by the
+//    triangle id, each value the reference's own expression evaluated once:
+//      isect_a = {n.x, n.y, n.z, d}        n = normalize(cross(p2-p1, p3-p1)), d = dot(n, p1)
+//      isect_b = {p1.x, p1.y, p1.z, d00}
+//      isect_c = {v0.x, v0.y, v0.z, d01}   v0 = p2-p1
+//      isect_d = {v1.x, v1.y, v1.z, d11}   v1 = p3-p1
+//      isect_r = 1/(d00*d11 - d01*d01)
+//    A test that is rejected by the plane (dn == 0, s < 1e-5, s >= closest)
+//    reads only isect_a (16 B).
+//  * shading record (hit only), 7 float4 per triangle: p1..p3, n1..n3,
+//    uv1..uv3 and the material id; materials deduplicated into a table.
+#pragma once
+#include <stdint.h>
+
+#include "../../include/isaklm_rt.h"
+
+#define RT_STACK_DEPTH 24       // traversal stack entries (reference: KD_TREE_DEPTH = 19)
+#define RT_LEAF_TAG 3u
+#define RT_WATCHDOG_BOUNCES 65536 // SURVEY H8; never reached by a parity config
+
+struct RtDevMaterial {          // 64 B
+    float albedo[3];
+    float roughness;
+    float emittance[3];
+    float refractive_index;
+    float extinction;
+    int transparent;
+    int tex_width, tex_height;
+    const RtUChar4 *tex;        // device texels or nullptr
+    int pad[2];
+};
+static_assert(sizeof(RtDevMaterial) == 64, "RtDevMaterial");
+
+struct RtF4 { float x, y, z, w; };
+
+struct RtDevScene {
+    const uint32_t *nodes;      // 2 words per node
+    const int *leaf_tris;       // KD triangle_indicies
+    const RtF4 *isect_a, *isect_b, *isect_c, *isect_d;
+    const float *isect_r;
+    const RtF4 *shade;          // 7 per triangle
+    const RtDevMaterial *materials;
+    const int *lights;          // light_count + 1 entries (SURVEY H4 padding)
+    int light_count;
+    int triangle_count;
+    float bmin[3], bmax[3];
+};
+
+struct RtDevCamera {            // Camera precomputed once per call (same ops as the reference)
+    float R[9];                 // rotation_matrix(yaw, pitch): i, j, k
+    float pos[3];
+    float tan_half_fov;         // tanf(FOV / 2)
+    float aperture;
+};
+
+struct RtDevFrame {
+    Vec3D *fb;
+    float *sq;
+    int *count;
+    uint32_t *rng;
+    int width, height, half_w, half_h;
+    int passes;
+    int adaptive;
+    int min_samples;
+    float tolerance;
+    float z_const;              // sqrtf(2) * erfinvf(1 - tolerance)
+    int max_depth;              // 0 = unbounded (watchdog)
+    int reset;                  // sample_count == 0
+    unsigned long long *counters;
+};

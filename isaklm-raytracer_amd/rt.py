@@ -1,0 +1,320 @@
+"""ctypes binding of include/isaklm_rt.h — the host-side mirror of the
+reference's render interface (create_scene / G_Buffer / Camera / render /
+save_render, rt/main.cu:97-132) used by the tests, smoke() and bench.py.
+
+The product path is the in-tree libisaklm_rt.so (HIP kernels for gfx950);
+importing this module fails loudly if it is missing — there is no CPU
+fallback.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libisaklm_rt.so")
+
+
+class Vec3D(ctypes.Structure):
+    _fields_ = [("x", ctypes.c_float), ("y", ctypes.c_float), ("z", ctypes.c_float)]
+
+
+class Bounding_Box(ctypes.Structure):
+    _fields_ = [("min", Vec3D), ("max", Vec3D)]
+
+
+class KD_Tree(ctypes.Structure):
+    _fields_ = [("bounding_box", Bounding_Box), ("nodes", ctypes.c_void_p), ("triangle_indicies", ctypes.c_void_p)]
+
+
+class Scene(ctypes.Structure):  # rt/scene.cuh:114-121
+    _fields_ = [("triangles", ctypes.c_void_p), ("triangle_count", ctypes.c_int),
+                ("light_indicies", ctypes.c_void_p), ("light_count", ctypes.c_int), ("kd_tree", KD_Tree)]
+
+
+class G_Buffer(ctypes.Structure):  # rt/screen.cuh:15-21
+    _fields_ = [("frame_buffer", ctypes.c_void_p), ("squared_luminance", ctypes.c_void_p),
+                ("sample_count", ctypes.c_void_p), ("random_numbers", ctypes.c_void_p)]
+
+
+class Camera(ctypes.Structure):  # rt/camera.cuh:15-26
+    _fields_ = [("position", Vec3D), ("yaw", ctypes.c_float), ("pitch", ctypes.c_float),
+                ("FOV", ctypes.c_float), ("aperture_radius", ctypes.c_float)]
+
+    def as_list(self):
+        p = self.position
+        return [p.x, p.y, p.z, self.yaw, self.pitch, self.FOV, self.aperture_radius]
+
+
+class RtOptions(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_int), ("height", ctypes.c_int), ("passes", ctypes.c_int),
+                ("adaptive", ctypes.c_int), ("min_samples", ctypes.c_int), ("tolerance", ctypes.c_float),
+                ("max_depth", ctypes.c_int), ("kernel", ctypes.c_int), ("stream", ctypes.c_void_p),
+                ("counters_device", ctypes.c_void_p)]
+
+
+TRIANGLE_BYTES = 152
+NODE_BYTES = 20
+COUNTER_NAMES = ["node", "tri", "hit", "texel", "nee", "sample", "skip", "ray", "watchdog"]
+N_COUNTERS = 16
+
+_lib = None
+
+
+class RtError(RuntimeError):
+    pass
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RtError(f"{LIB_PATH} is missing: run __graft_entry__.build() (no CPU fallback exists)")
+        L = ctypes.CDLL(LIB_PATH)
+        vp, i, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
+        L.rt_last_error.restype = ctypes.c_char_p
+        L.rt_version.restype = ctypes.c_char_p
+        L.rt_device_alloc.argtypes = [ctypes.POINTER(vp), sz]
+        L.rt_free.argtypes = [vp]
+        L.rt_upload.argtypes = [vp, vp, sz]
+        L.rt_download.argtypes = [vp, vp, sz]
+        L.rt_memset.argtypes = [vp, i, sz]
+        L.rt_device_count.argtypes = [ctypes.POINTER(i)]
+        L.rt_set_device.argtypes = [i]
+        L.rt_host_free.argtypes = [vp]
+        L.rt_host_free.restype = None
+        L.rt_gbuffer_seeds.argtypes = [vp, sz, ctypes.c_uint64]
+        L.rt_gbuffer_create.argtypes = [i, i, ctypes.c_uint64, ctypes.POINTER(G_Buffer)]
+        L.rt_gbuffer_destroy.argtypes = [ctypes.POINTER(G_Buffer)]
+        L.rt_host_scene_create.argtypes = [ctypes.POINTER(vp)]
+        L.rt_host_scene_destroy.argtypes = [vp]
+        L.rt_host_scene_destroy.restype = None
+        L.rt_host_scene_load_mesh.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, vp, vp, i]
+        L.rt_host_scene_load_file.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(Camera)]
+        L.rt_host_scene_triangles.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(i)]
+        L.rt_generate_scene.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, sz]
+        L.rt_build_kd_tree.argtypes = [vp, i, ctypes.POINTER(vp), ctypes.POINTER(i), ctypes.POINTER(vp),
+                                       ctypes.POINTER(i), ctypes.POINTER(Bounding_Box)]
+        L.rt_create_scene.argtypes = [vp, ctypes.POINTER(Scene), ctypes.POINTER(i), ctypes.POINTER(i)]
+        L.rt_destroy_scene.argtypes = [ctypes.POINTER(Scene)]
+        L.rt_scene_prepare.argtypes = [ctypes.POINTER(Scene), i, i, ctypes.POINTER(vp)]
+        L.rt_scene_prepare_host.argtypes = [vp, i, vp, i, vp, i, vp, i, Bounding_Box, ctypes.POINTER(vp)]
+        L.rt_scene_release.argtypes = [vp]
+        L.rt_scene_info.argtypes = [vp, ctypes.POINTER(sz), ctypes.POINTER(i), ctypes.POINTER(i),
+                                    ctypes.POINTER(i), ctypes.POINTER(i)]
+        L.rt_default_options.argtypes = [ctypes.POINTER(RtOptions)]
+        L.rt_default_options.restype = None
+        L.rt_render.argtypes = [vp, G_Buffer, Camera, i, ctypes.POINTER(RtOptions)]
+        L.rt_tonemap.argtypes = [G_Buffer, vp, i, i, vp]
+        L.rt_save_render.argtypes = [G_Buffer, i, i, ctypes.c_char_p]
+        _lib = L
+    return _lib
+
+
+def check(rc):
+    if rc != 0:
+        raise RtError(f"rt error {rc}: {lib().rt_last_error().decode()}")
+
+
+def _ptr(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def generate_scene(name, out_dir):
+    buf = ctypes.create_string_buffer(4096)
+    check(lib().rt_generate_scene(name.encode(), out_dir.encode(), buf, 4096))
+    return buf.value.decode()
+
+
+def seeds(count, skip=0):
+    out = np.zeros(count, dtype=np.uint32)
+    check(lib().rt_gbuffer_seeds(_ptr(out), count, skip))
+    return out
+
+
+class HostScene:
+    """Host triangle list (create_models / load_mesh, rt/create_models.cuh:17)."""
+
+    def __init__(self, scene_path=None):
+        h = ctypes.c_void_p()
+        check(lib().rt_host_scene_create(ctypes.byref(h)))
+        self.h = h
+        self.camera = Camera()
+        if scene_path:
+            check(lib().rt_host_scene_load_file(self.h, scene_path.encode(), ctypes.byref(self.camera)))
+
+    def load_mesh(self, obj, mat, offset, matrix, smooth=False):
+        off = np.asarray(offset, dtype=np.float32)
+        m = np.asarray(matrix, dtype=np.float32).reshape(9)
+        check(lib().rt_host_scene_load_mesh(self.h, obj.encode(), mat.encode(), _ptr(off), _ptr(m), int(smooth)))
+
+    def triangles_bytes(self):
+        p, n = ctypes.c_void_p(), ctypes.c_int()
+        check(lib().rt_host_scene_triangles(self.h, ctypes.byref(p), ctypes.byref(n)))
+        return ctypes.string_at(p, n.value * TRIANGLE_BYTES), n.value
+
+    def triangle_ptr(self):
+        p, n = ctypes.c_void_p(), ctypes.c_int()
+        check(lib().rt_host_scene_triangles(self.h, ctypes.byref(p), ctypes.byref(n)))
+        return p, n.value
+
+    def __del__(self):
+        try:
+            if getattr(self, "h", None):
+                lib().rt_host_scene_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+
+def build_kd_tree(tri_ptr, n):
+    """create_kd_tree on the host -> (nodes bytes, indices int32 array, bounds[6])."""
+    L = lib()
+    nodes, idx = ctypes.c_void_p(), ctypes.c_void_p()
+    nn, ni = ctypes.c_int(), ctypes.c_int()
+    bb = Bounding_Box()
+    check(L.rt_build_kd_tree(tri_ptr, n, ctypes.byref(nodes), ctypes.byref(nn), ctypes.byref(idx),
+                             ctypes.byref(ni), ctypes.byref(bb)))
+    nb = ctypes.string_at(nodes, nn.value * NODE_BYTES)
+    ib = np.frombuffer(ctypes.string_at(idx, ni.value * 4), dtype=np.int32).copy()
+    L.rt_host_free(nodes)
+    L.rt_host_free(idx)
+    return nb, ib, [bb.min.x, bb.min.y, bb.min.z, bb.max.x, bb.max.y, bb.max.z]
+
+
+class DeviceScene:
+    """create_scene (rt/create_scene.cuh:18) -> reference-layout device Scene,
+    then rt_scene_prepare -> traversal layout."""
+
+    def __init__(self, host_scene):
+        self.scene = Scene()
+        nn, ni = ctypes.c_int(), ctypes.c_int()
+        check(lib().rt_create_scene(host_scene.h, ctypes.byref(self.scene), ctypes.byref(nn), ctypes.byref(ni)))
+        self.node_count, self.index_count = nn.value, ni.value
+        self.prepared = ctypes.c_void_p()
+        check(lib().rt_scene_prepare(ctypes.byref(self.scene), nn, ni, ctypes.byref(self.prepared)))
+
+    def info(self):
+        b, t, n, i, d = ctypes.c_size_t(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        check(lib().rt_scene_info(self.prepared, ctypes.byref(b), ctypes.byref(t), ctypes.byref(n), ctypes.byref(i),
+                                  ctypes.byref(d)))
+        return {"device_bytes": b.value, "triangles": t.value, "nodes": n.value, "indices": i.value,
+                "max_depth": d.value, "lights": self.scene.light_count}
+
+    def release(self):
+        if getattr(self, "prepared", None):
+            lib().rt_scene_release(self.prepared)
+            self.prepared = None
+        if getattr(self, "scene", None) is not None and self.scene.triangles:
+            lib().rt_destroy_scene(ctypes.byref(self.scene))
+
+    def __del__(self):
+        try:
+            self.release()
+        except Exception:
+            pass
+
+
+class GBuffer:
+    """G_Buffer (rt/screen.cuh:22-46) on the device; seeds = mt19937 outputs
+    [seed_skip, seed_skip + W*H)."""
+
+    def __init__(self, width, height, seed_skip=0):
+        self.width, self.height = width, height
+        self.g = G_Buffer()
+        check(lib().rt_gbuffer_create(width, height, seed_skip, ctypes.byref(self.g)))
+
+    @property
+    def n(self):
+        return self.width * self.height
+
+    def download(self):
+        n = self.n
+        fb = np.zeros((n, 3), dtype=np.float32)
+        sq = np.zeros(n, dtype=np.float32)
+        cnt = np.zeros(n, dtype=np.int32)
+        rng = np.zeros(n, dtype=np.uint32)
+        L = lib()
+        check(L.rt_download(_ptr(fb), self.g.frame_buffer, fb.nbytes))
+        check(L.rt_download(_ptr(sq), self.g.squared_luminance, sq.nbytes))
+        check(L.rt_download(_ptr(cnt), self.g.sample_count, cnt.nbytes))
+        check(L.rt_download(_ptr(rng), self.g.random_numbers, rng.nbytes))
+        return fb, sq, cnt, rng
+
+    def upload(self, fb, sq, cnt, rng):
+        L = lib()
+        fb = np.ascontiguousarray(fb, dtype=np.float32)
+        sq = np.ascontiguousarray(sq, dtype=np.float32)
+        cnt = np.ascontiguousarray(cnt, dtype=np.int32)
+        rng = np.ascontiguousarray(rng, dtype=np.uint32)
+        check(L.rt_upload(self.g.frame_buffer, _ptr(fb), fb.nbytes))
+        check(L.rt_upload(self.g.squared_luminance, _ptr(sq), sq.nbytes))
+        check(L.rt_upload(self.g.sample_count, _ptr(cnt), cnt.nbytes))
+        check(L.rt_upload(self.g.random_numbers, _ptr(rng), rng.nbytes))
+
+    def free(self):
+        if getattr(self, "g", None) is not None and self.g.frame_buffer:
+            lib().rt_gbuffer_destroy(ctypes.byref(self.g))
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def options(width, height, passes=1, adaptive=True, min_samples=100, tolerance=0.05, max_depth=0, stream=None,
+            counters=None):
+    o = RtOptions()
+    lib().rt_default_options(ctypes.byref(o))
+    o.width, o.height, o.passes = width, height, passes
+    o.adaptive, o.min_samples, o.tolerance, o.max_depth = int(adaptive), min_samples, tolerance, max_depth
+    o.stream = stream
+    o.counters_device = counters
+    return o
+
+
+def render(dscene, gbuf, camera, sample_count, opt):
+    """render() (rt/render.cuh:62): resets when sample_count == 0, then opt.passes passes."""
+    check(lib().rt_render(dscene.prepared, gbuf.g, camera, sample_count, ctypes.byref(opt)))
+
+
+class DeviceCounters:
+    def __init__(self):
+        p = ctypes.c_void_p()
+        check(lib().rt_device_alloc(ctypes.byref(p), N_COUNTERS * 8))
+        self.p = p
+        self.zero()
+
+    def zero(self):
+        check(lib().rt_memset(self.p, 0, N_COUNTERS * 8))
+
+    def read(self):
+        a = np.zeros(N_COUNTERS, dtype=np.uint64)
+        check(lib().rt_download(_ptr(a), self.p, a.nbytes))
+        return {k: int(a[i]) for i, k in enumerate(COUNTER_NAMES)}
+
+    def __del__(self):
+        try:
+            lib().rt_free(self.p)
+        except Exception:
+            pass
+
+
+def tonemap(gbuf):
+    """draw_frame colour math -> (H*W, 4) uint8, row 0 = bottom."""
+    L = lib()
+    n = gbuf.n
+    d = ctypes.c_void_p()
+    check(L.rt_device_alloc(ctypes.byref(d), n * 4))
+    try:
+        check(L.rt_tonemap(gbuf.g, d, gbuf.width, gbuf.height, None))
+        out = np.zeros((n, 4), dtype=np.uint8)
+        check(L.rt_download(_ptr(out), d, out.nbytes))
+    finally:
+        L.rt_free(d)
+    return out
+
+
+def save_render(gbuf, path):
+    check(lib().rt_save_render(gbuf.g, gbuf.width, gbuf.height, path.encode()))
