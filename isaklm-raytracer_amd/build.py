@@ -5,6 +5,7 @@ kernels and the C-ABI by hipcc --offload-arch=gfx950; everything with
 -ffp-contract=off so host-precomputed constants and
 GPU arithmetic round identically.  Rebuilds only what changed.
 """
+import hashlib
 import os
 import subprocess
 import sys
@@ -45,7 +46,26 @@ def _stale(out, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+STAMP = LIB + ".stamp"
+
+
+def _digest(extra_hip_flags):
+    h = hashlib.sha256()
+    files = [os.path.join(CSRC, f) for f in HOST_SOURCES + HIP_SOURCES + HEADERS] + [os.path.join(INCLUDE,
+                                                                                                  "isaklm_rt.h")]
+    for f in files:
+        with open(f, "rb") as fh:
+            h.update(os.path.relpath(f, ROOT).encode() + fh.read())
+    flags = [x for x in COMMON + HOST_FLAGS + HIP_FLAGS + list(extra_hip_flags) if not x.startswith("-I")]
+    h.update(" ".join(flags).encode())
+    return h.hexdigest()
+
+
 def build(verbose=False, extra_hip_flags=()):
+    """Builds libisaklm_rt.so unless the stamp shows it was built from these exact sources."""
+    digest = _digest(extra_hip_flags)
+    if os.path.exists(LIB) and os.path.exists(STAMP) and open(STAMP).read().strip() == digest:
+        return LIB
     os.makedirs(BUILD, exist_ok=True)
     headers = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(INCLUDE, "isaklm_rt.h")]
     objs = []
@@ -66,6 +86,8 @@ def build(verbose=False, extra_hip_flags=()):
         _run(["g++", "-shared", "-o", LIB] + objs +
              ["-L" + os.path.join(ROCM, "lib"), "-lamdhip64", "-fopenmp",
               "-Wl,-rpath," + os.path.join(ROCM, "lib")], verbose)
+    with open(STAMP, "w") as fh:
+        fh.write(digest + "\n")
     return LIB
 
 
