@@ -87,6 +87,7 @@ def main():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--kernel", choices=["mega", "wavefront"], default="mega")
     ap.add_argument("--scene-dir", default=os.environ.get("RT_SCENE_DIR", os.path.join(ROOT, "build", "scenes")))
     args = ap.parse_args()
 
@@ -119,7 +120,8 @@ def main():
     n = W * H
     gb = TorchGBuffer(torch, n, rank * n)
     stream = torch.cuda.current_stream()
-    opt = rt.options(W, H, P, adaptive=False, stream=ctypes.c_void_p(stream.cuda_stream))
+    kernel = rt.KERNEL_WAVEFRONT if args.kernel == "wavefront" else rt.KERNEL_MEGA
+    opt = rt.options(W, H, P, adaptive=False, stream=ctypes.c_void_p(stream.cuda_stream), kernel=kernel)
 
     def step(i):
         rt.render(dscene, gb, host.camera, 0 if i == 0 else 1, opt)
@@ -163,7 +165,7 @@ def main():
 
     # work counters on one extra (untimed) step -> algorithmic bytes per launch
     counters = rt.DeviceCounters()
-    copt = rt.options(W, H, P, adaptive=False, counters=counters.p)
+    copt = rt.options(W, H, P, adaptive=False, counters=counters.p, kernel=kernel)
     rt.render(dscene, gb, host.camera, 1, copt)
     c = counters.read()
     bytes_per_launch = algorithmic_bytes(c)
@@ -200,7 +202,7 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4),
             "traffic": None,
-            "kernel": "rt_path_kernel<false,19>",
+            "kernel": "rt_path_kernel<false,20>" if kernel == rt.KERNEL_MEGA else "wf_trace+wf_shade (per render call)",
             "kernel_ms": round(kernel_ms, 3),
             "algorithmic_bytes_per_launch": bytes_per_launch,
             "bytes_per_sample": round(bytes_per_launch / max(c["sample"], 1), 1),

@@ -232,8 +232,12 @@ enum {
     RT_CNT_SKIP = 6,   /* pixel-passes skipped by the adaptive test */
     RT_CNT_RAY = 7,    /* trace_ray calls */
     RT_CNT_WATCHDOG = 8, /* paths cut by the bounce watchdog */
+    RT_CNT_MAXDEPTH = 9, /* longest path (extension rays) seen: atomic max, not a sum */
     RT_CNT_COUNT = 16
 };
+
+#define RT_KERNEL_MEGA 0
+#define RT_KERNEL_WAVEFRONT 1
 
 typedef struct RtOptions {
     int width, height;   /* frame (rt/macros.h:3-4: 1920x1080) */
@@ -242,9 +246,10 @@ typedef struct RtOptions {
     int min_samples;     /* MIN_SAMPLES (rt/macros.h:13) */
     float tolerance;     /* MAX_TOLERANCE (rt/macros.h:17) */
     int max_depth;       /* 0 = unbounded (reference); else max extension rays per path */
-    int kernel;          /* kernel variant, 0 = default */
+    int kernel;          /* RT_KERNEL_MEGA (one launch) or RT_KERNEL_WAVEFRONT (trace/shade queues) */
     void *stream;        /* hipStream_t; NULL = synchronous on the null stream */
     unsigned long long *counters_device; /* optional RT_CNT_COUNT u64 counters (adds) */
+    unsigned long long *wave_times_device; /* optional debug: 2 u64 per wave (megakernel, with counters) */
 } RtOptions;
 
 void rt_default_options(RtOptions *opt);

@@ -20,8 +20,8 @@ ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
 HOST_SOURCES = ["host/mesh_loading.cpp", "host/kd_build.cpp", "host/scene_prepare.cpp", "host/misc.cpp",
                 "host/scenes.cpp"]
-HIP_SOURCES = ["path_kernel.hip", "abi.hip"]
-HEADERS = ["rt_libm.h", "rt_vecmath.h", "rt_device.h", "host/rt_host.h"]
+HIP_SOURCES = ["path_kernel.hip", "wavefront.hip", "abi.hip"]
+HEADERS = ["rt_libm.h", "rt_vecmath.h", "rt_device.h", "rt_kernels.h", "host/rt_host.h"]
 
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-I" + INCLUDE, "-I" + CSRC]
 HOST_FLAGS = ["-fopenmp", "-Wall", "-Wno-unused-function"]

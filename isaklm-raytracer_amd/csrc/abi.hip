@@ -18,6 +18,8 @@
 int rt_launch_path(const RtDevScene &sc, const RtDevFrame &fr, const RtDevCamera &cam, int stack_depth,
                    hipStream_t stream);
 int rt_launch_tonemap(const Vec3D *fb, const int *count, RtUChar4 *out, int n, hipStream_t stream);
+int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevCamera &cam, hipStream_t stream,
+                        int variant);
 
 static thread_local std::string g_error;
 
@@ -74,26 +76,25 @@ int upload_prepared(const rt_host::PreparedHost &h, int ntris, int nindices, rt_
     RtPreparedScene *s = new RtPreparedScene();
     int rc = RT_OK;
     const uint32_t *nodes = nullptr;
-    const int *leaf = nullptr, *lights = nullptr;
+    const int *lights = nullptr;
     const RtF4 *a = nullptr, *b = nullptr, *c = nullptr, *d = nullptr, *sh = nullptr;
-    const float *r = nullptr;
+    const uint32_t *rt = nullptr;
     const RtDevMaterial *mats = nullptr;
-    if ((rc = upload_vec(*s, h.nodes, &nodes)) || (rc = upload_vec(*s, h.leaf_tris, &leaf)) ||
-        (rc = upload_vec(*s, h.isect_a, &a)) || (rc = upload_vec(*s, h.isect_b, &b)) ||
-        (rc = upload_vec(*s, h.isect_c, &c)) || (rc = upload_vec(*s, h.isect_d, &d)) ||
-        (rc = upload_vec(*s, h.isect_r, &r)) || (rc = upload_vec(*s, h.shade, &sh)) ||
+    if ((rc = upload_vec(*s, h.nodes, &nodes)) || (rc = upload_vec(*s, h.isect_a, &a)) ||
+        (rc = upload_vec(*s, h.isect_b, &b)) || (rc = upload_vec(*s, h.isect_c, &c)) ||
+        (rc = upload_vec(*s, h.isect_d, &d)) || (rc = upload_vec(*s, h.isect_rt, &rt)) ||
+        (rc = upload_vec(*s, h.shade, &sh)) ||
         (rc = upload_vec(*s, h.materials, &mats)) || (rc = upload_vec(*s, h.lights, &lights))) {
         release(s);
         return rc;
     }
     RtDevScene &dv = s->dev;
     dv.nodes = nodes;
-    dv.leaf_tris = leaf;
     dv.isect_a = a;
     dv.isect_b = b;
     dv.isect_c = c;
     dv.isect_d = d;
-    dv.isect_r = r;
+    dv.isect_rt = rt;
     dv.shade = sh;
     dv.materials = mats;
     dv.lights = lights;
@@ -388,6 +389,7 @@ int rt_render(rt_scene_t scene, G_Buffer g, Camera cam, int sample_count, const 
     fr.max_depth = o.max_depth;
     fr.reset = sample_count == 0;
     fr.counters = o.counters_device;
+    fr.wave_times = o.wave_times_device;
 
     // Camera::rotation() and tanf(FOV / 2) are frame constants (rt/camera.cuh:22-25, :381)
     RtDevCamera dc;
@@ -400,7 +402,12 @@ int rt_render(rt_scene_t scene, G_Buffer g, Camera cam, int sample_count, const 
     dc.aperture = cam.aperture_radius;
 
     hipStream_t stream = (hipStream_t)o.stream;
-    if (rt_launch_path(scene->dev, fr, dc, scene->max_depth, stream) != 0) {
+    if (o.kernel == RT_KERNEL_WAVEFRONT || o.kernel == 2) {
+        if (scene->max_depth > RT_STACK_DEPTH || rt_launch_wavefront(scene->dev, fr, dc, stream, o.kernel) != 0) {
+            rt_set_error("rt_render: wavefront launch failed: %s", hipGetErrorString(hipGetLastError()));
+            return RT_E_HIP;
+        }
+    } else if (rt_launch_path(scene->dev, fr, dc, scene->max_depth, stream) != 0) {
         rt_set_error("rt_render: kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
         return RT_E_HIP;
     }

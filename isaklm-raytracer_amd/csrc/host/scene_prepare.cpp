@@ -95,7 +95,6 @@ int prepare_host(const Triangle *tris, int ntris, const KD_Tree_Node *nodes, int
             out.nodes[2 * k + 1] = ((uint32_t)new_id[n.child_index2] << 2) | (uint32_t)n.plane_axis;
         }
     }
-    out.leaf_tris.assign(indices, indices + nindices);
     for (int i = 0; i < nindices; ++i)
         if (indices[i] < 0 || indices[i] >= ntris) {
             rt_set_error("prepare: triangle index %d out of range", indices[i]);
@@ -128,12 +127,9 @@ int prepare_host(const Triangle *tris, int ntris, const KD_Tree_Node *nodes, int
         tri_mat[i] = it->second;
     }
 
-    // --- per-triangle constants (rt/trace_ray.cuh:48-113) -----------------
-    out.isect_a.resize((size_t)ntris);
-    out.isect_b.resize((size_t)ntris);
-    out.isect_c.resize((size_t)ntris);
-    out.isect_d.resize((size_t)ntris);
-    out.isect_r.resize((size_t)ntris);
+    // --- intersection constants (rt/trace_ray.cuh:48-113), per triangle ---
+    std::vector<RtF4> ta((size_t)ntris), tb((size_t)ntris), tc((size_t)ntris), td((size_t)ntris);
+    std::vector<float> tr((size_t)ntris);
     out.shade.resize(7 * (size_t)ntris);
 #pragma omp parallel for schedule(static)
     for (int i = 0; i < ntris; ++i) {
@@ -144,11 +140,11 @@ int prepare_host(const Triangle *tris, int ntris, const KD_Tree_Node *nodes, int
         float d = rt_dot(n, t.p1);
         float d00 = rt_dot(v0, v0), d01 = rt_dot(v0, v1), d11 = rt_dot(v1, v1);
         float rd = 1.0f / (d00 * d11 - d01 * d01);
-        out.isect_a[i] = f4(n.x, n.y, n.z, d);
-        out.isect_b[i] = f4(t.p1.x, t.p1.y, t.p1.z, d00);
-        out.isect_c[i] = f4(v0.x, v0.y, v0.z, d01);
-        out.isect_d[i] = f4(v1.x, v1.y, v1.z, d11);
-        out.isect_r[i] = rd;
+        ta[i] = f4(n.x, n.y, n.z, d);
+        tb[i] = f4(t.p1.x, t.p1.y, t.p1.z, d00);
+        tc[i] = f4(v0.x, v0.y, v0.z, d01);
+        td[i] = f4(v1.x, v1.y, v1.z, d11);
+        tr[i] = rd;
         RtF4 *s = &out.shade[7 * (size_t)i];
         s[0] = f4(t.p1.x, t.p1.y, t.p1.z, bitsf((uint32_t)tri_mat[i]));
         s[1] = f4(t.p2.x, t.p2.y, t.p2.z, t.uv1.x);
@@ -157,6 +153,23 @@ int prepare_host(const Triangle *tris, int ntris, const KD_Tree_Node *nodes, int
         s[4] = f4(t.n2.x, t.n2.y, t.n2.z, t.uv2.y);
         s[5] = f4(t.n3.x, t.n3.y, t.n3.z, t.uv3.x);
         s[6] = f4(t.uv3.y, 0.0f, 0.0f, 0.0f);
+    }
+    // ... gathered into leaf-entry order (a leaf's tests read consecutive memory)
+    const size_t ne = (size_t)(nindices > 0 ? nindices : 0);
+    out.isect_a.resize(ne);
+    out.isect_b.resize(ne);
+    out.isect_c.resize(ne);
+    out.isect_d.resize(ne);
+    out.isect_rt.resize(2 * ne);
+#pragma omp parallel for schedule(static)
+    for (long long e = 0; e < (long long)ne; ++e) {
+        const int t = indices[e];
+        out.isect_a[e] = ta[t];
+        out.isect_b[e] = tb[t];
+        out.isect_c[e] = tc[t];
+        out.isect_d[e] = td[t];
+        out.isect_rt[2 * e] = fbits(tr[t]);
+        out.isect_rt[2 * e + 1] = (uint32_t)t;
     }
 
     // --- lights: one padding entry for the xi == 1.0 draw -----

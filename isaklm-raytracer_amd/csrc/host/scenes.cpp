@@ -10,15 +10,18 @@
 //
 //   name          config (BASELINE.json)            triangles
 //   cornell       1: Cornell box, 256x256            36
-//   cornell_blob  2: + displaced sphere (gold)       36 + 50,176
-//   room2m        3/4: room + 2M displaced mesh       12+2 + 1,999,392 + 2 x 20,224 glass
+//   cornell_blob  2: + displaced sphere (gold)       36 + 50,700
+//   room2m        3/4: room + 2M displaced mesh       12+2 + 1,997,568 + 2 x 20,172 glass
 //                    (dragon.mat gold) + 2 glass spheres + emissive quad
 //   room2m_glass  5: as room2m, the big mesh glass with smooth normals
-//   room_small    test-size room (blob 20,224 tris) for fast parity tests
+//   room_small    test-size room (blob 20,172 tris) for fast parity tests
+// Meshes are displaced cube-spheres (12 n^2 near-uniform triangles).
 #include <stdio.h>
 #include <string.h>
 #include <sys/stat.h>
 
+#include <cmath>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -95,6 +98,50 @@ void block(Obj &o, double cx, double cy, double cz, double sx, double sy, double
     for (auto &q : f) o.quad(id[q[0]], id[q[1]], id[q[2]], id[q[3]]);
 }
 
+// displaced cube-sphere: the 6 faces of [-1,1]^3 cut into n x n quads, vertices
+// pushed onto the unit sphere and displaced radially; 12 n^2 triangles of
+// near-uniform size, shared vertices, no pole fans (a UV sphere's poles put
+// ~1,400 slivers in one KD leaf, nothing like a scanned model)
+void cube_blob(Obj &o, int n, double amp)
+{
+    std::map<long long, int> ids;
+    auto key = [&](int i, int j, int k) { return ((long long)i * (n + 1) + j) * (n + 1) + k; };
+    auto vert = [&](int i, int j, int k) {
+        auto it = ids.find(key(i, j, k));
+        if (it != ids.end()) return it->second;
+        double x = -1.0 + 2.0 * i / n, y = -1.0 + 2.0 * j / n, z = -1.0 + 2.0 * k / n;
+        double len = sqrt(x * x + y * y + z * z);
+        x /= len; y /= len; z /= len;
+        double r = 1.0 + amp * (0.10 * rt_sin_d(3.1 * x + 1.7) * rt_cos_d(2.3 * y - 0.4) +
+                                0.05 * rt_sin_d(9.7 * y + 0.3) * rt_sin_d(8.9 * z + 1.1) +
+                                0.02 * rt_cos_d(27.1 * z - 0.2) * rt_sin_d(23.3 * x + 0.9));
+        int id = o.v(r * x, r * y, r * z);
+        ids.emplace(key(i, j, k), id);
+        return id;
+    };
+    // each face: fixed axis a at value s (0 or n), the other two axes u, v
+    for (int a = 0; a < 3; ++a) {
+        for (int side = 0; side < 2; ++side) {
+            const int s = side ? n : 0;
+            for (int u = 0; u < n; ++u) {
+                for (int v = 0; v < n; ++v) {
+                    int c[4][3];
+                    const int uu[4] = {u, u + 1, u + 1, u}, vv[4] = {v, v, v + 1, v + 1};
+                    for (int q = 0; q < 4; ++q) {
+                        c[q][a] = s;
+                        c[q][(a + 1) % 3] = uu[q];
+                        c[q][(a + 2) % 3] = vv[q];
+                    }
+                    int id[4];
+                    for (int q = 0; q < 4; ++q) id[q] = vert(c[q][0], c[q][1], c[q][2]);
+                    if (side) o.quad(id[0], id[1], id[2], id[3]);
+                    else o.quad(id[0], id[3], id[2], id[1]);
+                }
+            }
+        }
+    }
+}
+
 // displaced UV sphere: 2*slices*(stacks-1) triangles, unit radius before displacement
 void blob(Obj &o, int slices, int stacks, double amp)
 {
@@ -163,12 +210,12 @@ std::string room_obj()
     return o.text;
 }
 
-std::string blob_obj(const char *mat, int slices, int stacks, double amp)
+std::string blob_obj(const char *mat, int n, double amp)
 {
     Obj o;
-    o.text.reserve((size_t)slices * stacks * 80);
+    o.text.reserve((size_t)n * n * 6 * 80);
     o.use(mat);
-    blob(o, slices, stacks, amp);
+    cube_blob(o, n, amp);
     return o.text;
 }
 
@@ -194,7 +241,7 @@ extern "C" int rt_generate_scene(const char *name, const char *out_dir, char *sc
         scene = "# BASELINE config " + std::string(n == "cornell" ? "1" : "2") + "\n"
                 "mesh cornell.obj cornell.mat 0 1 0 0.1 0 1 0\n";
         if (n == "cornell_blob") {
-            files.push_back({"blob50k.obj", blob_obj("dragon", 224, 113, 1.0)});
+            files.push_back({"blob50k.obj", blob_obj("dragon", 65, 1.0)});
             files.push_back({"dragon.mat", kDragonMat});
             scene += "mesh blob50k.obj dragon.mat 0.27 0.93 -0.33 2.1 0 0.33 0\n";
         }
@@ -207,9 +254,9 @@ extern "C" int rt_generate_scene(const char *name, const char *out_dir, char *sc
         files.push_back({"dragon.mat", kDragonMat});
         files.push_back({"glass.mat", kGlassMat});
         const char *blob_name = big ? "blob2m.obj" : "blob20k.obj";
-        files.push_back({blob_name, big ? blob_obj(glass ? "glass" : "dragon", 1416, 707, 1.0)
-                                        : blob_obj("dragon", 128, 80, 1.0)});
-        files.push_back({"glass_sphere.obj", blob_obj("glass", 128, 80, 0.0)});
+        files.push_back({blob_name, big ? blob_obj(glass ? "glass" : "dragon", 408, 1.0)
+                                        : blob_obj("dragon", 41, 1.0)});
+        files.push_back({"glass_sphere.obj", blob_obj("glass", 41, 0.0)});
         scene = "# BASELINE config " + std::string(glass ? "5" : (big ? "3/4" : "test")) + "\n";
         scene += "mesh room.obj room.mat 0 1.5 0 0.1 0 1 0\n";
         scene += std::string("mesh ") + blob_name + (glass ? " glass.mat" : " dragon.mat") +

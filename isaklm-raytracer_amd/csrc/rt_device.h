@@ -8,13 +8,15 @@
 //  * nodes: 8 B each, pre-order, child1 == node+1 implicit
 //      inner:  x = plane_offset bits, y = (child2 << 2) | axis      (axis 0..2)
 //      leaf:   x = index_offset,      y = (triangle_count << 2) | 3
-//  * per-triangle intersection constants, SoA float4 streams indexed by the
-//    triangle id, each value the reference's own expression evaluated once:
-//      isect_a = {n.x, n.y, n.z, d}        n = normalize(cross(p2-p1, p3-p1)), d = dot(n, p1)
-//      isect_b = {p1.x, p1.y, p1.z, d00}
-//      isect_c = {v0.x, v0.y, v0.z, d01}   v0 = p2-p1
-//      isect_d = {v1.x, v1.y, v1.z, d11}   v1 = p3-p1
-//      isect_r = 1/(d00*d11 - d01*d01)
+//  * intersection constants in LEAF-ENTRY order (entry e = position in the
+//    KD triangle_indicies array, so a leaf's tests read consecutive memory
+//    and need no index load first), SoA float4 streams, each value the
+//    reference's own expression evaluated once:
+//      isect_a  = {n.x, n.y, n.z, d}      n = normalize(cross(p2-p1, p3-p1)), d = dot(n, p1)
+//      isect_b  = {p1.x, p1.y, p1.z, d00}
+//      isect_c  = {v0.x, v0.y, v0.z, d01} v0 = p2-p1
+//      isect_d  = {v1.x, v1.y, v1.z, d11} v1 = p3-p1
+//      isect_rt = {bits(1/(d00*d11 - d01*d01)), triangle index}
 //    A test that is rejected by the plane (dn == 0, s < 1e-5, s >= closest)
 //    reads only isect_a (16 B).
 //  * shading record (hit only), 7 float4 per triangle: p1..p3, n1..n3,
@@ -24,7 +26,13 @@
 
 #include "../../include/isaklm_rt.h"
 
-#define RT_STACK_DEPTH 24       // traversal stack entries (reference: KD_TREE_DEPTH = 19)
+// Traversal stack entries.  The reference declares KD_TREE_DEPTH = 19 entries
+// (rt/trace_ray.cuh:246-248) but its builder makes inner nodes at depths
+// 0..19 (rt/create_kd_tree.cuh:225,246: split while depth < 19), i.e. up to
+// 20 nested pushes: a latent overflow in the reference.  The kernel is built
+// for 20 (every create_kd_tree tree) and 32 (other trees).
+#define RT_STACK_SMALL 20
+#define RT_STACK_DEPTH 32
 #define RT_LEAF_TAG 3u
 #define RT_WATCHDOG_BOUNCES 65536 // SURVEY H8; never reached by a parity config
 
@@ -45,9 +53,8 @@ struct RtF4 { float x, y, z, w; };
 
 struct RtDevScene {
     const uint32_t *nodes;      // 2 words per node
-    const int *leaf_tris;       // KD triangle_indicies
-    const RtF4 *isect_a, *isect_b, *isect_c, *isect_d;
-    const float *isect_r;
+    const RtF4 *isect_a, *isect_b, *isect_c, *isect_d; // per leaf entry
+    const uint32_t *isect_rt;   // 2 words per leaf entry: rd bits, triangle index
     const RtF4 *shade;          // 7 per triangle
     const RtDevMaterial *materials;
     const int *lights;          // light_count + 1 entries (SURVEY H4 padding)
@@ -77,4 +84,5 @@ struct RtDevFrame {
     int max_depth;              // 0 = unbounded (watchdog)
     int reset;                  // sample_count == 0
     unsigned long long *counters;
+    unsigned long long *wave_times; // debug: per-wave s_memrealtime [start, end] (counting variant)
 };

@@ -1,0 +1,526 @@
+// wavefront.hip — the wavefront variant of the render hot path (kernel 1).
+//
+// The per-pixel loop of rt/path_tracing.cuh:268-325 is cut at its ray
+// queries.  Each iteration runs two kernels over a compacted queue of rays:
+//   wf_trace  — trace_ray (rt/trace_ray.cuh:244-318) for every queued ray;
+//               nothing else, so it is small (VGPRs) and keeps more waves in
+//               flight to hide the dependent node/triangle loads
+//   wf_shade  — consumes each hit: emission, BSDF sample, NEE shadow-ray set
+//               up, roulette, accumulation, and starts the pixel's next pass
+//               (adaptive test + camera ray) when its path ends; appends the
+//               next ray of every live path to the other queue
+// Path state lives in HBM between kernels (SoA, ~72 B per pixel).  Queue
+// order is arbitrary (wave-aggregated atomics) but every pixel's sequence of
+// events is the reference's, so results are bit-identical to the megakernel
+// and the CPU oracle.
+#include <hip/hip_runtime.h>
+
+#include <map>
+
+#include "rt_kernels.h"
+
+using namespace rtk;
+
+#define WF_BLOCK 256
+#define WF_LDS_STACK 8  // stack entries in LDS; deeper ones spill to HBM (rare)
+
+struct WfState {
+    int *passes_left;
+    uint32_t *flags;   // bit0 shadow, bit1 inside, bits 2..4 prev_type, bits 8.. depth
+    Vec3D *T, *L, *cont, *snorm, *rp;
+    int *light;
+    uint32_t *q_slot[2];
+    RtF4 *q_ray[2];    // 2 per entry: {o.xyz, -}, {d.xyz, -}
+    RtF4 *hits;        // per queue entry: {tri bits, bx, by, bz}
+    uint32_t *counts;  // [0], [1]: queue sizes
+    uint2 *spill;      // traversal stack spill
+    int spill_threads;
+};
+
+namespace {
+
+__device__ __forceinline__ uint32_t lanemask_lt() { return (uint32_t)__lane_id(); }
+
+// append `want` lanes' rays to queue q (wave-aggregated atomic)
+__device__ __forceinline__ void enqueue(const WfState &st, int q, bool want, uint32_t slot, Vec3D o, Vec3D d)
+{
+    const unsigned long long mask = __ballot(want);
+    if (mask == 0) return;
+    const int lane = __lane_id();
+    const int leader = __ffsll((long long)mask) - 1;
+    const int rank = __popcll(mask & ((1ull << lane) - 1ull));
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(st.counts + q, (uint32_t)__popcll(mask));
+    base = __shfl(base, leader);
+    if (want) {
+        const uint32_t e = base + (uint32_t)rank;
+        st.q_slot[q][e] = slot;
+        st.q_ray[q][2 * (size_t)e] = RtF4{o.x, o.y, o.z, 0.0f};
+        st.q_ray[q][2 * (size_t)e + 1] = RtF4{d.x, d.y, d.z, 0.0f};
+    }
+}
+
+// start the pixel's next pass(es): adaptive test, camera ray.  Returns true
+// (and the ray) when a sample starts.
+template <bool COUNT>
+__device__ __forceinline__ bool start_sample(const RtDevFrame &fr, const RtDevCamera &cam, int slot, int &passes_left,
+                                             uint32_t &rng, Vec3D fb, float sq, int count, Vec3D &ro, Vec3D &rd,
+                                             Cnt &c)
+{
+    while (passes_left > 0) {
+        --passes_left;
+        if (!adaptive_run(fr, fb, sq, count)) {
+            if (COUNT) c.v[RT_CNT_SKIP]++;
+            continue;
+        }
+        camera_ray(fr, cam, slot % fr.width, slot / fr.width, rng, ro, rd);
+        if (COUNT) c.v[RT_CNT_SAMPLE]++;
+        return true;
+    }
+    return false;
+}
+
+} // namespace
+
+template <bool COUNT>
+__global__ void __launch_bounds__(WF_BLOCK) wf_start(RtDevFrame fr, RtDevCamera cam, WfState st)
+{
+    Cnt c;
+    if (COUNT) c.zero();
+    const int n = fr.width * fr.height;
+    const int tile = xcd_tile(blockIdx.x, gridDim.x);
+    const int tiles_x = (fr.width + 15) / 16;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int x = (tile % tiles_x) * 16 + (wave & 1) * 8 + (lane & 7);
+    const int y = (tile / tiles_x) * 16 + (wave >> 1) * 8 + (lane >> 3);
+    const bool valid = x < fr.width && y < fr.height;
+    const int slot = valid ? y * fr.width + x : 0;
+    bool want = false;
+    Vec3D ro = rt_v3(0, 0, 0), rd = rt_v3(0, 0, 0);
+    if (valid && slot < n) {
+        Vec3D fb = rt_v3(0.0f, 0.0f, 0.0f);
+        float sq = 0.0f;
+        int count = 0;
+        if (fr.reset) {
+            fr.fb[slot] = fb;
+            fr.sq[slot] = sq;
+            fr.count[slot] = count;
+        } else {
+            fb = fr.fb[slot];
+            sq = fr.sq[slot];
+            count = fr.count[slot];
+        }
+        int passes_left = fr.passes;
+        uint32_t rng = fr.rng[slot];
+        want = start_sample<COUNT>(fr, cam, slot, passes_left, rng, fb, sq, count, ro, rd, c);
+        fr.rng[slot] = rng;
+        st.passes_left[slot] = passes_left;
+        st.flags[slot] = 1u << 8; // depth 1 (first extension ray), prev PRIMARY
+        st.T[slot] = rt_v3(1.0f, 1.0f, 1.0f);
+        st.L[slot] = rt_v3(0.0f, 0.0f, 0.0f);
+    }
+    enqueue(st, 0, want, (uint32_t)slot, ro, rd);
+    if (COUNT) flush_counters(c, fr.counters);
+}
+
+template <bool COUNT>
+__global__ void __launch_bounds__(WF_BLOCK) wf_trace(RtDevScene sc, WfState st, int q, unsigned long long *counters)
+{
+    __shared__ uint32_t s_node[WF_LDS_STACK * WF_BLOCK];
+    __shared__ float s_entry[WF_LDS_STACK * WF_BLOCK];
+    const int tid = threadIdx.x;
+    const int gtid = blockIdx.x * WF_BLOCK + tid;
+    Stack<WF_LDS_STACK> stk{s_node + tid, s_entry + tid, WF_BLOCK, st.spill + gtid, st.spill_threads};
+    Cnt c;
+    if (COUNT) c.zero();
+    const uint32_t n = st.counts[q];
+    const RtF4 *rays = st.q_ray[q];
+    for (uint32_t base = blockIdx.x * WF_BLOCK; base < n; base += gridDim.x * WF_BLOCK) {
+        const uint32_t e = base + tid;
+        if (e < n) {
+            const RtF4 o4 = ldf4(rays + 2 * (size_t)e), d4 = ldf4(rays + 2 * (size_t)e + 1);
+            float bx = 0.0f, by = 0.0f, bz = 0.0f;
+            const int hit = trace<COUNT>(sc, ld3(o4), ld3(d4), bx, by, bz, stk, c);
+            *reinterpret_cast<float4 *>(st.hits + e) = make_float4(__int_as_float(hit), bx, by, bz);
+        }
+    }
+    if (COUNT) flush_counters(c, counters);
+}
+
+// Persistent trace with dynamic ray fetch: every lane runs rays one leaf at a
+// time; a lane whose ray is done writes its hit and takes the next queued ray
+// at the next leaf boundary (one wave-aggregated atomic), so a wave is never
+// held by its slowest ray.  Same per-ray arithmetic as trace().
+template <bool COUNT>
+__global__ void __launch_bounds__(WF_BLOCK) wf_trace_dyn(RtDevScene sc, WfState st, int q,
+                                                         unsigned long long *counters)
+{
+    __shared__ uint32_t s_node[WF_LDS_STACK * WF_BLOCK];
+    __shared__ float s_entry[WF_LDS_STACK * WF_BLOCK];
+    const int tid = threadIdx.x;
+    const int gtid = blockIdx.x * WF_BLOCK + tid;
+    Stack<WF_LDS_STACK> stk{s_node + tid, s_entry + tid, WF_BLOCK, st.spill + gtid, st.spill_threads};
+    Cnt c;
+    if (COUNT) c.zero();
+    const uint32_t n = st.counts[q];
+    const RtF4 *rays = st.q_ray[q];
+    uint32_t *fetch = st.counts + 2 + q;
+    const int lane = __lane_id();
+
+    bool live = false, exhausted = false;
+    uint32_t e = 0, node = 0;
+    int sp = 0;
+    Vec3D o = rt_v3(0, 0, 0), d = rt_v3(0, 0, 0);
+    float entry = 0.0f, exit_ = 0.0f, root_exit = 0.0f;
+    while (true) {
+        // ---- refill idle lanes
+        const bool need = !live && !exhausted;
+        const unsigned long long m = __ballot(need);
+        if (m) {
+            const int leader = __ffsll((long long)m) - 1;
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(fetch, (uint32_t)__popcll(m));
+            base = __shfl(base, leader);
+            if (need) {
+                e = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+                if (e >= n) {
+                    exhausted = true;
+                } else {
+                    o = ld3(ldf4(rays + 2 * (size_t)e));
+                    d = ld3(ldf4(rays + 2 * (size_t)e + 1));
+                    if (COUNT) c.v[RT_CNT_RAY]++;
+                    if (bbox_hit(sc, o, d, entry, exit_)) {
+                        root_exit = exit_;
+                        node = 0;
+                        sp = 0;
+                        live = true;
+                    } else {
+                        *reinterpret_cast<float4 *>(st.hits + e) = make_float4(__int_as_float(-1), 0.f, 0.f, 0.f);
+                    }
+                }
+            }
+        }
+        if (!__any(live)) {
+            if (__all(exhausted)) break;
+            continue;
+        }
+        if (!live) continue;
+        // ---- descend to a leaf (rt/trace_ray.cuh:273-306)
+        uint2 nd = *reinterpret_cast<const uint2 *>(sc.nodes + 2 * (size_t)node);
+        if (COUNT) c.v[RT_CNT_NODE]++;
+        while ((nd.y & 3u) != RT_LEAF_TAG) {
+            const uint32_t axis = nd.y & 3u;
+            const float split = as_float(nd.x);
+            const float oax = axis == 0 ? o.x : (axis == 1 ? o.y : o.z);
+            const float dax = axis == 0 ? d.x : (axis == 1 ? d.y : d.z);
+            uint32_t near_c = node + 1, far_c = nd.y >> 2;
+            if (oax >= split) {
+                near_c = nd.y >> 2;
+                far_c = node + 1;
+            }
+            const float t = (split - oax) / dax;
+            if (t >= exit_ || t < 0) {
+                node = near_c;
+            } else if (t <= entry) {
+                node = far_c;
+            } else {
+                stk.put(sp, far_c, t);
+                ++sp;
+                node = near_c;
+                exit_ = t;
+            }
+            nd = *reinterpret_cast<const uint2 *>(sc.nodes + 2 * (size_t)node);
+            if (COUNT) c.v[RT_CNT_NODE]++;
+        }
+        // ---- leaf (rt/trace_ray.cuh:115-172)
+        const int count = (int)(nd.y >> 2);
+        int best = -1;
+        float bx = 0.0f, by = 0.0f, bz = 0.0f;
+        if (count > 0) {
+            const uint32_t e0 = nd.x, e1 = nd.x + (uint32_t)count;
+            float smallest = exit_;
+            for (uint32_t k = e0; k < e1; k += 2) {
+                const bool two = k + 1 < e1;
+                if (COUNT) c.v[RT_CNT_TRI] += two ? 2 : 1;
+                const RtF4 A0 = ldf4(sc.isect_a + k);
+                const RtF4 A1 = ldf4(sc.isect_a + (two ? k + 1 : k));
+                const float dn0 = d.x * A0.x + d.y * A0.y + d.z * A0.z;
+                const float dn1 = d.x * A1.x + d.y * A1.y + d.z * A1.z;
+                const float s0 = (A0.w - (o.x * A0.x + o.y * A0.y + o.z * A0.z)) / dn0;
+                const float s1 = (A1.w - (o.x * A1.x + o.y * A1.y + o.z * A1.z)) / dn1;
+                const bool p0 = dn0 != 0 && s0 >= 0.00001f && s0 < smallest;
+                const bool p1 = two && dn1 != 0 && s1 >= 0.00001f && s1 < smallest;
+                RtF4 B0, C0, D0, B1, C1, D1;
+                uint2 R0, R1;
+                if (p0) {
+                    B0 = ldf4(sc.isect_b + k);
+                    C0 = ldf4(sc.isect_c + k);
+                    D0 = ldf4(sc.isect_d + k);
+                    R0 = *reinterpret_cast<const uint2 *>(sc.isect_rt + 2 * (size_t)k);
+                }
+                if (p1) {
+                    B1 = ldf4(sc.isect_b + k + 1);
+                    C1 = ldf4(sc.isect_c + k + 1);
+                    D1 = ldf4(sc.isect_d + k + 1);
+                    R1 = *reinterpret_cast<const uint2 *>(sc.isect_rt + 2 * (size_t)(k + 1));
+                }
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const bool p = j == 0 ? p0 : p1;
+                    const float s = j == 0 ? s0 : s1;
+                    if (!p || !(s < smallest)) continue;
+                    const RtF4 B = j == 0 ? B0 : B1, C = j == 0 ? C0 : C1, D = j == 0 ? D0 : D1;
+                    const uint2 R = j == 0 ? R0 : R1;
+                    const float rd = as_float(R.x);
+                    const float px = o.x + d.x * s, py = o.y + d.y * s, pz = o.z + d.z * s;
+                    const float v2x = px - B.x, v2y = py - B.y, v2z = pz - B.z;
+                    const float d20 = v2x * C.x + v2y * C.y + v2z * C.z;
+                    const float d21 = v2x * D.x + v2y * D.y + v2z * D.z;
+                    const float cy = (D.w * d20 - C.w * d21) * rd;
+                    const float cz = (B.w * d21 - C.w * d20) * rd;
+                    const float cx = 1.0f - cy - cz;
+                    if (cx >= 0.0f && cx <= 1.0f && cy >= 0.0f && cy <= 1.0f && cz >= 0.0f && cz <= 1.0f) {
+                        smallest = s;
+                        best = (int)R.y;
+                        bx = cx;
+                        by = cy;
+                        bz = cz;
+                    }
+                }
+            }
+        }
+        if (best >= 0) {
+            if (COUNT) c.v[RT_CNT_HIT]++;
+            *reinterpret_cast<float4 *>(st.hits + e) = make_float4(__int_as_float(best), bx, by, bz);
+            live = false;
+        } else if (sp == 0) {
+            *reinterpret_cast<float4 *>(st.hits + e) = make_float4(__int_as_float(-1), 0.f, 0.f, 0.f);
+            live = false;
+        } else {
+            --sp;
+            node = stk.node_at(sp);
+            entry = stk.entry_at(sp);
+            exit_ = sp > 0 ? stk.entry_at(sp - 1) : root_exit;
+        }
+    }
+    if (COUNT) flush_counters(c, counters);
+}
+
+template <bool COUNT>
+__global__ void __launch_bounds__(WF_BLOCK) wf_shade(RtDevScene sc, RtDevFrame fr, RtDevCamera cam, WfState st, int q)
+{
+    Cnt c;
+    if (COUNT) c.zero();
+    const uint32_t n = st.counts[q];
+    const int qn = q ^ 1;
+    const int limit = fr.max_depth > 0 ? fr.max_depth : RT_WATCHDOG_BOUNCES;
+    for (uint32_t base = blockIdx.x * WF_BLOCK; base < n; base += gridDim.x * WF_BLOCK) {
+        const uint32_t e = base + threadIdx.x;
+        bool want = false;
+        uint32_t slot = 0;
+        Vec3D ro = rt_v3(0, 0, 0), rd = rt_v3(0, 0, 0);
+        if (e < n) {
+            slot = st.q_slot[q][e];
+            const RtF4 h = ldf4(st.hits + e);
+            const int hit = __float_as_int(h.x);
+            const float bx = h.y, by = h.z, bz = h.w;
+            ro = ld3(ldf4(st.q_ray[q] + 2 * (size_t)e));
+            rd = ld3(ldf4(st.q_ray[q] + 2 * (size_t)e + 1));
+            uint32_t flags = st.flags[slot];
+            bool shadow = flags & 1u;
+            bool inside = (flags >> 1) & 1u;
+            int prev_type = (int)((flags >> 2) & 7u);
+            int depth = (int)(flags >> 8);
+            uint32_t rng = fr.rng[slot];
+            Vec3D T = st.T[slot], L = st.L[slot];
+            bool finish = false, roulette = true;
+            if (!shadow) {
+                if (hit < 0) {
+                    finish = true; // miss: break without roulette (:303-306)
+                    roulette = false;
+                } else {
+                    Surface s;
+                    shade<COUNT>(sc, hit, bx, by, bz, rd, s, c);
+                    if (prev_type != DIFFUSE) L = L + s.emittance * T; // :285-288
+                    Vec3D nd, w;
+                    prev_type = scatter(rd, inside, rng, s, nd, w);
+                    T = T * w;
+                    ro = s.position;
+                    rd = nd;
+                    if (prev_type == DIFFUSE) { // sample_direct_light (:235-265)
+                        if (COUNT) c.v[RT_CNT_NEE]++;
+                        float xi = rng_next(rng);
+                        if (sc.light_count == 0) {
+                            rng_next(rng);
+                            rng_next(rng);
+                            L = L + rt_v3(0.0f, 0.0f, 0.0f) * T;
+                        } else {
+                            const int light = sc.lights[(int)(xi * (float)sc.light_count)];
+                            const Vec3D rp = light_point(sc, light, rng);
+                            st.light[slot] = light;
+                            st.rp[slot] = rp;
+                            st.cont[slot] = rd;
+                            st.snorm[slot] = s.normal;
+                            rd = rt_normalize(rp - ro);
+                            shadow = true;
+                            roulette = false; // roulette after the shadow ray
+                            want = true;
+                        }
+                    }
+                }
+            } else {
+                const int light = st.light[slot];
+                Vec3D direct = rt_v3(0.0f, 0.0f, 0.0f);
+                if (hit >= 0 && hit == light)
+                    direct = light_contribution(sc, light, bx, by, bz, ro, rd, st.rp[slot], st.snorm[slot]);
+                if (COUNT && hit >= 0 && material_of(sc, hit).tex) c.v[RT_CNT_TEXEL] += 2; // every hit is shaded
+                L = L + direct * T;
+                rd = st.cont[slot];
+                shadow = false;
+            }
+            if (roulette) { // Russian roulette (:309-318)
+                float p = fmaxf(T.x, fmaxf(T.y, T.z));
+                float r = rng_next(rng);
+                if (r > p) {
+                    finish = true;
+                } else {
+                    T = T * (1.0f / p);
+                    if (depth == limit) { // max_depth / watchdog before the next extension ray
+                        if (COUNT && fr.max_depth <= 0) c.v[RT_CNT_WATCHDOG]++;
+                        finish = true;
+                    } else {
+                        ++depth;
+                        want = true;
+                    }
+                }
+            }
+            if (finish) { // accumulation (:322-324), then the pixel's next pass
+                if (COUNT) c.path_end(depth);
+                Vec3D fb = fr.fb[slot] + L;
+                float sq = fr.sq[slot] + rt_square(rt_luminance(L));
+                int count = fr.count[slot] + 1;
+                fr.fb[slot] = fb;
+                fr.sq[slot] = sq;
+                fr.count[slot] = count;
+                int passes_left = st.passes_left[slot];
+                if (passes_left > 0) {
+                    want = start_sample<COUNT>(fr, cam, (int)slot, passes_left, rng, fb, sq, count, ro, rd, c);
+                    st.passes_left[slot] = passes_left;
+                    if (want) {
+                        T = rt_v3(1.0f, 1.0f, 1.0f);
+                        L = rt_v3(0.0f, 0.0f, 0.0f);
+                        inside = false;
+                        prev_type = PRIMARY;
+                        depth = 1;
+                        shadow = false;
+                    }
+                }
+            }
+            fr.rng[slot] = rng;
+            st.T[slot] = T;
+            st.L[slot] = L;
+            st.flags[slot] = (shadow ? 1u : 0u) | (inside ? 2u : 0u) | ((uint32_t)prev_type << 2) |
+                             ((uint32_t)depth << 8);
+        }
+        enqueue(st, qn, want, slot, ro, rd);
+    }
+    if (COUNT) flush_counters(c, fr.counters);
+}
+
+// ---------------------------------------------------------------- launcher
+namespace {
+
+struct Workspace {
+    size_t slots = 0;
+    int grid = 0;
+    WfState st{};
+    void *blob = nullptr;
+    uint32_t *host_count = nullptr;
+};
+
+std::map<int, Workspace> g_ws; // per device
+
+int ensure(Workspace &w, size_t slots, int grid)
+{
+    if (w.slots >= slots && w.grid >= grid) return 0;
+    if (w.blob) (void)hipFree(w.blob);
+    if (!w.host_count && hipHostMalloc((void **)&w.host_count, 64) != hipSuccess) return -1;
+    const size_t spill_threads = (size_t)grid * WF_BLOCK;
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        size_t o = off;
+        off += (bytes + 255) & ~(size_t)255;
+        return o;
+    };
+    const size_t o_pl = take(slots * 4), o_fl = take(slots * 4), o_T = take(slots * 12), o_L = take(slots * 12),
+                 o_c = take(slots * 12), o_n = take(slots * 12), o_rp = take(slots * 12), o_li = take(slots * 4),
+                 o_qs0 = take(slots * 4), o_qs1 = take(slots * 4), o_qr0 = take(slots * 32),
+                 o_qr1 = take(slots * 32), o_h = take(slots * 16), o_cnt = take(64),
+                 o_sp = take(spill_threads * 8 * (RT_STACK_DEPTH - WF_LDS_STACK));
+    if (hipMalloc(&w.blob, off) != hipSuccess) {
+        w.blob = nullptr;
+        return -1;
+    }
+    char *b = (char *)w.blob;
+    w.st.passes_left = (int *)(b + o_pl);
+    w.st.flags = (uint32_t *)(b + o_fl);
+    w.st.T = (Vec3D *)(b + o_T);
+    w.st.L = (Vec3D *)(b + o_L);
+    w.st.cont = (Vec3D *)(b + o_c);
+    w.st.snorm = (Vec3D *)(b + o_n);
+    w.st.rp = (Vec3D *)(b + o_rp);
+    w.st.light = (int *)(b + o_li);
+    w.st.q_slot[0] = (uint32_t *)(b + o_qs0);
+    w.st.q_slot[1] = (uint32_t *)(b + o_qs1);
+    w.st.q_ray[0] = (RtF4 *)(b + o_qr0);
+    w.st.q_ray[1] = (RtF4 *)(b + o_qr1);
+    w.st.hits = (RtF4 *)(b + o_h);
+    w.st.counts = (uint32_t *)(b + o_cnt);
+    w.st.spill = (uint2 *)(b + o_sp);
+    w.st.spill_threads = (int)spill_threads;
+    w.slots = slots;
+    w.grid = grid;
+    return 0;
+}
+
+} // namespace
+
+int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevCamera &cam, hipStream_t stream,
+                        int variant)
+{
+    const bool dyn = variant != 2;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return -1;
+    Workspace &w = g_ws[dev];
+    const int grid = 2048; // persistent-ish grid for trace/shade (grid-stride over the queue)
+    const size_t slots = (size_t)fr.width * fr.height;
+    if (ensure(w, slots, grid) != 0) return -1;
+    const bool count = fr.counters != nullptr;
+    if (hipMemsetAsync(w.st.counts, 0, 64, stream) != hipSuccess) return -1;
+    const int tiles = ((fr.width + 15) / 16) * ((fr.height + 15) / 16);
+    if (count) hipLaunchKernelGGL(wf_start<true>, dim3(tiles), dim3(WF_BLOCK), 0, stream, fr, cam, w.st);
+    else hipLaunchKernelGGL(wf_start<false>, dim3(tiles), dim3(WF_BLOCK), 0, stream, fr, cam, w.st);
+    const int check_every = 8;
+    for (int it = 0;; ++it) {
+        const int q = it & 1;
+        if (hipMemsetAsync(w.st.counts + (q ^ 1), 0, 4, stream) != hipSuccess) return -1;
+        if (hipMemsetAsync(w.st.counts + 2 + q, 0, 4, stream) != hipSuccess) return -1; // fetch cursor
+        if (count) {
+            if (dyn) hipLaunchKernelGGL(wf_trace_dyn<true>, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, w.st, q, fr.counters);
+            else hipLaunchKernelGGL(wf_trace<true>, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, w.st, q, fr.counters);
+            hipLaunchKernelGGL(wf_shade<true>, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, fr, cam, w.st, q);
+        } else {
+            if (dyn) hipLaunchKernelGGL(wf_trace_dyn<false>, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, w.st, q, fr.counters);
+            else hipLaunchKernelGGL(wf_trace<false>, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, w.st, q, fr.counters);
+            hipLaunchKernelGGL(wf_shade<false>, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, fr, cam, w.st, q);
+        }
+        if (hipGetLastError() != hipSuccess) return -1;
+        if (it % check_every == check_every - 1) {
+            if (hipMemcpyAsync(w.host_count, w.st.counts + (q ^ 1), 4, hipMemcpyDeviceToHost, stream) != hipSuccess)
+                return -1;
+            if (hipStreamSynchronize(stream) != hipSuccess) return -1;
+            if (*w.host_count == 0) break;
+        }
+    }
+    return 0;
+}

@@ -50,12 +50,12 @@ class RtOptions(ctypes.Structure):
     _fields_ = [("width", ctypes.c_int), ("height", ctypes.c_int), ("passes", ctypes.c_int),
                 ("adaptive", ctypes.c_int), ("min_samples", ctypes.c_int), ("tolerance", ctypes.c_float),
                 ("max_depth", ctypes.c_int), ("kernel", ctypes.c_int), ("stream", ctypes.c_void_p),
-                ("counters_device", ctypes.c_void_p)]
+                ("counters_device", ctypes.c_void_p), ("wave_times_device", ctypes.c_void_p)]
 
 
 TRIANGLE_BYTES = 152
 NODE_BYTES = 20
-COUNTER_NAMES = ["node", "tri", "hit", "texel", "nee", "sample", "skip", "ray", "watchdog"]
+COUNTER_NAMES = ["node", "tri", "hit", "texel", "nee", "sample", "skip", "ray", "watchdog", "maxdepth"]
 N_COUNTERS = 16
 
 _lib = None
@@ -263,12 +263,17 @@ class GBuffer:
             pass
 
 
+KERNEL_MEGA = 0
+KERNEL_WAVEFRONT = 1
+
+
 def options(width, height, passes=1, adaptive=True, min_samples=100, tolerance=0.05, max_depth=0, stream=None,
-            counters=None):
+            counters=None, kernel=KERNEL_MEGA):
     o = RtOptions()
     lib().rt_default_options(ctypes.byref(o))
     o.width, o.height, o.passes = width, height, passes
     o.adaptive, o.min_samples, o.tolerance, o.max_depth = int(adaptive), min_samples, tolerance, max_depth
+    o.kernel = kernel
     o.stream = stream
     o.counters_device = counters
     return o

@@ -47,7 +47,7 @@ const char *or_last_error(void) { return g_err; }
 #define TAUF (PIF * 2)                   /* rt/math_library.cuh:10 */
 #define WATCHDOG_BOUNCES 65536           /* never fires in parity configs */
 
-enum { CNT_NODE = 0, CNT_TRI, CNT_HIT, CNT_TEXEL, CNT_NEE, CNT_SAMPLE, CNT_SKIP, CNT_RAY, CNT_WATCHDOG };
+enum { CNT_NODE = 0, CNT_TRI, CNT_HIT, CNT_TEXEL, CNT_NEE, CNT_SAMPLE, CNT_SKIP, CNT_RAY, CNT_WATCHDOG, CNT_MAXDEPTH };
 
 /* ------------------------------------------------ types (rt/scene.cuh etc.) */
 typedef struct { float x, y; } V2;                     /* rt/math_library.cuh:55-66 */
@@ -397,6 +397,22 @@ void or_trace_rays(const OrScene *s, const float *rays6, int n, float *out12)
     }
 }
 
+/* per-ray work statistics (analysis aid): out per ray = [nodes, tris, hit] */
+void or_trace_stats(const OrScene *s, const float *rays6, int n, unsigned long long *out3)
+{
+#pragma omp parallel for schedule(dynamic, 64)
+    for (int i = 0; i < n; ++i) {
+        unsigned long long cnt[OR_CNT_COUNT] = {0};
+        Ray r = {v3(rays6[6 * i], rays6[6 * i + 1], rays6[6 * i + 2]),
+                 v3(rays6[6 * i + 3], rays6[6 * i + 4], rays6[6 * i + 5])};
+        Sample sm;
+        bool h = trace_ray(s, r, &sm, cnt);
+        out3[3 * i] = cnt[CNT_NODE];
+        out3[3 * i + 1] = cnt[CNT_TRI];
+        out3[3 * i + 2] = h ? 1 : 0;
+    }
+}
+
 /* ------------------------------------------- BSDF (rt/path_tracing.cuh) */
 enum { PRIMARY, DIFFUSE, SPECULAR, METALLIC, TRANSMISSION }; /* :18-25 */
 typedef struct { Ray ray; V3 weight; int type; } Event;     /* :27-32 */
@@ -610,6 +626,7 @@ static V3 trace_path(const OrScene *sc, Ray primary, uint32_t *rng, int max_dept
         if (r > p) break;
         T = mulvs(T, 1.0f / p);
     }
+    if ((unsigned long long)depth > cnt[CNT_MAXDEPTH]) cnt[CNT_MAXDEPTH] = (unsigned long long)depth;
     return L;
 }
 
@@ -703,7 +720,10 @@ int or_render(const OrScene *sc, const float cam[7], float *fb, float *sq, int *
         }
         if (counters) {
 #pragma omp critical
-            for (int c = 0; c < OR_CNT_COUNT; ++c) counters[c] += cnt[c];
+            for (int c = 0; c < OR_CNT_COUNT; ++c) {
+                if (c == CNT_MAXDEPTH) counters[c] = counters[c] > cnt[c] ? counters[c] : cnt[c];
+                else counters[c] += cnt[c];
+            }
         }
     }
     return 0;

@@ -1,6 +1,7 @@
 """GPU parity: the HIP path (through the C-ABI) against the CPU oracle on the
-same seeds.  The bar is bit-exact accumulators (fb, sq, count, RNG state) and
-equal work counters; north_star's 1e-4 relative L-infinity is reported too.
+same seeds, for both kernel variants (megakernel, wavefront).  The bar is
+bit-exact accumulators (fb, sq, count, RNG state) and equal work counters;
+north_star's 1e-4 relative L-infinity is asserted too.
 """
 import numpy as np
 import pytest
@@ -10,6 +11,7 @@ import oracle
 import rt
 
 pytestmark = pytest.mark.gpu
+KERNELS = [pytest.param(rt.KERNEL_MEGA, id="mega"), pytest.param(rt.KERNEL_WAVEFRONT, id="wavefront")]
 
 
 @pytest.fixture(scope="module")
@@ -17,9 +19,10 @@ def cornell():
     return helpers.GpuRun("cornell")
 
 
-def test_cornell_bitwise_adaptive_off(cornell):
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_cornell_bitwise_adaptive_off(cornell, kernel):
     W, H, P = 64, 64, 8
-    gpu, gcnt, _ = cornell.render(W, H, P, count=True)
+    gpu, gcnt, _ = cornell.render(W, H, P, count=True, kernel=kernel)
     ref, rcnt = helpers.oracle_render(cornell.path, W, H, P)
     helpers.assert_bitwise(gpu, ref, what="cornell")
     for k in rt.COUNTER_NAMES:
@@ -27,30 +30,42 @@ def test_cornell_bitwise_adaptive_off(cornell):
     assert helpers.rel_linf(gpu[0], gpu[2], ref[0], ref[2]) < 1e-4
 
 
-def test_cornell_split_calls_equal_one_call(cornell):
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_cornell_split_calls_equal_one_call(cornell, kernel):
     """render() called 3x with passes=2 == one call with passes=6 (state carried in the G_Buffer)."""
     W, H = 48, 32
-    a, _, _ = cornell.render(W, H, 2, calls=3)
-    b, _, _ = cornell.render(W, H, 6, calls=1)
+    a, _, _ = cornell.render(W, H, 2, calls=3, kernel=kernel)
+    b, _, _ = cornell.render(W, H, 6, calls=1, kernel=kernel)
     helpers.assert_bitwise(a, b, what="split")
 
 
-def test_cornell_adaptive_on(cornell):
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_cornell_adaptive_on(cornell, kernel):
     """Adaptive sampling (rt/path_tracing.cuh:352-376) with a low min_samples so it engages."""
     W, H, P = 40, 40, 24
-    gpu, gcnt, _ = cornell.render(W, H, P, adaptive=True, min_samples=6, count=True)
+    gpu, gcnt, _ = cornell.render(W, H, P, adaptive=True, min_samples=6, count=True, kernel=kernel)
     ref, rcnt = helpers.oracle_render(cornell.path, W, H, P, adaptive=True, min_samples=6)
     helpers.assert_bitwise(gpu, ref, what="adaptive")
     assert gcnt == rcnt
     assert rcnt["skip"] > 0  # the test really skipped pixels
 
 
-def test_odd_resolution_and_max_depth(cornell):
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_odd_resolution_and_max_depth(cornell, kernel):
     """W, H odd (SCREEN_W/2 integer truncation), max_depth cap applied identically."""
     W, H, P = 37, 23, 5
-    gpu, _, _ = cornell.render(W, H, P, max_depth=3)
-    ref, _ = helpers.oracle_render(cornell.path, W, H, P, max_depth=3)
+    gpu, gcnt, _ = cornell.render(W, H, P, max_depth=3, count=True, kernel=kernel)
+    ref, rcnt = helpers.oracle_render(cornell.path, W, H, P, max_depth=3)
     helpers.assert_bitwise(gpu, ref, what="odd")
+    assert gcnt == rcnt
+
+
+def test_kernels_agree_multi_call(cornell):
+    """Megakernel and wavefront give the same bits across calls with reset."""
+    W, H = 33, 31
+    a, _, _ = cornell.render(W, H, 3, calls=2, kernel=rt.KERNEL_MEGA)
+    b, _, _ = cornell.render(W, H, 3, calls=2, kernel=rt.KERNEL_WAVEFRONT)
+    helpers.assert_bitwise(a, b, what="mega-vs-wavefront")
 
 
 def test_tonemap_matches_oracle(cornell):
@@ -61,38 +76,42 @@ def test_tonemap_matches_oracle(cornell):
     assert np.max(np.abs(img.astype(int) - ref.astype(int))) <= 1
 
 
-def test_seed_shard_offset(cornell):
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_seed_shard_offset(cornell, kernel):
     """Shard g of an spp-sliced render seeds from mt19937 outputs [g*W*H, (g+1)*W*H)."""
     W, H, P = 24, 24, 3
-    gpu, _, _ = cornell.render(W, H, P, seed_skip=2 * W * H)
+    gpu, _, _ = cornell.render(W, H, P, seed_skip=2 * W * H, kernel=kernel)
     ref, _ = helpers.oracle_render(cornell.path, W, H, P, seed_skip=2 * W * H)
     helpers.assert_bitwise(gpu, ref, what="shard")
 
 
-def test_cornell_blob_bitwise():
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_cornell_blob_bitwise(kernel):
     run = helpers.GpuRun("cornell_blob")
     W, H, P = 64, 36, 4
-    gpu, gcnt, _ = run.render(W, H, P, count=True)
+    gpu, gcnt, _ = run.render(W, H, P, count=True, kernel=kernel)
     ref, rcnt = helpers.oracle_render(run.path, W, H, P)
     helpers.assert_bitwise(gpu, ref, what="cornell_blob")
     assert gcnt == rcnt
 
 
-def test_room_small_bitwise():
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_room_small_bitwise(kernel):
     run = helpers.GpuRun("room_small")
     W, H, P = 64, 36, 4
-    gpu, gcnt, _ = run.render(W, H, P, count=True)
+    gpu, gcnt, _ = run.render(W, H, P, count=True, kernel=kernel)
     ref, rcnt = helpers.oracle_render(run.path, W, H, P)
     helpers.assert_bitwise(gpu, ref, what="room_small")
     assert gcnt == rcnt
 
 
-def test_room2m_full_frame_sparse_pixels():
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_room2m_full_frame_sparse_pixels(kernel):
     """BASELINE config 3 scene at 1920x1080: full-frame GPU render, every
     4099th pixel re-rendered by the oracle (pixels are independent)."""
     run = helpers.GpuRun("room2m")
     W, H, P = 1920, 1080, 2
-    gpu, _, _ = run.render(W, H, P)
+    gpu, _, _ = run.render(W, H, P, kernel=kernel)
     pixels = np.arange(0, W * H, 4099, dtype=np.int32)
     ref, _ = helpers.oracle_render(run.path, W, H, P, pixels=pixels)
     helpers.assert_bitwise(gpu, ref, pixels=pixels, what="room2m")

@@ -1,0 +1,51 @@
+"""A/B kernel variants in ONE process, interleaved rounds (guide §5.4 rule 24).
+
+usage: python tools/ab.py SCENE PASSES MAX_DEPTH ROUNDS VARIANT[,VARIANT...]
+  VARIANT = kernel id (0 mega, 1 wavefront+dynamic fetch, 2 wavefront static)
+Prints per-variant Msamples/s (median, min, max) at 1920x1080 and the work
+counters of one counted run.
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in ("isaklm-raytracer_amd", "tests", "oracle"):
+    sys.path.insert(0, os.path.join(ROOT, p))
+import helpers  # noqa: E402
+import rt  # noqa: E402
+
+
+def main():
+    scene, P, maxd, rounds = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])
+    variants = [int(v) for v in sys.argv[5].split(",")]
+    W, H = int(os.environ.get("AB_W", 1920)), int(os.environ.get("AB_H", 1080))
+    run = helpers.GpuRun(scene)
+    g = rt.GBuffer(W, H)
+    times = {v: [] for v in variants}
+    for r in range(rounds):
+        for v in variants:
+            opt = rt.options(W, H, P, adaptive=False, max_depth=maxd, kernel=v)
+            rt.check(rt.lib().rt_synchronize())
+            t = time.perf_counter()
+            rt.render(run.dev, g, run.camera, 0, opt)
+            times[v].append(time.perf_counter() - t)
+    out = {}
+    for v in variants:
+        cnt = rt.DeviceCounters()
+        opt = rt.options(W, H, P, adaptive=False, max_depth=maxd, kernel=v, counters=cnt.p)
+        rt.render(run.dev, g, run.camera, 0, opt)
+        c = cnt.read()
+        ts = np.array(times[v])
+        out[v] = {"msamples_s_median": round(W * H * P / np.median(ts) / 1e6, 3),
+                  "msamples_s_best": round(W * H * P / ts.min() / 1e6, 3),
+                  "s": [round(x, 3) for x in ts], "maxdepth": c["maxdepth"],
+                  "per_sample": {k: round(c[k] / max(c["sample"], 1), 2) for k in ("ray", "node", "tri")}}
+    print(json.dumps({"scene": scene, "passes": P, "max_depth": maxd, "variants": out}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
