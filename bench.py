@@ -27,6 +27,7 @@ for p in (os.path.join(ROOT, "isaklm-raytracer_amd"), os.path.join(ROOT, "oracle
     sys.path.insert(0, p)
 
 import rt  # noqa: E402
+import shard  # noqa: E402
 
 METRIC = "Msamples/sec (W×H×spp/s) at 1920×1080; achieved HBM GB/s vs peak"
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
@@ -118,7 +119,7 @@ def main():
 
     W, H, P = args.width, args.height, args.passes
     n = W * H
-    gb = TorchGBuffer(torch, n, rank * n)
+    gb = TorchGBuffer(torch, n, shard.seed_skip(rank, W, H))
     stream = torch.cuda.current_stream()
     kernel = rt.KERNEL_WAVEFRONT if args.kernel == "wavefront" else rt.KERNEL_MEGA
     opt = rt.options(W, H, P, adaptive=False, stream=ctypes.c_void_p(stream.cuda_stream), kernel=kernel)
@@ -141,9 +142,7 @@ def main():
         step(args.warmup + k)
         ends[k].record(stream)
     if dist:  # one RCCL reduce over xGMI into rank 0's accumulation buffers
-        dist.reduce(gb.fb, 0)
-        dist.reduce(gb.sq, 0)
-        dist.reduce(gb.cnt, 0)
+        shard.reduce_to_root(dist, gb.fb, gb.sq, gb.cnt, root=0)
     if rank == 0:
         rt.check(rt.lib().rt_tonemap(gb.g, ctypes.c_void_p(rgba.data_ptr()), W, H,
                                      ctypes.c_void_p(stream.cuda_stream)))

@@ -263,6 +263,9 @@ int rt_render(rt_scene_t scene, G_Buffer g_buffer, Camera camera, int sample_cou
 int rt_tonemap(G_Buffer g_buffer, uint8_t *rgba_device, int width, int height, void *stream);
 /* save_render (rt/save_render.cuh:25-67): tonemap, flip vertically, write PNG */
 int rt_save_render(G_Buffer g_buffer, int width, int height, const char *png_path);
+/* the PNG encoder rt_save_render uses (replaces lodepng::encode,
+ * rt/save_render.cuh:18-23): host RGBA8 rows top to bottom */
+int rt_write_png(const char *png_path, const uint8_t *rgba_host, int width, int height);
 
 #ifdef __cplusplus
 }

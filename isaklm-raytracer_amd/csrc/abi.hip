@@ -449,4 +449,10 @@ int rt_save_render(G_Buffer g, int w, int h, const char *path)
     return rt_host::write_png(path, flipped.data(), w, h);
 }
 
+int rt_write_png(const char *path, const uint8_t *rgba, int w, int h)
+{
+    if (!path || !rgba || w <= 0 || h <= 0) { rt_set_error("rt_write_png: bad arguments"); return RT_E_INVALID; }
+    return rt_host::write_png(path, rgba, w, h);
+}
+
 } // extern "C"

@@ -74,6 +74,7 @@ RT_LIBM_FN double rt_reduce_pio2(double x, int *quadrant)
 
 RT_LIBM_FN double rt_sin_d(double x)
 {
+    if (x == 0.0) return x; /* keeps the sign of zero */
     int q;
     double r = rt_reduce_pio2(x, &q);
     switch (q & 3) {
@@ -101,6 +102,7 @@ RT_LIBM_FN float rt_cosf(float x) { return (float)rt_cos_d((double)x); }
 
 RT_LIBM_FN float rt_tanf(float xf)
 {
+    if (xf == 0.0f) return xf;
     int q;
     double r = rt_reduce_pio2((double)xf, &q);
     double s = rt_ksin(r), c = rt_kcos(r);

@@ -397,6 +397,19 @@ void or_trace_rays(const OrScene *s, const float *rays6, int n, float *out12)
     }
 }
 
+/* the shared transcendentals (rt_libm.h) for tests: kind 0 sinf, 1 cosf, 2 tanf, 3 powf(x, 1/2.4) */
+void or_libm(int kind, const float *in, float *out, int n)
+{
+    for (int i = 0; i < n; ++i) {
+        switch (kind) {
+        case 0: out[i] = rt_sinf(in[i]); break;
+        case 1: out[i] = rt_cosf(in[i]); break;
+        case 2: out[i] = rt_tanf(in[i]); break;
+        default: out[i] = rt_powf(in[i], (float)(1.0 / 2.4)); break;
+        }
+    }
+}
+
 /* per-ray work statistics (analysis aid): out per ray = [nodes, tris, hit] */
 void or_trace_stats(const OrScene *s, const float *rays6, int n, unsigned long long *out3)
 {

@@ -63,7 +63,7 @@ def oracle_render(path, W, H, passes, calls=1, adaptive=False, min_samples=100, 
         k = sc.render(cam, fb, sq, cnt, rng, W, H, passes, sample_count_arg=0 if c == 0 else 1, pixels=pixels,
                       adaptive=adaptive, min_samples=min_samples, tolerance=tolerance, max_depth=max_depth)
         for key, v in k.items():
-            total[key] = total.get(key, 0) + v
+            total[key] = max(total.get(key, 0), v) if key == "maxdepth" else total.get(key, 0) + v
     return (fb.reshape(n, 3), sq, cnt, rng), total
 
 

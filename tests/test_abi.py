@@ -1,0 +1,81 @@
+"""The C-ABI library (CPU only): it loads without a GPU, exports every
+function include/isaklm_rt.h declares, its structs have the reference's byte
+layout, and argument errors are reported, not crashed on."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+import rt
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "isaklm_rt.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(rt_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_exports_every_declared_symbol():
+    names = declared_functions()
+    assert len(names) >= 30
+    out = subprocess.run(["nm", "-D", "--defined-only", rt.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r" T (rt_\w+)", out))
+    missing = [n for n in names if n not in exported]
+    assert not missing, missing
+    lib = rt.lib()
+    for n in names:
+        getattr(lib, n)
+
+
+def test_struct_layouts_match_reference():
+    # sizes from SURVEY §8b (measured on the reference with g++ x86-64)
+    assert ctypes.sizeof(rt.Camera) == 28
+    assert ctypes.sizeof(rt.G_Buffer) == 32
+    assert ctypes.sizeof(rt.Scene) == 72
+    assert ctypes.sizeof(rt.KD_Tree) == 40
+    assert rt.Scene.light_indicies.offset == 16 and rt.Scene.kd_tree.offset == 32
+    assert rt.Camera.FOV.offset == 20
+    assert rt.TRIANGLE_BYTES == 152 and rt.NODE_BYTES == 20
+
+
+def test_header_compiles_as_c_and_cpp(tmp_path):
+    src = tmp_path / "t.c"
+    src.write_text('#include "isaklm_rt.h"\n'
+                   "_Static_assert(sizeof(Triangle) == 152, \"t\");\n"
+                   "_Static_assert(sizeof(Material) == 56, \"m\");\n"
+                   "_Static_assert(sizeof(KD_Tree_Node) == 20, \"n\");\n"
+                   "int main(void){ RtOptions o; rt_default_options(&o); return o.width == 1920 ? 0 : 1; }\n")
+    inc = os.path.join(ROOT, "include")
+    subprocess.run(["gcc", "-std=c11", "-Wall", "-Werror", "-I", inc, "-c", str(src), "-o", str(tmp_path / "t.o")],
+                   check=True)
+    cpp = tmp_path / "t.cpp"
+    cpp.write_text('#include "isaklm_rt.h"\nint main(){ return sizeof(Scene) == 72 ? 0 : 1; }\n')
+    subprocess.run(["g++", "-std=c++17", "-Wall", "-Werror", "-I", inc, "-c", str(cpp), "-o", str(tmp_path / "u.o")],
+                   check=True)
+
+
+def test_default_options_are_the_reference_macros():
+    o = rt.RtOptions()
+    rt.lib().rt_default_options(ctypes.byref(o))
+    assert (o.width, o.height, o.passes, o.adaptive, o.min_samples) == (1920, 1080, 1, 1, 100)
+    assert abs(o.tolerance - 0.05) < 1e-9 and o.max_depth == 0
+
+
+def test_argument_errors_are_reported():
+    L = rt.lib()
+    o = rt.RtOptions()
+    L.rt_default_options(ctypes.byref(o))
+    rc = L.rt_render(None, rt.G_Buffer(), rt.Camera(), 0, ctypes.byref(o))
+    assert rc == -1 and b"null" in L.rt_last_error()
+    assert L.rt_gbuffer_create(0, 10, 0, ctypes.byref(rt.G_Buffer())) == -1
+    assert L.rt_generate_scene(b"no_such_scene", b"/tmp", None, 0) == -1
+    assert L.rt_build_kd_tree(None, 0, None, None, None, None, None) == -1
+
+
+def test_version_string():
+    assert b"gfx950" in rt.lib().rt_version()

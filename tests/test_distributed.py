@@ -1,0 +1,75 @@
+"""The N>1 path on CPU: two gloo ranks each render their spp slice (seeded
+with their own mt19937 window), reduce into rank 0, and rank 0 checks the sum
+against a single-process emulation of the same shards — bit for bit."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import helpers
+import shard
+
+W, H, PASSES = 16, 12, 3
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _render_shard(path, rank):
+    (fb, sq, cnt, rng), _ = helpers.oracle_render(path, W, H, PASSES, seed_skip=shard.seed_skip(rank, W, H))
+    return fb, sq, cnt
+
+
+def _worker(rank, world, port, path, q):
+    import torch
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        fb, sq, cnt = _render_shard(path, rank)
+        t_fb, t_sq, t_cnt = torch.from_numpy(fb.copy()), torch.from_numpy(sq.copy()), torch.from_numpy(cnt.copy())
+        shard.reduce_to_root(dist, t_fb, t_sq, t_cnt, root=0)
+        if rank == 0:
+            q.put((t_fb.numpy().copy(), t_sq.numpy().copy(), t_cnt.numpy().copy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_pass_slices_cover_the_job():
+    for world in (1, 2, 3, 8):
+        spans = [shard.pass_slice(r, world, 5000) for r in range(world)]
+        assert spans[0][0] == 0 and spans[-1][1] == 5000
+        assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+
+
+def test_two_rank_gloo_reduce_matches_emulation():
+    import torch.multiprocessing as mp
+
+    path = helpers.scene_path("cornell")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, path, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    a = _render_shard(path, 0)
+    b = _render_shard(path, 1)
+    np.testing.assert_array_equal(got[0].view(np.uint32), (a[0] + b[0]).view(np.uint32))
+    np.testing.assert_array_equal(got[1].view(np.uint32), (a[1] + b[1]).view(np.uint32))
+    np.testing.assert_array_equal(got[2], a[2] + b[2])
+    assert np.all(got[2] == 2 * PASSES)
+    # rank 0's slice alone is the single-stream reference for its passes
+    single, _ = helpers.oracle_render(path, W, H, PASSES)
+    np.testing.assert_array_equal(a[0].view(np.uint32), single[0].view(np.uint32))

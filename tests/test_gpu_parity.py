@@ -105,6 +105,32 @@ def test_room_small_bitwise(kernel):
     assert gcnt == rcnt
 
 
+def _golden_cases():
+    import json
+    import os
+
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "oracle_regression.json")
+    return sorted(json.load(open(path))["renders"].items())
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+@pytest.mark.parametrize("key,gold", _golden_cases(), ids=[k for k, _ in _golden_cases()])
+def test_golden_vectors(key, gold, kernel):
+    """The committed fixtures (tests/golden/oracle_regression.json) reproduced on the GPU."""
+    import sys
+    import os
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    import make_golden
+
+    name, W, H, P, calls, adaptive, ms, md, skip = gold["case"]
+    run = helpers.GpuRun(name)
+    (fb, sq, cnt, rng), counters, _ = run.render(W, H, P, calls=calls, adaptive=adaptive, min_samples=ms,
+                                                 max_depth=md, seed_skip=skip, count=True, kernel=kernel)
+    assert make_golden.accum_digest(fb, sq, cnt, rng) == gold["sha256"]
+    assert counters == gold["counters"]
+
+
 @pytest.mark.parametrize("kernel", KERNELS)
 def test_room2m_full_frame_sparse_pixels(kernel):
     """BASELINE config 3 scene at 1920x1080: full-frame GPU render, every

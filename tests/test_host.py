@@ -1,0 +1,151 @@
+"""Host side of the boundary (CPU only): the product's OBJ/.mat loader,
+scene file, exact KD builder and seeds against the oracle's independent C
+restatement, plus error behaviour."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+import helpers
+import oracle
+import rt
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _compare_scene(path):
+    hs = rt.HostScene(path)
+    tb, n = hs.triangles_bytes()
+    osc = oracle.OracleScene(path)
+    otb, onodes, oidx, olights, obounds = osc.arrays()
+    assert n == osc.ntris
+    assert tb == otb, "triangles differ"
+    ptr, n = hs.triangle_ptr()
+    nodes, idx, bounds = rt.build_kd_tree(ptr, n)
+    assert nodes == onodes, "KD nodes differ"
+    np.testing.assert_array_equal(idx, oidx)
+    np.testing.assert_array_equal(np.array(bounds, np.float32), obounds)
+    cam = np.array(hs.camera.as_list(), np.float32)
+    np.testing.assert_array_equal(cam, osc.camera)
+    return hs, osc
+
+
+def test_features_obj_matches_oracle():
+    hs, osc = _compare_scene(os.path.join(GOLDEN, "features", "scene.txt"))
+    tb, n = hs.triangles_bytes()
+    # 8 faces -> 1 + 2 + 1 + 1 + 1 + 0 (false normal on v1) + 3 + 1 = 10 triangles per instance
+    assert n == 20
+    t = np.frombuffer(tb, np.uint8).reshape(n, 152)
+    mats = t[:, 96:152].copy().view(np.float32)[:, :9]
+    emissive = (mats[:, 3:6] > 0).any(axis=1)
+    assert emissive.sum() == 6  # the pentagon fan x 2 instances
+    uv = t[:, 72:96].copy().view(np.float32)
+    assert (uv == 1.0).any()  # ZERO_VEC2D = {1, 1} default UVs
+
+
+@pytest.mark.parametrize("name", ["cornell", "cornell_blob", "room_small"])
+def test_generated_scenes_match_oracle(name):
+    _compare_scene(helpers.scene_path(name))
+
+
+@pytest.mark.slow
+def test_room2m_matches_oracle():
+    """BASELINE config 3 scene: 2.04M triangles, 2.1M nodes, 11.5M indices."""
+    _compare_scene(helpers.scene_path("room2m"))
+
+
+def test_seeds_match_oracle():
+    for skip in (0, 1, 623, 624, 5000):
+        np.testing.assert_array_equal(rt.seeds(1000, skip), oracle.mt19937(1000, skip))
+
+
+def test_light_list_and_bounds_from_oracle_scene():
+    osc = oracle.OracleScene(helpers.scene_path("cornell"))
+    assert osc.nlights == 2  # the ceiling quad
+
+
+def _expect_error(fn, code):
+    with pytest.raises(rt.RtError) as e:
+        fn()
+    assert f"rt error {code}" in str(e.value)
+
+
+def test_missing_obj_is_io_error(tmp_path):
+    hs = rt.HostScene()
+    _expect_error(lambda: hs.load_mesh(str(tmp_path / "nope.obj"), str(tmp_path / "nope.mat"), [0, 0, 0],
+                                       np.eye(3)), -3)
+
+
+def test_malformed_obj_is_parse_error(tmp_path):
+    p = tmp_path / "bad.obj"
+    p.write_text("v 0 0 0\nv 1 x 0\n")
+    hs = rt.HostScene()
+    _expect_error(lambda: hs.load_mesh(str(p), str(tmp_path / "m.mat"), [0, 0, 0], np.eye(3)), -4)
+
+
+def test_face_index_out_of_range_is_parse_error(tmp_path):
+    p = tmp_path / "bad.obj"
+    p.write_text("v 0 0 0\nv 1 0 0\nv 0 1 0\nf 1 2 4\n")
+    hs = rt.HostScene()
+    _expect_error(lambda: hs.load_mesh(str(p), str(tmp_path / "m.mat"), [0, 0, 0], np.eye(3)), -4)
+
+
+def test_textured_material_is_unsupported(tmp_path):
+    (tmp_path / "t.obj").write_text("usemtl walls\nv 0 0 0\nv 1 0 0\nv 0 1 0\nf 1 2 3\n")
+    import shutil
+
+    shutil.copy(os.path.join(GOLDEN, "materials", "room.mat"), tmp_path / "room.mat")
+    hs = rt.HostScene()
+    _expect_error(lambda: hs.load_mesh(str(tmp_path / "t.obj"), str(tmp_path / "room.mat"), [0, 0, 0],
+                                       np.eye(3)), -5)
+
+
+def test_load_mesh_api_matches_scene_file(tmp_path):
+    """rt_host_scene_load_mesh with an explicit matrix == the scene-file path."""
+    d = os.path.join(GOLDEN, "features")
+    scene = tmp_path / "s.txt"
+    scene.write_text(f"mesh {d}/features.obj {d}/features.mat 0 0 0 0 0 1 0\n")
+    a = rt.HostScene(str(scene))
+    b = rt.HostScene()
+    b.load_mesh(f"{d}/features.obj", f"{d}/features.mat", [0, 0, 0],
+                np.array([[1, 0, 0], [0, 1, 0], [0, 0, 1]], np.float32))
+    ta, _ = a.triangles_bytes()
+    tb, _ = b.triangles_bytes()
+    assert ta == tb
+
+
+def _decode_png(path):
+    import struct
+    import zlib
+
+    data = open(path, "rb").read()
+    assert data[:8] == b"\x89PNG\r\n\x1a\n"
+    pos, idat = 8, b""
+    w = h = None
+    while pos < len(data):
+        n, = struct.unpack(">I", data[pos:pos + 4])
+        kind, body = data[pos + 4:pos + 8], data[pos + 8:pos + 8 + n]
+        crc, = struct.unpack(">I", data[pos + 8 + n:pos + 12 + n])
+        assert crc == zlib.crc32(kind + body) & 0xFFFFFFFF
+        if kind == b"IHDR":
+            w, h = struct.unpack(">II", body[:8])
+            assert body[8:10] == b"\x08\x06"  # 8-bit RGBA
+        elif kind == b"IDAT":
+            idat += body
+        pos += 12 + n
+    raw = zlib.decompress(idat)
+    rows = [raw[y * (4 * w + 1):(y + 1) * (4 * w + 1)] for y in range(h)]
+    assert all(r[0] == 0 for r in rows)
+    return np.frombuffer(b"".join(r[1:] for r in rows), np.uint8).reshape(h, w, 4)
+
+
+@pytest.mark.parametrize("w,h", [(3, 5), (300, 220)])  # 300x220 spans several 64 KiB stored blocks
+def test_png_writer_roundtrip(tmp_path, w, h):
+    """The PNG encoder behind rt_save_render (replaces lodepng::encode, rt/save_render.cuh:18-23)."""
+    img = np.random.default_rng(w).integers(0, 256, (h, w, 4), dtype=np.uint8)
+    path = str(tmp_path / "x.png")
+    L = rt.lib()
+    L.rt_write_png.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+    rt.check(L.rt_write_png(path.encode(), img.ctypes.data, w, h))
+    np.testing.assert_array_equal(_decode_png(path), img)
