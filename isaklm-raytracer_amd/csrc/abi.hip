@@ -100,6 +100,7 @@ int upload_prepared(const rt_host::PreparedHost &h, int ntris, int nindices, rt_
     dv.lights = lights;
     dv.light_count = h.light_count;
     dv.triangle_count = ntris;
+    dv.index_count = nindices;
     dv.bmin[0] = h.bounds.min.x; dv.bmin[1] = h.bounds.min.y; dv.bmin[2] = h.bounds.min.z;
     dv.bmax[0] = h.bounds.max.x; dv.bmax[1] = h.bounds.max.y; dv.bmax[2] = h.bounds.max.z;
     s->ntris = ntris;
@@ -402,7 +403,7 @@ int rt_render(rt_scene_t scene, G_Buffer g, Camera cam, int sample_count, const 
     dc.aperture = cam.aperture_radius;
 
     hipStream_t stream = (hipStream_t)o.stream;
-    if (o.kernel == RT_KERNEL_WAVEFRONT || o.kernel == 2) {
+    if (o.kernel >= RT_KERNEL_WAVEFRONT && o.kernel <= 3) {
         if (scene->max_depth > RT_STACK_DEPTH || rt_launch_wavefront(scene->dev, fr, dc, stream, o.kernel) != 0) {
             rt_set_error("rt_render: wavefront launch failed: %s", hipGetErrorString(hipGetLastError()));
             return RT_E_HIP;

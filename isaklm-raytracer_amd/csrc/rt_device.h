@@ -60,6 +60,7 @@ struct RtDevScene {
     const int *lights;          // light_count + 1 entries (SURVEY H4 padding)
     int light_count;
     int triangle_count;
+    int index_count;            // KD leaf entries
     float bmin[3], bmax[3];
 };
 

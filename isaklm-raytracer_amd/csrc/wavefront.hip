@@ -306,6 +306,360 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_trace_dyn(RtDevScene sc, WfState 
     if (COUNT) flush_counters(c, counters);
 }
 
+// ---------------------------------------------------------------------------
+// Wave-cooperative trace.  Lanes descend their own rays to a leaf (dynamic
+// ray fetch at leaf boundaries, as wf_trace_dyn); then the whole wave tests
+// the UNION of its lanes' leaf entries, 64 (ray, entry) pairs per round, so a
+// lane with a 40-entry leaf no longer idles 63 others.  Pair p belongs to the
+// lane j with start_j <= p < start_j + count_j (wave prefix sum, found by a
+// 6-step shuffle binary search); the owner's ray comes by __shfl.  Plane-test
+// survivors (dn != 0, 1e-5 <= s < leaf exit) are compacted into an LDS list
+// and run through the barycentric test 64 at a time.  A hit posts
+// (bits(s) << 32 | entry) to the owner's 64-bit LDS key with atomicMin:
+// s > 0, so the key order is (s, entry order) — exactly the first-wins
+// strict-< scan of trace_leaf_node (rt/trace_ray.cuh:124-141).  The owner
+// then recomputes the winner's barycentrics with the same arithmetic.
+#define WF_COOP_LIST 128
+
+namespace {
+
+struct CoopTest { // the barycentric part of intersect_triangle for leaf entry k at parameter s
+    __device__ static __forceinline__ bool bary(const RtDevScene &sc, uint32_t k, Vec3D o, Vec3D d, float s,
+                                                float &cx, float &cy, float &cz, int &tri)
+    {
+        const RtF4 B = ldf4(sc.isect_b + k), C = ldf4(sc.isect_c + k), D = ldf4(sc.isect_d + k);
+        const uint2 R = *reinterpret_cast<const uint2 *>(sc.isect_rt + 2 * (size_t)k);
+        const float rd = __uint_as_float(R.x);
+        const float px = o.x + d.x * s, py = o.y + d.y * s, pz = o.z + d.z * s;
+        const float v2x = px - B.x, v2y = py - B.y, v2z = pz - B.z;
+        const float d20 = v2x * C.x + v2y * C.y + v2z * C.z;
+        const float d21 = v2x * D.x + v2y * D.y + v2z * D.z;
+        cy = (D.w * d20 - C.w * d21) * rd;
+        cz = (B.w * d21 - C.w * d20) * rd;
+        cx = 1.0f - cy - cz;
+        tri = (int)R.y;
+        return cx >= 0.0f && cx <= 1.0f && cy >= 0.0f && cy <= 1.0f && cz >= 0.0f && cz <= 1.0f;
+    }
+};
+
+} // namespace
+
+template <bool COUNT>
+__global__ void __launch_bounds__(WF_BLOCK) wf_trace_coop(RtDevScene sc, WfState st, int q,
+                                                          unsigned long long *counters)
+{
+    __shared__ uint32_t s_node[WF_LDS_STACK * WF_BLOCK];
+    __shared__ float s_entry[WF_LDS_STACK * WF_BLOCK];
+    __shared__ unsigned long long s_key[WF_BLOCK];
+    __shared__ uint2 s_list[(WF_BLOCK / 64) * WF_COOP_LIST];
+    const int tid = threadIdx.x;
+    const int gtid = blockIdx.x * WF_BLOCK + tid;
+    const int lane = __lane_id();
+    const int wave = tid >> 6;
+    Stack<WF_LDS_STACK> stk{s_node + tid, s_entry + tid, WF_BLOCK, st.spill + gtid, st.spill_threads};
+    unsigned long long *wkey = s_key + wave * 64;
+    uint2 *list = s_list + wave * WF_COOP_LIST;
+    Cnt c;
+    if (COUNT) c.zero();
+    const uint32_t n = st.counts[q];
+    const RtF4 *rays = st.q_ray[q];
+    uint32_t *fetch = st.counts + 2 + q;
+
+    bool live = false, exhausted = false;
+    uint32_t e = 0, node = 0;
+    int sp = 0;
+    Vec3D o = rt_v3(0, 0, 0), d = rt_v3(0, 0, 0);
+    float entry = 0.0f, exit_ = 0.0f, root_exit = 0.0f;
+    while (true) {
+        // ---- refill idle lanes (dynamic ray fetch)
+        const bool need = !live && !exhausted;
+        const unsigned long long m = __ballot(need);
+        if (m) {
+            const int leader = __ffsll((long long)m) - 1;
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(fetch, (uint32_t)__popcll(m));
+            base = __shfl(base, leader);
+            if (need) {
+                e = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+                if (e >= n) {
+                    exhausted = true;
+                } else {
+                    o = ld3(ldf4(rays + 2 * (size_t)e));
+                    d = ld3(ldf4(rays + 2 * (size_t)e + 1));
+                    if (COUNT) c.v[RT_CNT_RAY]++;
+                    if (bbox_hit(sc, o, d, entry, exit_)) {
+                        root_exit = exit_;
+                        node = 0;
+                        sp = 0;
+                        live = true;
+                    } else {
+                        *reinterpret_cast<float4 *>(st.hits + e) = make_float4(__int_as_float(-1), 0.f, 0.f, 0.f);
+                    }
+                }
+            }
+        }
+        if (!__any(live)) {
+            if (__all(exhausted)) break;
+            continue;
+        }
+        // ---- descend to a leaf (rt/trace_ray.cuh:273-306), per lane
+        uint32_t leaf_begin = 0;
+        int leaf_count = 0;
+        if (live) {
+            uint2 nd = *reinterpret_cast<const uint2 *>(sc.nodes + 2 * (size_t)node);
+            if (COUNT) c.v[RT_CNT_NODE]++;
+            while ((nd.y & 3u) != RT_LEAF_TAG) {
+                const uint32_t axis = nd.y & 3u;
+                const float split = as_float(nd.x);
+                const float oax = axis == 0 ? o.x : (axis == 1 ? o.y : o.z);
+                const float dax = axis == 0 ? d.x : (axis == 1 ? d.y : d.z);
+                uint32_t near_c = node + 1, far_c = nd.y >> 2;
+                if (oax >= split) {
+                    near_c = nd.y >> 2;
+                    far_c = node + 1;
+                }
+                const float t = (split - oax) / dax;
+                if (t >= exit_ || t < 0) {
+                    node = near_c;
+                } else if (t <= entry) {
+                    node = far_c;
+                } else {
+                    stk.put(sp, far_c, t);
+                    ++sp;
+                    node = near_c;
+                    exit_ = t;
+                }
+                nd = *reinterpret_cast<const uint2 *>(sc.nodes + 2 * (size_t)node);
+                if (COUNT) c.v[RT_CNT_NODE]++;
+            }
+            leaf_begin = nd.x;
+            leaf_count = (int)(nd.y >> 2);
+            if (COUNT) c.v[RT_CNT_TRI] += (unsigned long long)leaf_count;
+        }
+        // ---- wave-cooperative leaf tests (all 64 lanes active from here)
+        int start = leaf_count; // inclusive scan -> exclusive
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int v = __shfl_up(start, off);
+            if (lane >= off) start += v;
+        }
+        const int total = __shfl(start, 63);
+        start -= leaf_count;
+        wkey[lane] = ~0ull;
+        int list_n = 0;
+        for (int base = 0; base < total || list_n > 0; base += 64) {
+            if (base < total) {
+                const int p = base + lane;
+                int j = 0; // owner: largest lane with start_j <= p
+#pragma unroll
+                for (int step = 32; step >= 1; step >>= 1) {
+                    const int sv = __shfl(start, j + step);
+                    if (sv <= p) j += step;
+                }
+                const uint32_t k = (uint32_t)__shfl((int)leaf_begin, j) + (uint32_t)(p - __shfl(start, j));
+                const Vec3D oo = rt_v3(__shfl(o.x, j), __shfl(o.y, j), __shfl(o.z, j));
+                const Vec3D dd = rt_v3(__shfl(d.x, j), __shfl(d.y, j), __shfl(d.z, j));
+                const float ex = __shfl(exit_, j);
+                bool pass = false;
+                float s = 0.0f;
+                if (p < total) {
+                    const RtF4 A = ldf4(sc.isect_a + k); // n, d
+                    const float dn = dd.x * A.x + dd.y * A.y + dd.z * A.z;
+                    s = (A.w - (oo.x * A.x + oo.y * A.y + oo.z * A.z)) / dn;
+                    pass = dn != 0 && s >= 0.00001f && s < ex;
+                }
+                const unsigned long long pm = __ballot(pass);
+                if (pass) list[list_n + __popcll(pm & ((1ull << lane) - 1ull))] = make_uint2((k << 6) | (uint32_t)j,
+                                                                                             __float_as_uint(s));
+                list_n += __popcll(pm);
+            }
+            // barycentric stage over up to 64 listed candidates
+            if (list_n >= 64 || (base + 64 >= total && list_n > 0)) {
+                const int take = list_n < 64 ? list_n : 64;
+                const bool act = lane < take;
+                const uint2 it = list[lane < take ? lane : 0];
+                const int j = (int)(it.x & 63u);
+                const Vec3D oo = rt_v3(__shfl(o.x, j), __shfl(o.y, j), __shfl(o.z, j));
+                const Vec3D dd = rt_v3(__shfl(d.x, j), __shfl(d.y, j), __shfl(d.z, j));
+                if (act) {
+                    float cx, cy, cz;
+                    int tri;
+                    const float s = __uint_as_float(it.y);
+                    if (CoopTest::bary(sc, it.x >> 6, oo, dd, s, cx, cy, cz, tri))
+                        atomicMin(wkey + j, ((unsigned long long)it.y << 32) | (it.x >> 6));
+                }
+                // move the rest (< 64) to the front
+                const int rest = list_n - take;
+                uint2 mv = make_uint2(0, 0);
+                if (lane < rest) mv = list[take + lane];
+                if (lane < rest) list[lane] = mv;
+                list_n = rest;
+            }
+        }
+        // ---- per-lane result: winner, or pop, or miss
+        const unsigned long long key = wkey[lane];
+        if (live) {
+            if (key != ~0ull) {
+                const uint32_t k = (uint32_t)key;
+                float cx, cy, cz;
+                int tri;
+                CoopTest::bary(sc, k, o, d, __uint_as_float((uint32_t)(key >> 32)), cx, cy, cz, tri);
+                if (COUNT) c.v[RT_CNT_HIT]++;
+                *reinterpret_cast<float4 *>(st.hits + e) = make_float4(__int_as_float(tri), cx, cy, cz);
+                live = false;
+            } else if (sp == 0) {
+                *reinterpret_cast<float4 *>(st.hits + e) = make_float4(__int_as_float(-1), 0.f, 0.f, 0.f);
+                live = false;
+            } else {
+                --sp;
+                node = stk.node_at(sp);
+                entry = stk.entry_at(sp);
+                exit_ = sp > 0 ? stk.entry_at(sp - 1) : root_exit;
+            }
+        }
+    }
+    if (COUNT) flush_counters(c, counters);
+}
+
+namespace {
+
+// the state of one pixel's path between two ray queries
+struct PathRegs {
+    uint32_t slot;
+    bool shadow, inside;
+    int prev_type, depth, passes_left, light;
+    uint32_t rng;
+    Vec3D T, L, rp, cont, snorm, ro, rd;
+};
+
+__device__ __forceinline__ void load_regs(const WfState &st, const RtDevFrame &fr, uint32_t slot, PathRegs &p)
+{
+    p.slot = slot;
+    const uint32_t flags = st.flags[slot];
+    p.shadow = flags & 1u;
+    p.inside = (flags >> 1) & 1u;
+    p.prev_type = (int)((flags >> 2) & 7u);
+    p.depth = (int)(flags >> 8);
+    p.rng = fr.rng[slot];
+    p.T = st.T[slot];
+    p.L = st.L[slot];
+    p.passes_left = st.passes_left[slot];
+    if (p.shadow) {
+        p.light = st.light[slot];
+        p.rp = st.rp[slot];
+        p.cont = st.cont[slot];
+        p.snorm = st.snorm[slot];
+    }
+}
+
+__device__ __forceinline__ void store_regs(const WfState &st, const RtDevFrame &fr, const PathRegs &p)
+{
+    const uint32_t slot = p.slot;
+    fr.rng[slot] = p.rng;
+    st.T[slot] = p.T;
+    st.L[slot] = p.L;
+    st.passes_left[slot] = p.passes_left;
+    st.flags[slot] = (p.shadow ? 1u : 0u) | (p.inside ? 2u : 0u) | ((uint32_t)p.prev_type << 2) |
+                     ((uint32_t)p.depth << 8);
+    if (p.shadow) {
+        st.light[slot] = p.light;
+        st.rp[slot] = p.rp;
+        st.cont[slot] = p.cont;
+        st.snorm[slot] = p.snorm;
+    }
+}
+
+// One event of trace_path (rt/path_tracing.cuh:268-325) for the hit of the
+// ray p.ro/p.rd: emission, BSDF, NEE set-up, roulette, accumulation and the
+// pixel's next pass.  Returns true with the next ray in p.ro/p.rd.
+template <bool COUNT>
+__device__ __forceinline__ bool shade_step(const RtDevScene &sc, const RtDevFrame &fr, const RtDevCamera &cam,
+                                           PathRegs &p, int hit, float bx, float by, float bz, int limit, Cnt &c)
+{
+    bool finish = false, roulette = true, want = false;
+    if (!p.shadow) {
+        if (hit < 0) {
+            finish = true; // miss: break without roulette (:303-306)
+            roulette = false;
+        } else {
+            Surface s;
+            shade<COUNT>(sc, hit, bx, by, bz, p.rd, s, c);
+            if (p.prev_type != DIFFUSE) p.L = p.L + s.emittance * p.T; // :285-288
+            Vec3D nd, w;
+            p.prev_type = scatter(p.rd, p.inside, p.rng, s, nd, w);
+            p.T = p.T * w;
+            p.ro = s.position;
+            p.rd = nd;
+            if (p.prev_type == DIFFUSE) { // sample_direct_light (:235-265)
+                if (COUNT) c.v[RT_CNT_NEE]++;
+                float xi = rng_next(p.rng);
+                if (sc.light_count == 0) {
+                    rng_next(p.rng);
+                    rng_next(p.rng);
+                    p.L = p.L + rt_v3(0.0f, 0.0f, 0.0f) * p.T;
+                } else {
+                    p.light = sc.lights[(int)(xi * (float)sc.light_count)];
+                    p.rp = light_point(sc, p.light, p.rng);
+                    p.cont = p.rd;
+                    p.snorm = s.normal;
+                    p.rd = rt_normalize(p.rp - p.ro);
+                    p.shadow = true;
+                    roulette = false; // roulette after the shadow ray
+                    want = true;
+                }
+            }
+        }
+    } else {
+        Vec3D direct = rt_v3(0.0f, 0.0f, 0.0f);
+        if (hit >= 0 && hit == p.light)
+            direct = light_contribution(sc, p.light, bx, by, bz, p.ro, p.rd, p.rp, p.snorm);
+        if (COUNT && hit >= 0 && material_of(sc, hit).tex) c.v[RT_CNT_TEXEL] += 2; // every hit is shaded
+        p.L = p.L + direct * p.T;
+        p.rd = p.cont;
+        p.shadow = false;
+    }
+    if (roulette) { // Russian roulette (:309-318)
+        float pr = fmaxf(p.T.x, fmaxf(p.T.y, p.T.z));
+        float r = rng_next(p.rng);
+        if (r > pr) {
+            finish = true;
+        } else {
+            p.T = p.T * (1.0f / pr);
+            if (p.depth == limit) { // max_depth / watchdog before the next extension ray
+                if (COUNT && fr.max_depth <= 0) c.v[RT_CNT_WATCHDOG]++;
+                finish = true;
+            } else {
+                ++p.depth;
+                want = true;
+            }
+        }
+    }
+    if (finish) { // accumulation (:322-324), then the pixel's next pass
+        if (COUNT) c.path_end(p.depth);
+        const uint32_t slot = p.slot;
+        Vec3D fb = fr.fb[slot] + p.L;
+        float sq = fr.sq[slot] + rt_square(rt_luminance(p.L));
+        int count = fr.count[slot] + 1;
+        fr.fb[slot] = fb;
+        fr.sq[slot] = sq;
+        fr.count[slot] = count;
+        if (p.passes_left > 0) {
+            want = start_sample<COUNT>(fr, cam, (int)slot, p.passes_left, p.rng, fb, sq, count, p.ro, p.rd, c);
+            if (want) {
+                p.T = rt_v3(1.0f, 1.0f, 1.0f);
+                p.L = rt_v3(0.0f, 0.0f, 0.0f);
+                p.inside = false;
+                p.prev_type = PRIMARY;
+                p.depth = 1;
+                p.shadow = false;
+            }
+        }
+    }
+    return want;
+}
+
+} // namespace
+
 template <bool COUNT>
 __global__ void __launch_bounds__(WF_BLOCK) wf_shade(RtDevScene sc, RtDevFrame fr, RtDevCamera cam, WfState st, int q)
 {
@@ -317,112 +671,52 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_shade(RtDevScene sc, RtDevFrame f
     for (uint32_t base = blockIdx.x * WF_BLOCK; base < n; base += gridDim.x * WF_BLOCK) {
         const uint32_t e = base + threadIdx.x;
         bool want = false;
-        uint32_t slot = 0;
-        Vec3D ro = rt_v3(0, 0, 0), rd = rt_v3(0, 0, 0);
+        PathRegs p;
+        p.slot = 0;
+        p.ro = p.rd = rt_v3(0, 0, 0);
         if (e < n) {
-            slot = st.q_slot[q][e];
+            load_regs(st, fr, st.q_slot[q][e], p);
             const RtF4 h = ldf4(st.hits + e);
-            const int hit = __float_as_int(h.x);
-            const float bx = h.y, by = h.z, bz = h.w;
-            ro = ld3(ldf4(st.q_ray[q] + 2 * (size_t)e));
-            rd = ld3(ldf4(st.q_ray[q] + 2 * (size_t)e + 1));
-            uint32_t flags = st.flags[slot];
-            bool shadow = flags & 1u;
-            bool inside = (flags >> 1) & 1u;
-            int prev_type = (int)((flags >> 2) & 7u);
-            int depth = (int)(flags >> 8);
-            uint32_t rng = fr.rng[slot];
-            Vec3D T = st.T[slot], L = st.L[slot];
-            bool finish = false, roulette = true;
-            if (!shadow) {
-                if (hit < 0) {
-                    finish = true; // miss: break without roulette (:303-306)
-                    roulette = false;
-                } else {
-                    Surface s;
-                    shade<COUNT>(sc, hit, bx, by, bz, rd, s, c);
-                    if (prev_type != DIFFUSE) L = L + s.emittance * T; // :285-288
-                    Vec3D nd, w;
-                    prev_type = scatter(rd, inside, rng, s, nd, w);
-                    T = T * w;
-                    ro = s.position;
-                    rd = nd;
-                    if (prev_type == DIFFUSE) { // sample_direct_light (:235-265)
-                        if (COUNT) c.v[RT_CNT_NEE]++;
-                        float xi = rng_next(rng);
-                        if (sc.light_count == 0) {
-                            rng_next(rng);
-                            rng_next(rng);
-                            L = L + rt_v3(0.0f, 0.0f, 0.0f) * T;
-                        } else {
-                            const int light = sc.lights[(int)(xi * (float)sc.light_count)];
-                            const Vec3D rp = light_point(sc, light, rng);
-                            st.light[slot] = light;
-                            st.rp[slot] = rp;
-                            st.cont[slot] = rd;
-                            st.snorm[slot] = s.normal;
-                            rd = rt_normalize(rp - ro);
-                            shadow = true;
-                            roulette = false; // roulette after the shadow ray
-                            want = true;
-                        }
-                    }
-                }
-            } else {
-                const int light = st.light[slot];
-                Vec3D direct = rt_v3(0.0f, 0.0f, 0.0f);
-                if (hit >= 0 && hit == light)
-                    direct = light_contribution(sc, light, bx, by, bz, ro, rd, st.rp[slot], st.snorm[slot]);
-                if (COUNT && hit >= 0 && material_of(sc, hit).tex) c.v[RT_CNT_TEXEL] += 2; // every hit is shaded
-                L = L + direct * T;
-                rd = st.cont[slot];
-                shadow = false;
-            }
-            if (roulette) { // Russian roulette (:309-318)
-                float p = fmaxf(T.x, fmaxf(T.y, T.z));
-                float r = rng_next(rng);
-                if (r > p) {
-                    finish = true;
-                } else {
-                    T = T * (1.0f / p);
-                    if (depth == limit) { // max_depth / watchdog before the next extension ray
-                        if (COUNT && fr.max_depth <= 0) c.v[RT_CNT_WATCHDOG]++;
-                        finish = true;
-                    } else {
-                        ++depth;
-                        want = true;
-                    }
-                }
-            }
-            if (finish) { // accumulation (:322-324), then the pixel's next pass
-                if (COUNT) c.path_end(depth);
-                Vec3D fb = fr.fb[slot] + L;
-                float sq = fr.sq[slot] + rt_square(rt_luminance(L));
-                int count = fr.count[slot] + 1;
-                fr.fb[slot] = fb;
-                fr.sq[slot] = sq;
-                fr.count[slot] = count;
-                int passes_left = st.passes_left[slot];
-                if (passes_left > 0) {
-                    want = start_sample<COUNT>(fr, cam, (int)slot, passes_left, rng, fb, sq, count, ro, rd, c);
-                    st.passes_left[slot] = passes_left;
-                    if (want) {
-                        T = rt_v3(1.0f, 1.0f, 1.0f);
-                        L = rt_v3(0.0f, 0.0f, 0.0f);
-                        inside = false;
-                        prev_type = PRIMARY;
-                        depth = 1;
-                        shadow = false;
-                    }
-                }
-            }
-            fr.rng[slot] = rng;
-            st.T[slot] = T;
-            st.L[slot] = L;
-            st.flags[slot] = (shadow ? 1u : 0u) | (inside ? 2u : 0u) | ((uint32_t)prev_type << 2) |
-                             ((uint32_t)depth << 8);
+            p.ro = ld3(ldf4(st.q_ray[q] + 2 * (size_t)e));
+            p.rd = ld3(ldf4(st.q_ray[q] + 2 * (size_t)e + 1));
+            want = shade_step<COUNT>(sc, fr, cam, p, __float_as_int(h.x), h.y, h.z, h.w, limit, c);
+            store_regs(st, fr, p);
         }
-        enqueue(st, qn, want, slot, ro, rd);
+        enqueue(st, qn, want, p.slot, p.ro, p.rd);
+    }
+    if (COUNT) flush_counters(c, fr.counters);
+}
+
+// Tail finisher: once few paths remain, each remaining pixel is run to the end
+// of its passes by one lane (trace + shade in registers, megakernel style), so
+// the long total-internal-reflection paths cost one launch instead of one
+// trace/shade iteration per bounce.
+template <bool COUNT>
+__global__ void __launch_bounds__(WF_BLOCK) wf_finish(RtDevScene sc, RtDevFrame fr, RtDevCamera cam, WfState st, int q)
+{
+    __shared__ uint32_t s_node[WF_LDS_STACK * WF_BLOCK];
+    __shared__ float s_entry[WF_LDS_STACK * WF_BLOCK];
+    const int tid = threadIdx.x;
+    const int gtid = blockIdx.x * WF_BLOCK + tid;
+    Stack<WF_LDS_STACK> stk{s_node + tid, s_entry + tid, WF_BLOCK, st.spill + gtid, st.spill_threads};
+    Cnt c;
+    if (COUNT) c.zero();
+    const uint32_t n = st.counts[q];
+    const int limit = fr.max_depth > 0 ? fr.max_depth : RT_WATCHDOG_BOUNCES;
+    for (uint32_t base = blockIdx.x * WF_BLOCK; base < n; base += gridDim.x * WF_BLOCK) {
+        const uint32_t e = base + tid;
+        if (e < n) {
+            PathRegs p;
+            load_regs(st, fr, st.q_slot[q][e], p);
+            p.ro = ld3(ldf4(st.q_ray[q] + 2 * (size_t)e));
+            p.rd = ld3(ldf4(st.q_ray[q] + 2 * (size_t)e + 1));
+            while (true) {
+                float bx = 0.0f, by = 0.0f, bz = 0.0f;
+                const int hit = trace<COUNT>(sc, p.ro, p.rd, bx, by, bz, stk, c);
+                if (!shade_step<COUNT>(sc, fr, cam, p, hit, bx, by, bz, limit, c)) break;
+            }
+            store_regs(st, fr, p);
+        }
     }
     if (COUNT) flush_counters(c, fr.counters);
 }
@@ -488,7 +782,9 @@ int ensure(Workspace &w, size_t slots, int grid)
 int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevCamera &cam, hipStream_t stream,
                         int variant)
 {
-    const bool dyn = variant != 2;
+    // 1: wave-cooperative leaves (entries packed as k << 6 | lane: needs < 2^26 entries), 2: static, 3: per-lane fetch
+    int trace_kind = variant;
+    if (trace_kind == 1 && sc.index_count >= (1 << 26)) trace_kind = 3;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return -1;
     Workspace &w = g_ws[dev];
@@ -500,26 +796,40 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
     const int tiles = ((fr.width + 15) / 16) * ((fr.height + 15) / 16);
     if (count) hipLaunchKernelGGL(wf_start<true>, dim3(tiles), dim3(WF_BLOCK), 0, stream, fr, cam, w.st);
     else hipLaunchKernelGGL(wf_start<false>, dim3(tiles), dim3(WF_BLOCK), 0, stream, fr, cam, w.st);
-    const int check_every = 8;
+    // below this many live paths the rest of the call runs in one wf_finish launch
+    static const uint32_t tail = [] {
+        const char *e = getenv("RT_WF_TAIL");
+        return e ? (uint32_t)atoi(e) : 65536u;
+    }();
     for (int it = 0;; ++it) {
         const int q = it & 1;
         if (hipMemsetAsync(w.st.counts + (q ^ 1), 0, 4, stream) != hipSuccess) return -1;
         if (hipMemsetAsync(w.st.counts + 2 + q, 0, 4, stream) != hipSuccess) return -1; // fetch cursor
-        if (count) {
-            if (dyn) hipLaunchKernelGGL(wf_trace_dyn<true>, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, w.st, q, fr.counters);
-            else hipLaunchKernelGGL(wf_trace<true>, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, w.st, q, fr.counters);
-            hipLaunchKernelGGL(wf_shade<true>, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, fr, cam, w.st, q);
-        } else {
-            if (dyn) hipLaunchKernelGGL(wf_trace_dyn<false>, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, w.st, q, fr.counters);
-            else hipLaunchKernelGGL(wf_trace<false>, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, w.st, q, fr.counters);
-            hipLaunchKernelGGL(wf_shade<false>, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, fr, cam, w.st, q);
-        }
+#define WF_LAUNCH_TRACE(C)                                                                                         \
+    do {                                                                                                           \
+        if (trace_kind == 1)                                                                                       \
+            hipLaunchKernelGGL(wf_trace_coop<C>, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, w.st, q, fr.counters); \
+        else if (trace_kind == 3)                                                                                  \
+            hipLaunchKernelGGL(wf_trace_dyn<C>, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, w.st, q, fr.counters);  \
+        else                                                                                                       \
+            hipLaunchKernelGGL(wf_trace<C>, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, w.st, q, fr.counters);      \
+        hipLaunchKernelGGL(wf_shade<C>, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, fr, cam, w.st, q);              \
+    } while (0)
+        if (count) WF_LAUNCH_TRACE(true);
+        else WF_LAUNCH_TRACE(false);
+#undef WF_LAUNCH_TRACE
         if (hipGetLastError() != hipSuccess) return -1;
-        if (it % check_every == check_every - 1) {
-            if (hipMemcpyAsync(w.host_count, w.st.counts + (q ^ 1), 4, hipMemcpyDeviceToHost, stream) != hipSuccess)
-                return -1;
-            if (hipStreamSynchronize(stream) != hipSuccess) return -1;
-            if (*w.host_count == 0) break;
+        if (hipMemcpyAsync(w.host_count, w.st.counts + (q ^ 1), 4, hipMemcpyDeviceToHost, stream) != hipSuccess)
+            return -1;
+        if (hipStreamSynchronize(stream) != hipSuccess) return -1;
+        const uint32_t live = *w.host_count;
+        if (live == 0) break;
+        if (live < tail) {
+            const int fgrid = (int)((live + WF_BLOCK - 1) / WF_BLOCK);
+            if (count) hipLaunchKernelGGL(wf_finish<true>, dim3(fgrid), dim3(WF_BLOCK), 0, stream, sc, fr, cam, w.st, q ^ 1);
+            else hipLaunchKernelGGL(wf_finish<false>, dim3(fgrid), dim3(WF_BLOCK), 0, stream, sc, fr, cam, w.st, q ^ 1);
+            if (hipGetLastError() != hipSuccess) return -1;
+            break;
         }
     }
     return 0;

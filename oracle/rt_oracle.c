@@ -329,6 +329,13 @@ static bool intersect_bbox(Ray r, BBox b, float *t1, float *t2)
     return tn <= tf;
 }
 
+/* analysis aids (single-threaded use only): a log of traced rays, and of the
+ * (descent steps, leaf size) sequence of each traversal */
+static float *g_raylog = NULL;
+static int g_raylog_n = 0, g_raylog_cap = 0;
+static int *g_visits = NULL;
+static int g_visits_n = 0, g_visits_cap = 0;
+
 /* trace_ray (rt/trace_ray.cuh:244-318) with ray_behind_plane (:174-188) and
  * intersect_plane (:190-210) inlined */
 static bool trace_ray(const OrScene *sc, Ray ray, Sample *sm, unsigned long long *cnt)
@@ -337,6 +344,12 @@ static bool trace_ray(const OrScene *sc, Ray ray, Sample *sm, unsigned long long
     float entry_d[KD_TREE_DEPTH + 8], exit_d[KD_TREE_DEPTH + 8];
     float t1, t2;
     cnt[CNT_RAY] += 1;
+    if (g_raylog && g_raylog_n < g_raylog_cap) {
+        float *r = g_raylog + 6 * g_raylog_n++;
+        r[0] = ray.position.x; r[1] = ray.position.y; r[2] = ray.position.z;
+        r[3] = ray.direction.x; r[4] = ray.direction.y; r[5] = ray.direction.z;
+    }
+    unsigned long long nodes_before = cnt[CNT_NODE];
     if (!intersect_bbox(ray, sc->bounds, &t1, &t2)) return false;
     node_idx[0] = 0;
     entry_d[0] = t1;
@@ -371,11 +384,62 @@ static bool trace_ray(const OrScene *sc, Ray ray, Sample *sm, unsigned long long
             }
             cnt[CNT_NODE] += 1;
         }
+        if (g_visits && g_visits_n + 2 <= g_visits_cap) {
+            g_visits[g_visits_n++] = (int)(cnt[CNT_NODE] - nodes_before);
+            g_visits[g_visits_n++] = node.b;
+            nodes_before = cnt[CNT_NODE];
+        }
         if (node.b > 0) {
             if (trace_leaf(sc, ray, exit_, node.a, node.b, sm, cnt)) return true;
         }
     }
     return false;
+}
+
+/* analysis: path-trace `pixels` (1 pass each, single thread) logging every traced ray */
+int or_log_rays(const OrScene *s, const float cam[7], int width, int height, const int *pixels, int npix,
+                float *rays_out, int max_rays)
+{
+    OrOptions o;
+    or_default_options(&o);
+    o.width = width;
+    o.height = height;
+    o.adaptive = 0;
+    o.threads = 1;
+    int n = width * height;
+    float *fb = (float *)calloc((size_t)n * 3, sizeof(float));
+    float *sq = (float *)calloc((size_t)n, sizeof(float));
+    int *count = (int *)calloc((size_t)n, sizeof(int));
+    uint32_t *rng = (uint32_t *)malloc((size_t)n * sizeof(uint32_t));
+    or_mt19937(rng, (size_t)n, 0);
+    g_raylog = rays_out;
+    g_raylog_n = 0;
+    g_raylog_cap = max_rays;
+    or_render(s, cam, fb, sq, count, rng, pixels, npix, 0, &o, NULL);
+    int got = g_raylog_n;
+    g_raylog = NULL;
+    free(fb); free(sq); free(count); free(rng);
+    return got;
+}
+
+/* analysis: per ray, the sequence of (descent node fetches, leaf size) pairs.
+ * offsets[i]..offsets[i+1] index pairs in visits_out (2 ints each). */
+int or_trace_visits(const OrScene *s, const float *rays6, int n, int *offsets, int *visits_out, int cap_ints)
+{
+    unsigned long long cnt[OR_CNT_COUNT] = {0};
+    g_visits = visits_out;
+    g_visits_n = 0;
+    g_visits_cap = cap_ints;
+    for (int i = 0; i < n; ++i) {
+        offsets[i] = g_visits_n / 2;
+        Ray r = {v3(rays6[6 * i], rays6[6 * i + 1], rays6[6 * i + 2]),
+                 v3(rays6[6 * i + 3], rays6[6 * i + 4], rays6[6 * i + 5])};
+        Sample sm;
+        trace_ray(s, r, &sm, cnt);
+    }
+    offsets[n] = g_visits_n / 2;
+    g_visits = NULL;
+    return offsets[n];
 }
 
 void or_trace_rays(const OrScene *s, const float *rays6, int n, float *out12)

@@ -60,6 +60,16 @@ def test_odd_resolution_and_max_depth(cornell, kernel):
     assert gcnt == rcnt
 
 
+@pytest.mark.parametrize("variant", [2, 3], ids=["wavefront-static-trace", "wavefront-lane-fetch"])
+def test_other_trace_variants(variant):
+    run = helpers.GpuRun("room_small")
+    W, H, P = 48, 27, 3
+    gpu, gcnt, _ = run.render(W, H, P, count=True, kernel=variant)
+    ref, rcnt = helpers.oracle_render(run.path, W, H, P)
+    helpers.assert_bitwise(gpu, ref, what=f"variant{variant}")
+    assert gcnt == rcnt
+
+
 def test_kernels_agree_multi_call(cornell):
     """Megakernel and wavefront give the same bits across calls with reset."""
     W, H = 33, 31
