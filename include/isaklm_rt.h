@@ -250,6 +250,12 @@ typedef struct RtOptions {
     void *stream;        /* hipStream_t; NULL = synchronous on the null stream */
     unsigned long long *counters_device; /* optional RT_CNT_COUNT u64 counters (adds) */
     unsigned long long *wave_times_device; /* optional debug: 2 u64 per wave (megakernel, with counters) */
+    /* wavefront tuning (0 = default): below wf_tail live paths the rest of
+     * the call runs in one cooperative finisher launch on at most
+     * wf_finish_waves waves; wf_tail > width*height runs the whole call in
+     * the finisher (persistent per-wave path fetch, no queue iterations) */
+    int wf_tail;
+    int wf_finish_waves;
 } RtOptions;
 
 void rt_default_options(RtOptions *opt);

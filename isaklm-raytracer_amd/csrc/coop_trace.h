@@ -1,0 +1,191 @@
+// coop_trace.h — wave-cooperative ray traversal (included by wavefront.hip).
+//
+// trace_ray (rt/trace_ray.cuh:244-318) for up to 64 rays per wave.  Each
+// step, every live lane descends its own ray to the next leaf (per-lane,
+// front to back, LDS/HBM stack as in rt_kernels.h); then the whole wave tests
+// the UNION of its lanes' leaf entries, 64 (ray, entry) pairs per round, so a
+// lane with a 40-entry leaf no longer idles the 63 others — and a single ray
+// (the tail finisher) gets its leaf tested 64 entries at a time.  Pair p
+// belongs to the lane j with start_j <= p < start_j + count_j (wave prefix sum
+// of leaf sizes, found by a 6-step shuffle binary search); the owner's ray
+// comes by __shfl.  Plane-test survivors (dn != 0, 1e-5 <= s < leaf exit) are
+// compacted into an LDS list and run through the barycentric test 64 at a
+// time.  A hit posts (bits(s) << 32 | entry) to the owner's 64-bit LDS key
+// with atomicMin: s > 0, so key order is (s, entry order) — exactly the
+// first-wins strict-< scan of trace_leaf_node (rt/trace_ray.cuh:124-141).
+// The owner then recomputes the winner's barycentrics with the same
+// arithmetic.  Results are bit-identical to the sequential scan.
+#pragma once
+
+#define WF_COOP_LIST 128 // per-wave LDS list of plane-test survivors
+
+namespace rtk {
+
+// barycentric part of intersect_triangle (rt/trace_ray.cuh:48-71,100-110) for
+// leaf entry k at the exact plane parameter s
+__device__ __forceinline__ bool coop_bary(const RtDevScene &sc, uint32_t k, Vec3D o, Vec3D d, float s, float &cx,
+                                          float &cy, float &cz, int &tri)
+{
+    const RtF4 B = ldf4(sc.isect_b + k), C = ldf4(sc.isect_c + k), D = ldf4(sc.isect_d + k);
+    const uint2 R = *reinterpret_cast<const uint2 *>(sc.isect_rt + 2 * (size_t)k);
+    const float rd = __uint_as_float(R.x);
+    const float px = o.x + d.x * s, py = o.y + d.y * s, pz = o.z + d.z * s;
+    const float v2x = px - B.x, v2y = py - B.y, v2z = pz - B.z;
+    const float d20 = v2x * C.x + v2y * C.y + v2z * C.z;
+    const float d21 = v2x * D.x + v2y * D.y + v2z * D.z;
+    cy = (D.w * d20 - C.w * d21) * rd;
+    cz = (B.w * d21 - C.w * d20) * rd;
+    cx = 1.0f - cy - cz;
+    tri = (int)R.y;
+    return cx >= 0.0f && cx <= 1.0f && cy >= 0.0f && cy <= 1.0f && cz >= 0.0f && cz <= 1.0f;
+}
+
+// per-lane traversal state
+struct CoopRay {
+    bool live;
+    Vec3D o, d;
+    float entry, exit_, root_exit;
+    uint32_t node;
+    int sp;
+};
+
+// start a ray: slab test on the scene box; false = miss
+__device__ __forceinline__ bool coop_begin(const RtDevScene &sc, CoopRay &r, Vec3D o, Vec3D d)
+{
+    r.o = o;
+    r.d = d;
+    r.node = 0;
+    r.sp = 0;
+    r.live = bbox_hit(sc, o, d, r.entry, r.exit_);
+    r.root_exit = r.exit_;
+    return r.live;
+}
+
+// One traversal step for every live lane of the wave (call with all 64 lanes
+// active).  Returns true for a lane whose ray finished in this step, with
+// tri >= 0 and the barycentrics of the hit, or tri = -1 for a miss.
+template <bool COUNT, typename STK>
+__device__ __forceinline__ bool coop_step(const RtDevScene &sc, CoopRay &r, STK &stk, unsigned long long *wkey,
+                                          uint2 *list, int &tri, float &hbx, float &hby, float &hbz, Cnt &c)
+{
+    const int lane = __lane_id();
+    // ---- descend to a leaf (rt/trace_ray.cuh:273-306), per lane
+    uint32_t leaf_begin = 0;
+    int leaf_count = 0;
+    if (r.live) {
+        // scalar copies: a select between struct members would become a
+        // dynamically indexed (scratch) load
+        const float ox = r.o.x, oy = r.o.y, oz = r.o.z, dx = r.d.x, dy = r.d.y, dz = r.d.z;
+        uint2 nd = *reinterpret_cast<const uint2 *>(sc.nodes + 2 * (size_t)r.node);
+        if (COUNT) c.v[RT_CNT_NODE]++;
+        while ((nd.y & 3u) != RT_LEAF_TAG) {
+            const uint32_t axis = nd.y & 3u;
+            const float split = as_float(nd.x);
+            const float oax = axis == 0 ? ox : (axis == 1 ? oy : oz);
+            const float dax = axis == 0 ? dx : (axis == 1 ? dy : dz);
+            uint32_t near_c = r.node + 1, far_c = nd.y >> 2;
+            if (oax >= split) { // ray_behind_plane (:174-188)
+                near_c = nd.y >> 2;
+                far_c = r.node + 1;
+            }
+            const float t = (split - oax) / dax; // intersect_plane (:190-210)
+            if (t >= r.exit_ || t < 0) {
+                r.node = near_c;
+            } else if (t <= r.entry) {
+                r.node = far_c;
+            } else {
+                stk.put(r.sp, far_c, t);
+                ++r.sp;
+                r.node = near_c;
+                r.exit_ = t;
+            }
+            nd = *reinterpret_cast<const uint2 *>(sc.nodes + 2 * (size_t)r.node);
+            if (COUNT) c.v[RT_CNT_NODE]++;
+        }
+        leaf_begin = nd.x;
+        leaf_count = (int)(nd.y >> 2);
+        if (COUNT) c.v[RT_CNT_TRI] += (unsigned long long)leaf_count;
+    }
+    // ---- wave-cooperative leaf tests
+    int start = leaf_count; // inclusive scan -> exclusive
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int v = __shfl_up(start, off);
+        if (lane >= off) start += v;
+    }
+    const int total = __shfl(start, 63);
+    start -= leaf_count;
+    wkey[lane] = ~0ull;
+    int list_n = 0;
+    for (int base = 0; base < total || list_n > 0; base += 64) {
+        if (base < total) {
+            const int p = base + lane;
+            int j = 0; // owner: the largest lane with start_j <= p
+#pragma unroll
+            for (int step = 32; step >= 1; step >>= 1) {
+                const int sv = __shfl(start, j + step);
+                if (sv <= p) j += step;
+            }
+            const uint32_t k = (uint32_t)__shfl((int)leaf_begin, j) + (uint32_t)(p - __shfl(start, j));
+            const Vec3D oo = rt_v3(__shfl(r.o.x, j), __shfl(r.o.y, j), __shfl(r.o.z, j));
+            const Vec3D dd = rt_v3(__shfl(r.d.x, j), __shfl(r.d.y, j), __shfl(r.d.z, j));
+            const float ex = __shfl(r.exit_, j);
+            bool pass = false;
+            float s = 0.0f;
+            if (p < total) {
+                const RtF4 A = ldf4(sc.isect_a + k); // n, d
+                const float dn = dd.x * A.x + dd.y * A.y + dd.z * A.z;
+                s = (A.w - (oo.x * A.x + oo.y * A.y + oo.z * A.z)) / dn;
+                pass = dn != 0 && s >= 0.00001f && s < ex;
+            }
+            const unsigned long long pm = __ballot(pass);
+            if (pass)
+                list[list_n + __popcll(pm & ((1ull << lane) - 1ull))] = make_uint2((k << 6) | (uint32_t)j,
+                                                                                   __float_as_uint(s));
+            list_n += __popcll(pm);
+        }
+        // barycentric stage over up to 64 listed candidates
+        if (list_n >= 64 || (base + 64 >= total && list_n > 0)) {
+            const int take = list_n < 64 ? list_n : 64;
+            const uint2 it = list[lane < take ? lane : 0];
+            const int j = (int)(it.x & 63u);
+            const Vec3D oo = rt_v3(__shfl(r.o.x, j), __shfl(r.o.y, j), __shfl(r.o.z, j));
+            const Vec3D dd = rt_v3(__shfl(r.d.x, j), __shfl(r.d.y, j), __shfl(r.d.z, j));
+            if (lane < take) {
+                float cx, cy, cz;
+                int t;
+                if (coop_bary(sc, it.x >> 6, oo, dd, __uint_as_float(it.y), cx, cy, cz, t))
+                    atomicMin(wkey + j, ((unsigned long long)it.y << 32) | (it.x >> 6));
+            }
+            const int rest = list_n - take; // move the rest (< 64) to the front
+            uint2 mv = make_uint2(0, 0);
+            if (lane < rest) mv = list[take + lane];
+            if (lane < rest) list[lane] = mv;
+            list_n = rest;
+        }
+    }
+    // ---- per-lane result: winner, or pop, or miss
+    const unsigned long long key = wkey[lane];
+    bool done = false;
+    if (r.live) {
+        if (key != ~0ull) {
+            const uint32_t k = (uint32_t)key;
+            coop_bary(sc, k, r.o, r.d, __uint_as_float((uint32_t)(key >> 32)), hbx, hby, hbz, tri);
+            if (COUNT) c.v[RT_CNT_HIT]++;
+            r.live = false;
+            done = true;
+        } else if (r.sp == 0) {
+            tri = -1;
+            r.live = false;
+            done = true;
+        } else {
+            --r.sp;
+            r.node = stk.node_at(r.sp);
+            r.entry = stk.entry_at(r.sp);
+            r.exit_ = r.sp > 0 ? stk.entry_at(r.sp - 1) : r.root_exit;
+        }
+    }
+    return done;
+}
+
+} // namespace rtk

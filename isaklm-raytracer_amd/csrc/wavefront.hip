@@ -15,6 +15,9 @@
 // and the CPU oracle.
 #include <hip/hip_runtime.h>
 
+#include <stdio.h>
+#include <time.h>
+
 #include <map>
 
 #include "rt_kernels.h"
@@ -23,6 +26,8 @@ using namespace rtk;
 
 #define WF_BLOCK 256
 #define WF_LDS_STACK 8  // stack entries in LDS; deeper ones spill to HBM (rare)
+#define WF_TAIL_DEFAULT 65536u       // RtOptions.wf_tail
+#define WF_FINISH_WAVES_DEFAULT 2048u // RtOptions.wf_finish_waves
 
 struct WfState {
     int *passes_left;
@@ -306,44 +311,10 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_trace_dyn(RtDevScene sc, WfState 
     if (COUNT) flush_counters(c, counters);
 }
 
-// ---------------------------------------------------------------------------
-// Wave-cooperative trace.  Lanes descend their own rays to a leaf (dynamic
-// ray fetch at leaf boundaries, as wf_trace_dyn); then the whole wave tests
-// the UNION of its lanes' leaf entries, 64 (ray, entry) pairs per round, so a
-// lane with a 40-entry leaf no longer idles 63 others.  Pair p belongs to the
-// lane j with start_j <= p < start_j + count_j (wave prefix sum, found by a
-// 6-step shuffle binary search); the owner's ray comes by __shfl.  Plane-test
-// survivors (dn != 0, 1e-5 <= s < leaf exit) are compacted into an LDS list
-// and run through the barycentric test 64 at a time.  A hit posts
-// (bits(s) << 32 | entry) to the owner's 64-bit LDS key with atomicMin:
-// s > 0, so the key order is (s, entry order) — exactly the first-wins
-// strict-< scan of trace_leaf_node (rt/trace_ray.cuh:124-141).  The owner
-// then recomputes the winner's barycentrics with the same arithmetic.
-#define WF_COOP_LIST 128
+#include "coop_trace.h"
 
-namespace {
-
-struct CoopTest { // the barycentric part of intersect_triangle for leaf entry k at parameter s
-    __device__ static __forceinline__ bool bary(const RtDevScene &sc, uint32_t k, Vec3D o, Vec3D d, float s,
-                                                float &cx, float &cy, float &cz, int &tri)
-    {
-        const RtF4 B = ldf4(sc.isect_b + k), C = ldf4(sc.isect_c + k), D = ldf4(sc.isect_d + k);
-        const uint2 R = *reinterpret_cast<const uint2 *>(sc.isect_rt + 2 * (size_t)k);
-        const float rd = __uint_as_float(R.x);
-        const float px = o.x + d.x * s, py = o.y + d.y * s, pz = o.z + d.z * s;
-        const float v2x = px - B.x, v2y = py - B.y, v2z = pz - B.z;
-        const float d20 = v2x * C.x + v2y * C.y + v2z * C.z;
-        const float d21 = v2x * D.x + v2y * D.y + v2z * D.z;
-        cy = (D.w * d20 - C.w * d21) * rd;
-        cz = (B.w * d21 - C.w * d20) * rd;
-        cx = 1.0f - cy - cz;
-        tri = (int)R.y;
-        return cx >= 0.0f && cx <= 1.0f && cy >= 0.0f && cy <= 1.0f && cz >= 0.0f && cz <= 1.0f;
-    }
-};
-
-} // namespace
-
+// Wave-cooperative trace with dynamic ray fetch (coop_trace.h): lanes whose
+// ray finished take the next queued ray at the next leaf boundary.
 template <bool COUNT>
 __global__ void __launch_bounds__(WF_BLOCK) wf_trace_coop(RtDevScene sc, WfState st, int q,
                                                           unsigned long long *counters)
@@ -365,14 +336,17 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_trace_coop(RtDevScene sc, WfState
     const RtF4 *rays = st.q_ray[q];
     uint32_t *fetch = st.counts + 2 + q;
 
-    bool live = false, exhausted = false;
-    uint32_t e = 0, node = 0;
-    int sp = 0;
-    Vec3D o = rt_v3(0, 0, 0), d = rt_v3(0, 0, 0);
-    float entry = 0.0f, exit_ = 0.0f, root_exit = 0.0f;
+    CoopRay r;
+    r.live = false;
+    r.o = r.d = rt_v3(0, 0, 0);
+    r.entry = r.exit_ = r.root_exit = 0.0f;
+    r.node = 0;
+    r.sp = 0;
+    bool exhausted = false;
+    uint32_t e = 0;
     while (true) {
         // ---- refill idle lanes (dynamic ray fetch)
-        const bool need = !live && !exhausted;
+        const bool need = !r.live && !exhausted;
         const unsigned long long m = __ballot(need);
         if (m) {
             const int leader = __ffsll((long long)m) - 1;
@@ -384,139 +358,20 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_trace_coop(RtDevScene sc, WfState
                 if (e >= n) {
                     exhausted = true;
                 } else {
-                    o = ld3(ldf4(rays + 2 * (size_t)e));
-                    d = ld3(ldf4(rays + 2 * (size_t)e + 1));
                     if (COUNT) c.v[RT_CNT_RAY]++;
-                    if (bbox_hit(sc, o, d, entry, exit_)) {
-                        root_exit = exit_;
-                        node = 0;
-                        sp = 0;
-                        live = true;
-                    } else {
+                    if (!coop_begin(sc, r, ld3(ldf4(rays + 2 * (size_t)e)), ld3(ldf4(rays + 2 * (size_t)e + 1))))
                         *reinterpret_cast<float4 *>(st.hits + e) = make_float4(__int_as_float(-1), 0.f, 0.f, 0.f);
-                    }
                 }
             }
         }
-        if (!__any(live)) {
+        if (!__any(r.live)) {
             if (__all(exhausted)) break;
             continue;
         }
-        // ---- descend to a leaf (rt/trace_ray.cuh:273-306), per lane
-        uint32_t leaf_begin = 0;
-        int leaf_count = 0;
-        if (live) {
-            uint2 nd = *reinterpret_cast<const uint2 *>(sc.nodes + 2 * (size_t)node);
-            if (COUNT) c.v[RT_CNT_NODE]++;
-            while ((nd.y & 3u) != RT_LEAF_TAG) {
-                const uint32_t axis = nd.y & 3u;
-                const float split = as_float(nd.x);
-                const float oax = axis == 0 ? o.x : (axis == 1 ? o.y : o.z);
-                const float dax = axis == 0 ? d.x : (axis == 1 ? d.y : d.z);
-                uint32_t near_c = node + 1, far_c = nd.y >> 2;
-                if (oax >= split) {
-                    near_c = nd.y >> 2;
-                    far_c = node + 1;
-                }
-                const float t = (split - oax) / dax;
-                if (t >= exit_ || t < 0) {
-                    node = near_c;
-                } else if (t <= entry) {
-                    node = far_c;
-                } else {
-                    stk.put(sp, far_c, t);
-                    ++sp;
-                    node = near_c;
-                    exit_ = t;
-                }
-                nd = *reinterpret_cast<const uint2 *>(sc.nodes + 2 * (size_t)node);
-                if (COUNT) c.v[RT_CNT_NODE]++;
-            }
-            leaf_begin = nd.x;
-            leaf_count = (int)(nd.y >> 2);
-            if (COUNT) c.v[RT_CNT_TRI] += (unsigned long long)leaf_count;
-        }
-        // ---- wave-cooperative leaf tests (all 64 lanes active from here)
-        int start = leaf_count; // inclusive scan -> exclusive
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const int v = __shfl_up(start, off);
-            if (lane >= off) start += v;
-        }
-        const int total = __shfl(start, 63);
-        start -= leaf_count;
-        wkey[lane] = ~0ull;
-        int list_n = 0;
-        for (int base = 0; base < total || list_n > 0; base += 64) {
-            if (base < total) {
-                const int p = base + lane;
-                int j = 0; // owner: largest lane with start_j <= p
-#pragma unroll
-                for (int step = 32; step >= 1; step >>= 1) {
-                    const int sv = __shfl(start, j + step);
-                    if (sv <= p) j += step;
-                }
-                const uint32_t k = (uint32_t)__shfl((int)leaf_begin, j) + (uint32_t)(p - __shfl(start, j));
-                const Vec3D oo = rt_v3(__shfl(o.x, j), __shfl(o.y, j), __shfl(o.z, j));
-                const Vec3D dd = rt_v3(__shfl(d.x, j), __shfl(d.y, j), __shfl(d.z, j));
-                const float ex = __shfl(exit_, j);
-                bool pass = false;
-                float s = 0.0f;
-                if (p < total) {
-                    const RtF4 A = ldf4(sc.isect_a + k); // n, d
-                    const float dn = dd.x * A.x + dd.y * A.y + dd.z * A.z;
-                    s = (A.w - (oo.x * A.x + oo.y * A.y + oo.z * A.z)) / dn;
-                    pass = dn != 0 && s >= 0.00001f && s < ex;
-                }
-                const unsigned long long pm = __ballot(pass);
-                if (pass) list[list_n + __popcll(pm & ((1ull << lane) - 1ull))] = make_uint2((k << 6) | (uint32_t)j,
-                                                                                             __float_as_uint(s));
-                list_n += __popcll(pm);
-            }
-            // barycentric stage over up to 64 listed candidates
-            if (list_n >= 64 || (base + 64 >= total && list_n > 0)) {
-                const int take = list_n < 64 ? list_n : 64;
-                const bool act = lane < take;
-                const uint2 it = list[lane < take ? lane : 0];
-                const int j = (int)(it.x & 63u);
-                const Vec3D oo = rt_v3(__shfl(o.x, j), __shfl(o.y, j), __shfl(o.z, j));
-                const Vec3D dd = rt_v3(__shfl(d.x, j), __shfl(d.y, j), __shfl(d.z, j));
-                if (act) {
-                    float cx, cy, cz;
-                    int tri;
-                    const float s = __uint_as_float(it.y);
-                    if (CoopTest::bary(sc, it.x >> 6, oo, dd, s, cx, cy, cz, tri))
-                        atomicMin(wkey + j, ((unsigned long long)it.y << 32) | (it.x >> 6));
-                }
-                // move the rest (< 64) to the front
-                const int rest = list_n - take;
-                uint2 mv = make_uint2(0, 0);
-                if (lane < rest) mv = list[take + lane];
-                if (lane < rest) list[lane] = mv;
-                list_n = rest;
-            }
-        }
-        // ---- per-lane result: winner, or pop, or miss
-        const unsigned long long key = wkey[lane];
-        if (live) {
-            if (key != ~0ull) {
-                const uint32_t k = (uint32_t)key;
-                float cx, cy, cz;
-                int tri;
-                CoopTest::bary(sc, k, o, d, __uint_as_float((uint32_t)(key >> 32)), cx, cy, cz, tri);
-                if (COUNT) c.v[RT_CNT_HIT]++;
-                *reinterpret_cast<float4 *>(st.hits + e) = make_float4(__int_as_float(tri), cx, cy, cz);
-                live = false;
-            } else if (sp == 0) {
-                *reinterpret_cast<float4 *>(st.hits + e) = make_float4(__int_as_float(-1), 0.f, 0.f, 0.f);
-                live = false;
-            } else {
-                --sp;
-                node = stk.node_at(sp);
-                entry = stk.entry_at(sp);
-                exit_ = sp > 0 ? stk.entry_at(sp - 1) : root_exit;
-            }
-        }
+        int tri = -1;
+        float bx = 0.0f, by = 0.0f, bz = 0.0f;
+        if (coop_step<COUNT>(sc, r, stk, wkey, list, tri, bx, by, bz, c))
+            *reinterpret_cast<float4 *>(st.hits + e) = make_float4(__int_as_float(tri), bx, by, bz);
     }
     if (COUNT) flush_counters(c, counters);
 }
@@ -721,6 +576,97 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_finish(RtDevScene sc, RtDevFrame 
     if (COUNT) flush_counters(c, fr.counters);
 }
 
+// Cooperative finisher: runs queued paths to the end of their passes in
+// registers (shade_step right after each ray query), megakernel style, while
+// the whole wave tests leaf entries for its live rays together (coop_step).
+// Each wave keeps up to `ppw` (1..64) paths in flight, one per lane; a lane
+// whose path is done takes the next queue entry (wave-aggregated atomic on
+// counts[4]).  With ppw = 1 a lone long glass path gets its leaves tested 64
+// entries at a time instead of one.
+template <bool COUNT>
+__global__ void __launch_bounds__(WF_BLOCK) wf_finish_coop(RtDevScene sc, RtDevFrame fr, RtDevCamera cam, WfState st,
+                                                           int q, int ppw)
+{
+    __shared__ uint32_t s_node[WF_LDS_STACK * WF_BLOCK];
+    __shared__ float s_entry[WF_LDS_STACK * WF_BLOCK];
+    __shared__ unsigned long long s_key[WF_BLOCK];
+    __shared__ uint2 s_list[(WF_BLOCK / 64) * WF_COOP_LIST];
+    const int tid = threadIdx.x;
+    const int gtid = blockIdx.x * WF_BLOCK + tid;
+    const int lane = __lane_id();
+    const int wave = tid >> 6;
+    Stack<WF_LDS_STACK> stk{s_node + tid, s_entry + tid, WF_BLOCK, st.spill + gtid, st.spill_threads};
+    unsigned long long *wkey = s_key + wave * 64;
+    uint2 *list = s_list + wave * WF_COOP_LIST;
+    Cnt c;
+    if (COUNT) c.zero();
+    const uint32_t n = st.counts[q];
+    uint32_t *fetch = st.counts + 4;
+    const int limit = fr.max_depth > 0 ? fr.max_depth : RT_WATCHDOG_BOUNCES;
+
+    PathRegs p;
+    p.slot = 0;
+    p.ro = p.rd = rt_v3(0, 0, 0);
+    CoopRay r;
+    r.live = false;
+    r.o = r.d = rt_v3(0, 0, 0);
+    r.entry = r.exit_ = r.root_exit = 0.0f;
+    r.node = 0;
+    r.sp = 0;
+    int hit = -1;
+    float bx = 0.0f, by = 0.0f, bz = 0.0f;
+    bool active = false;              // the lane holds a path
+    bool exhausted = lane >= ppw;     // no more queue entries for this lane
+    bool pending = false;             // a finished ray query waiting for shade_step
+    while (true) {
+        // ---- idle lanes take the next queued paths
+        const bool need = !active && !exhausted;
+        const unsigned long long m = __ballot(need);
+        if (m) {
+            const int leader = __ffsll((long long)m) - 1;
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(fetch, (uint32_t)__popcll(m));
+            base = __shfl(base, leader);
+            if (need) {
+                const uint32_t e = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+                if (e >= n) {
+                    exhausted = true;
+                } else {
+                    active = true;
+                    load_regs(st, fr, st.q_slot[q][e], p);
+                    p.ro = ld3(ldf4(st.q_ray[q] + 2 * (size_t)e));
+                    p.rd = ld3(ldf4(st.q_ray[q] + 2 * (size_t)e + 1));
+                    if (COUNT) c.v[RT_CNT_RAY]++;
+                    if (!coop_begin(sc, r, p.ro, p.rd)) {
+                        pending = true;
+                        hit = -1;
+                    }
+                }
+            }
+        }
+        while (pending) { // shade, and start the path's next ray (a scene-box miss is shaded at once)
+            pending = false;
+            if (shade_step<COUNT>(sc, fr, cam, p, hit, bx, by, bz, limit, c)) {
+                if (COUNT) c.v[RT_CNT_RAY]++;
+                if (!coop_begin(sc, r, p.ro, p.rd)) {
+                    pending = true;
+                    hit = -1;
+                }
+            } else {
+                store_regs(st, fr, p);
+                active = false;
+            }
+        }
+        // here every active lane has a live ray
+        if (!__any(r.live)) {
+            if (__all(exhausted)) break;
+            continue;
+        }
+        if (coop_step<COUNT>(sc, r, stk, wkey, list, hit, bx, by, bz, c)) pending = true;
+    }
+    if (COUNT) flush_counters(c, fr.counters);
+}
+
 // ---------------------------------------------------------------- launcher
 namespace {
 
@@ -780,7 +726,7 @@ int ensure(Workspace &w, size_t slots, int grid)
 } // namespace
 
 int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevCamera &cam, hipStream_t stream,
-                        int variant)
+                        int variant, int tail_opt, int finish_waves_opt)
 {
     // 1: wave-cooperative leaves (entries packed as k << 6 | lane: needs < 2^26 entries), 2: static, 3: per-lane fetch
     int trace_kind = variant;
@@ -797,10 +743,31 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
     if (count) hipLaunchKernelGGL(wf_start<true>, dim3(tiles), dim3(WF_BLOCK), 0, stream, fr, cam, w.st);
     else hipLaunchKernelGGL(wf_start<false>, dim3(tiles), dim3(WF_BLOCK), 0, stream, fr, cam, w.st);
     // below this many live paths the rest of the call runs in one wf_finish launch
-    static const uint32_t tail = [] {
-        const char *e = getenv("RT_WF_TAIL");
-        return e ? (uint32_t)atoi(e) : 65536u;
-    }();
+    const uint32_t tail = tail_opt > 0 ? (uint32_t)tail_opt : WF_TAIL_DEFAULT;
+    // the cooperative finisher runs on at most this many waves (up to 64 paths in flight each)
+    const uint32_t finish_waves = finish_waves_opt > 0 ? (uint32_t)finish_waves_opt : WF_FINISH_WAVES_DEFAULT;
+    static const bool trace_iters = getenv("RT_WF_TRACE_ITERS") != nullptr; // debug: per-iteration queue sizes
+    // run the `live` paths of queue qq to the end of the call in wf_finish_coop
+    auto finish_coop = [&](int qq, uint32_t live) -> int {
+        // paths per wave: spread over up to finish_waves waves, within the spill area (grid * WF_BLOCK threads)
+        const uint32_t max_waves = (uint32_t)grid * (WF_BLOCK / 64);
+        uint32_t ppw = (live + finish_waves - 1) / finish_waves;
+        ppw = ppw < 1 ? 1 : (ppw > 64 ? 64 : ppw);
+        uint32_t waves = (live + ppw - 1) / ppw;
+        if (waves > finish_waves) waves = finish_waves;
+        if (waves > max_waves) waves = max_waves; // persistent: lanes fetch paths until the queue is empty
+        if (hipMemsetAsync(w.st.counts + 4, 0, 4, stream) != hipSuccess) return -1;
+        const int fgrid = (int)((waves + WF_BLOCK / 64 - 1) / (WF_BLOCK / 64));
+        if (count)
+            hipLaunchKernelGGL(wf_finish_coop<true>, dim3(fgrid), dim3(WF_BLOCK), 0, stream, sc, fr, cam, w.st, qq,
+                               (int)ppw);
+        else
+            hipLaunchKernelGGL(wf_finish_coop<false>, dim3(fgrid), dim3(WF_BLOCK), 0, stream, sc, fr, cam, w.st, qq,
+                               (int)ppw);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    };
+    // wf_tail above the frame size: the whole call runs in the finisher (no queue iterations)
+    if (trace_kind == 1 && tail > slots) return finish_coop(0, (uint32_t)slots);
     for (int it = 0;; ++it) {
         const int q = it & 1;
         if (hipMemsetAsync(w.st.counts + (q ^ 1), 0, 4, stream) != hipSuccess) return -1;
@@ -823,8 +790,14 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
             return -1;
         if (hipStreamSynchronize(stream) != hipSuccess) return -1;
         const uint32_t live = *w.host_count;
+        if (trace_iters) {
+            timespec ts;
+            clock_gettime(CLOCK_MONOTONIC, &ts);
+            fprintf(stderr, "[wf] it %d live %u t %.4f\n", it, live, ts.tv_sec + ts.tv_nsec * 1e-9);
+        }
         if (live == 0) break;
         if (live < tail) {
+            if (trace_kind == 1) return finish_coop(q ^ 1, live);
             const int fgrid = (int)((live + WF_BLOCK - 1) / WF_BLOCK);
             if (count) hipLaunchKernelGGL(wf_finish<true>, dim3(fgrid), dim3(WF_BLOCK), 0, stream, sc, fr, cam, w.st, q ^ 1);
             else hipLaunchKernelGGL(wf_finish<false>, dim3(fgrid), dim3(WF_BLOCK), 0, stream, sc, fr, cam, w.st, q ^ 1);

@@ -50,7 +50,8 @@ class RtOptions(ctypes.Structure):
     _fields_ = [("width", ctypes.c_int), ("height", ctypes.c_int), ("passes", ctypes.c_int),
                 ("adaptive", ctypes.c_int), ("min_samples", ctypes.c_int), ("tolerance", ctypes.c_float),
                 ("max_depth", ctypes.c_int), ("kernel", ctypes.c_int), ("stream", ctypes.c_void_p),
-                ("counters_device", ctypes.c_void_p), ("wave_times_device", ctypes.c_void_p)]
+                ("counters_device", ctypes.c_void_p), ("wave_times_device", ctypes.c_void_p),
+                ("wf_tail", ctypes.c_int), ("wf_finish_waves", ctypes.c_int)]
 
 
 TRIANGLE_BYTES = 152
@@ -268,7 +269,7 @@ KERNEL_WAVEFRONT = 1
 
 
 def options(width, height, passes=1, adaptive=True, min_samples=100, tolerance=0.05, max_depth=0, stream=None,
-            counters=None, kernel=KERNEL_MEGA):
+            counters=None, kernel=KERNEL_MEGA, wf_tail=0, wf_finish_waves=0):
     o = RtOptions()
     lib().rt_default_options(ctypes.byref(o))
     o.width, o.height, o.passes = width, height, passes
@@ -276,6 +277,7 @@ def options(width, height, passes=1, adaptive=True, min_samples=100, tolerance=0
     o.kernel = kernel
     o.stream = stream
     o.counters_device = counters
+    o.wf_tail, o.wf_finish_waves = wf_tail, wf_finish_waves
     return o
 
 

@@ -70,6 +70,21 @@ def test_other_trace_variants(variant):
     assert gcnt == rcnt
 
 
+@pytest.mark.parametrize("tail,waves", [(1 << 30, 3), (1 << 30, 1 << 20), (700, 5), (1, 0)],
+                         ids=["finisher-only-refetch", "finisher-only-1-per-wave", "late-handoff-refetch",
+                              "queues-only"])
+def test_wavefront_finisher_modes(tail, waves):
+    """The cooperative finisher (wf_finish_coop) at every hand-off point and
+    width: whole call in the finisher with few waves (lanes refetch paths) or
+    one path per wave, a late hand-off, and no finisher at all."""
+    run = helpers.GpuRun("room_small")
+    W, H, P = 48, 27, 3
+    gpu, gcnt, _ = run.render(W, H, P, count=True, kernel=rt.KERNEL_WAVEFRONT, wf_tail=tail, wf_finish_waves=waves)
+    ref, rcnt = helpers.oracle_render(run.path, W, H, P)
+    helpers.assert_bitwise(gpu, ref, what=f"finisher tail={tail} waves={waves}")
+    assert gcnt == rcnt
+
+
 def test_kernels_agree_multi_call(cornell):
     """Megakernel and wavefront give the same bits across calls with reset."""
     W, H = 33, 31

@@ -1,7 +1,8 @@
 """A/B kernel variants in ONE process, interleaved rounds (guide §5.4 rule 24).
 
 usage: python tools/ab.py SCENE PASSES MAX_DEPTH ROUNDS VARIANT[,VARIANT...]
-  VARIANT = kernel id (0 mega, 1 wavefront+dynamic fetch, 2 wavefront static)
+  VARIANT = KERNEL[:WF_TAIL[:WF_FINISH_WAVES]]; KERNEL 0 mega, 1 wavefront
+            (cooperative leaves), 2 wavefront static, 3 wavefront lane fetch
 Prints per-variant Msamples/s (median, min, max) at 1920x1080 and the work
 counters of one counted run.
 """
@@ -21,14 +22,20 @@ import rt  # noqa: E402
 
 def main():
     scene, P, maxd, rounds = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])
-    variants = [int(v) for v in sys.argv[5].split(",")]
+    variants = sys.argv[5].split(",")
+
+    def opts(v, **kw):
+        f = [int(x) for x in v.split(":")] + [0, 0]
+        return rt.options(W, H, P, adaptive=False, max_depth=maxd, kernel=f[0], wf_tail=f[1], wf_finish_waves=f[2],
+                          **kw)
+
     W, H = int(os.environ.get("AB_W", 1920)), int(os.environ.get("AB_H", 1080))
     run = helpers.GpuRun(scene)
     g = rt.GBuffer(W, H)
     times = {v: [] for v in variants}
     for r in range(rounds):
         for v in variants:
-            opt = rt.options(W, H, P, adaptive=False, max_depth=maxd, kernel=v)
+            opt = opts(v)
             rt.check(rt.lib().rt_synchronize())
             t = time.perf_counter()
             rt.render(run.dev, g, run.camera, 0, opt)
@@ -36,7 +43,7 @@ def main():
     out = {}
     for v in variants:
         cnt = rt.DeviceCounters()
-        opt = rt.options(W, H, P, adaptive=False, max_depth=maxd, kernel=v, counters=cnt.p)
+        opt = opts(v, counters=cnt.p)
         rt.render(run.dev, g, run.camera, 0, opt)
         c = cnt.read()
         ts = np.array(times[v])
