@@ -1,17 +1,20 @@
 """Bench: Msamples/s of the render hot path at 1920x1080 (BASELINE.json metric).
 
 Workload (BASELINE.json configs[2]): the README-like 2M-triangle synthetic
-room ("room2m": room + 1,999,392-triangle displaced gold mesh + two glass
+room ("room2m": room + 1,997,568-triangle displaced gold mesh + two glass
 spheres + emissive quad), 1920x1080, adaptive sampling off.  One step = one
-rt_render call of `--passes` passes (spp) over the full frame.  With --gpus N
+rt_render call of `--passes` passes (spp) over the full frame (default 64:
+16 steps are the config's 1024 spp).  With --gpus N
 each rank renders its own spp slice (seeds = mt19937 outputs [rank*W*H,
 (rank+1)*W*H)) and one RCCL reduce (sum) of fb/sq/count into
 rank 0 plus the tonemap closes the timed region.  value = samples of all ranks
 / max-over-ranks wall time.
 
-Also reported: the kernel roofline (SURVEY §8d algorithmic bytes from the
-work counters / HIP-event kernel time, against 8 TB/s HBM) and the CPU
-oracle's rate on a bounded pixel sample (rank 0, N=1).
+Also reported: the roofline of the dominant kernel (wavefront: wf_trace_coop,
+whose SURVEY §8d traversal bytes 8*node + 40*tri come from the work counters
+of one counted call, over its launches' HIP-event time inside the timed
+steps, against 8 TB/s HBM) and the CPU oracle's rate on a bounded pixel
+sample (rank 0, N=1).
 """
 import argparse
 import ctypes
@@ -50,6 +53,19 @@ class TorchGBuffer:
         self.g = rt.G_Buffer(self.fb.data_ptr(), self.sq.data_ptr(), self.cnt.data_ptr(), self.rng.data_ptr())
 
 
+def pmc_traffic(kernel_name):
+    """HBM bytes per launch of `kernel_name` from the newest committed rocprofv3
+    PMC summary (profiles/r*/pmc_traffic_*.json: FETCH_SIZE / WRITE_SIZE passes
+    of this bench command, corrected as MI355X_MICROARCH.md prescribes)."""
+    import glob
+
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic_*.json")), reverse=True):
+        d = json.load(open(f))
+        if d.get("kernel") == kernel_name:
+            return d["traffic_bytes_per_launch"], os.path.relpath(f, ROOT)
+    return None, None
+
+
 def cpu_baseline(scene_path, W, H, seconds, threads):
     import oracle
 
@@ -80,15 +96,15 @@ def cpu_baseline(scene_path, W, H, seconds, threads):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=8)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--passes", type=int, default=8, help="spp per step (passes per rt_render call)")
+    ap.add_argument("--steps", type=int, default=4)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--passes", type=int, default=64, help="spp per step (passes per rt_render call)")
     ap.add_argument("--scene", default="room2m")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--kernel", choices=["mega", "wavefront"], default="mega")
+    ap.add_argument("--kernel", choices=["mega", "wavefront"], default="wavefront")
     ap.add_argument("--scene-dir", default=os.environ.get("RT_SCENE_DIR", os.path.join(ROOT, "build", "scenes")))
     args = ap.parse_args()
 
@@ -122,13 +138,19 @@ def main():
     gb = TorchGBuffer(torch, n, shard.seed_skip(rank, W, H))
     stream = torch.cuda.current_stream()
     kernel = rt.KERNEL_WAVEFRONT if args.kernel == "wavefront" else rt.KERNEL_MEGA
-    opt = rt.options(W, H, P, adaptive=False, stream=ctypes.c_void_p(stream.cuda_stream), kernel=kernel)
+    wavefront = kernel == rt.KERNEL_WAVEFRONT
+    opt = rt.options(W, H, P, adaptive=False, stream=ctypes.c_void_p(stream.cuda_stream), kernel=kernel,
+                     profile=wavefront)
+    profiles = []
 
     def step(i):
         rt.render(dscene, gb, host.camera, 0 if i == 0 else 1, opt)
+        if wavefront:
+            profiles.append(rt.last_profile())
 
     for i in range(args.warmup):
         step(i)
+    profiles.clear()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -162,18 +184,43 @@ def main():
     expect = world * P * (args.warmup + args.steps)
     got = int(gb.cnt.sum().item()) if rank == 0 else None
 
-    # work counters on one extra (untimed) step -> algorithmic bytes per launch
+    # work counters on one extra (untimed) step -> algorithmic bytes per call
     counters = rt.DeviceCounters()
-    copt = rt.options(W, H, P, adaptive=False, counters=counters.p, kernel=kernel)
+    copt = rt.options(W, H, P, adaptive=False, counters=counters.p, kernel=kernel, profile=wavefront)
     rt.render(dscene, gb, host.camera, 1, copt)
-    c = counters.read()
-    bytes_per_launch = algorithmic_bytes(c)
-    achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
+    c = counters.read(finisher=True)
+    bytes_per_call = algorithmic_bytes(c)
+    if wavefront:
+        # dominant kernel: wf_trace_coop.  Its traversal bytes per call (the
+        # finisher's share taken out) over its summed launch time per call.
+        cprof = rt.last_profile()
+        trace_bytes = 8 * (c["node"] - c["finish_node"]) + 40 * (c["tri"] - c["finish_tri"])
+        launches = sum(p["trace_launches"] for p in profiles)
+        trace_ms_call = float(np.mean([p["trace_ms"] for p in profiles]))
+        achieved = trace_bytes / (trace_ms_call * 1e-3) / 1e9
+        roof_kernel = "wf_trace_coop<false>"
+        kernel_detail = {
+            "trace_launches_per_call": launches / len(profiles),
+            "avg_launch_ms": round(sum(p["trace_ms"] for p in profiles) / max(launches, 1), 4),
+            "trace_ms_per_call": round(trace_ms_call, 3),
+            "shade_ms_per_call": round(float(np.mean([p["shade_ms"] for p in profiles])), 3),
+            "finish_ms_per_call": round(float(np.mean([p["finish_ms"] for p in profiles])), 3),
+            "call_ms": round(float(np.mean([p["call_ms"] for p in profiles])), 3),
+            "trace_bytes_per_call": trace_bytes,
+            "trace_bytes_per_launch": round(trace_bytes / max(cprof["trace_launches"], 1)),
+            "finisher_ray_share": round(c["finish_ray"] / max(c["ray"], 1), 4),
+            "call_achieved_GBps": round(bytes_per_call / (kernel_ms * 1e-3) / 1e9, 1),
+        }
+    else:
+        achieved = bytes_per_call / (kernel_ms * 1e-3) / 1e9
+        roof_kernel = "rt_path_kernel<false,20>"
+        kernel_detail = {"kernel_ms": round(kernel_ms, 3)}
 
     if rank != 0:
         if dist:
             dist.destroy_process_group()
         return
+    traffic, traffic_src = pmc_traffic(roof_kernel)
     line = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -200,11 +247,12 @@ def main():
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4),
-            "traffic": None,
-            "kernel": "rt_path_kernel<false,20>" if kernel == rt.KERNEL_MEGA else "wf_trace+wf_shade (per render call)",
-            "kernel_ms": round(kernel_ms, 3),
-            "algorithmic_bytes_per_launch": bytes_per_launch,
-            "bytes_per_sample": round(bytes_per_launch / max(c["sample"], 1), 1),
+            "traffic": traffic,
+            "traffic_source": traffic_src,
+            "kernel": roof_kernel,
+            **kernel_detail,
+            "call_algorithmic_bytes": bytes_per_call,
+            "bytes_per_sample": round(bytes_per_call / max(c["sample"], 1), 1),
         },
         "per_sample": {k: round(c[k] / max(c["sample"], 1), 3) for k in ("ray", "node", "tri", "hit", "nee")},
         "samples_check": {"accumulated": got, "expected": expect * n},

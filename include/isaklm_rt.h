@@ -233,6 +233,11 @@ enum {
     RT_CNT_RAY = 7,    /* trace_ray calls */
     RT_CNT_WATCHDOG = 8, /* paths cut by the bounce watchdog */
     RT_CNT_MAXDEPTH = 9, /* longest path (extension rays) seen: atomic max, not a sum */
+    /* the part of NODE / TRI / RAY done by the wavefront finisher launch
+     * (already included in the totals above) */
+    RT_CNT_FIN_NODE = 10,
+    RT_CNT_FIN_TRI = 11,
+    RT_CNT_FIN_RAY = 12,
     RT_CNT_COUNT = 16
 };
 
@@ -256,7 +261,22 @@ typedef struct RtOptions {
      * the finisher (persistent per-wave path fetch, no queue iterations) */
     int wf_tail;
     int wf_finish_waves;
+    int profile;         /* 1: time the wavefront kernels with HIP events (rt_last_profile) */
 } RtOptions;
+
+/* Per-call kernel timing of the last rt_render on this device with
+ * RtOptions.profile = 1 (wavefront kernels; HIP events on the call's stream,
+ * the call waits for its last event). */
+typedef struct RtProfile {
+    int iterations;      /* trace/shade queue iterations */
+    int trace_launches, shade_launches, finish_launches;
+    float start_ms;      /* wf_start */
+    float trace_ms;      /* sum over the call's trace launches */
+    float shade_ms;      /* sum over the call's shade launches */
+    float finish_ms;     /* the finisher launch (0 or 1 per call) */
+    float call_ms;       /* first to last event of the call */
+} RtProfile;
+int rt_last_profile(RtProfile *out);
 
 void rt_default_options(RtOptions *opt);
 /* render(): if sample_count == 0 the frame's fb/sq/count are reset first

@@ -446,6 +446,16 @@ __device__ __forceinline__ void flush_counters(Cnt &c, unsigned long long *out)
     }
 }
 
+// after flush_counters: the finisher's share of node / tri / ray
+__device__ __forceinline__ void flush_finish_counters(const Cnt &c, unsigned long long *out)
+{
+    if ((threadIdx.x & 63) == 0) {
+        if (c.v[RT_CNT_NODE]) atomicAdd(out + RT_CNT_FIN_NODE, c.v[RT_CNT_NODE]);
+        if (c.v[RT_CNT_TRI]) atomicAdd(out + RT_CNT_FIN_TRI, c.v[RT_CNT_TRI]);
+        if (c.v[RT_CNT_RAY]) atomicAdd(out + RT_CNT_FIN_RAY, c.v[RT_CNT_RAY]);
+    }
+}
+
 // per-wave [start, end] s_memrealtime stamps (100 MHz) into a debug buffer
 __device__ __forceinline__ unsigned long long realtime() { return __builtin_amdgcn_s_memrealtime(); }
 

@@ -573,7 +573,10 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_finish(RtDevScene sc, RtDevFrame 
             store_regs(st, fr, p);
         }
     }
-    if (COUNT) flush_counters(c, fr.counters);
+    if (COUNT) {
+        flush_counters(c, fr.counters);
+        flush_finish_counters(c, fr.counters);
+    }
 }
 
 // Cooperative finisher: runs queued paths to the end of their passes in
@@ -664,7 +667,10 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_finish_coop(RtDevScene sc, RtDevF
         }
         if (coop_step<COUNT>(sc, r, stk, wkey, list, hit, bx, by, bz, c)) pending = true;
     }
-    if (COUNT) flush_counters(c, fr.counters);
+    if (COUNT) {
+        flush_counters(c, fr.counters);
+        flush_finish_counters(c, fr.counters);
+    }
 }
 
 // ---------------------------------------------------------------- launcher
@@ -676,6 +682,9 @@ struct Workspace {
     WfState st{};
     void *blob = nullptr;
     uint32_t *host_count = nullptr;
+    hipEvent_t ev[6] = {};   // RtOptions.profile
+    bool ev_ok = false;
+    RtProfile prof{};        // last profiled call
 };
 
 std::map<int, Workspace> g_ws; // per device
@@ -723,10 +732,26 @@ int ensure(Workspace &w, size_t slots, int grid)
     return 0;
 }
 
+float elapsed_ms(hipEvent_t a, hipEvent_t b)
+{
+    float ms = 0.0f;
+    return hipEventElapsedTime(&ms, a, b) == hipSuccess ? ms : 0.0f;
+}
+
 } // namespace
 
+extern "C" int rt_last_profile(RtProfile *out)
+{
+    if (!out) return RT_E_INVALID;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return RT_E_HIP;
+    auto it = g_ws.find(dev);
+    *out = it == g_ws.end() ? RtProfile{} : it->second.prof;
+    return RT_OK;
+}
+
 int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevCamera &cam, hipStream_t stream,
-                        int variant, int tail_opt, int finish_waves_opt)
+                        int variant, int tail_opt, int finish_waves_opt, int profile)
 {
     // 1: wave-cooperative leaves (entries packed as k << 6 | lane: needs < 2^26 entries), 2: static, 3: per-lane fetch
     int trace_kind = variant;
@@ -738,72 +763,107 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
     const size_t slots = (size_t)fr.width * fr.height;
     if (ensure(w, slots, grid) != 0) return -1;
     const bool count = fr.counters != nullptr;
+    const bool prof = profile != 0;
+    if (prof && !w.ev_ok) {
+        for (auto &e : w.ev)
+            if (hipEventCreate(&e) != hipSuccess) return -1;
+        w.ev_ok = true;
+    }
+    RtProfile P{};
+    auto mark = [&](int i) { return !prof || hipEventRecord(w.ev[i], stream) == hipSuccess; };
+    if (!mark(0)) return -1;
     if (hipMemsetAsync(w.st.counts, 0, 64, stream) != hipSuccess) return -1;
     const int tiles = ((fr.width + 15) / 16) * ((fr.height + 15) / 16);
     if (count) hipLaunchKernelGGL(wf_start<true>, dim3(tiles), dim3(WF_BLOCK), 0, stream, fr, cam, w.st);
     else hipLaunchKernelGGL(wf_start<false>, dim3(tiles), dim3(WF_BLOCK), 0, stream, fr, cam, w.st);
-    // below this many live paths the rest of the call runs in one wf_finish launch
+    if (!mark(1)) return -1;
+    // below this many live paths the rest of the call runs in one finisher launch
     const uint32_t tail = tail_opt > 0 ? (uint32_t)tail_opt : WF_TAIL_DEFAULT;
     // the cooperative finisher runs on at most this many waves (up to 64 paths in flight each)
     const uint32_t finish_waves = finish_waves_opt > 0 ? (uint32_t)finish_waves_opt : WF_FINISH_WAVES_DEFAULT;
     static const bool trace_iters = getenv("RT_WF_TRACE_ITERS") != nullptr; // debug: per-iteration queue sizes
-    // run the `live` paths of queue qq to the end of the call in wf_finish_coop
-    auto finish_coop = [&](int qq, uint32_t live) -> int {
-        // paths per wave: spread over up to finish_waves waves, within the spill area (grid * WF_BLOCK threads)
-        const uint32_t max_waves = (uint32_t)grid * (WF_BLOCK / 64);
-        uint32_t ppw = (live + finish_waves - 1) / finish_waves;
-        ppw = ppw < 1 ? 1 : (ppw > 64 ? 64 : ppw);
-        uint32_t waves = (live + ppw - 1) / ppw;
-        if (waves > finish_waves) waves = finish_waves;
-        if (waves > max_waves) waves = max_waves; // persistent: lanes fetch paths until the queue is empty
-        if (hipMemsetAsync(w.st.counts + 4, 0, 4, stream) != hipSuccess) return -1;
-        const int fgrid = (int)((waves + WF_BLOCK / 64 - 1) / (WF_BLOCK / 64));
-        if (count)
-            hipLaunchKernelGGL(wf_finish_coop<true>, dim3(fgrid), dim3(WF_BLOCK), 0, stream, sc, fr, cam, w.st, qq,
-                               (int)ppw);
-        else
-            hipLaunchKernelGGL(wf_finish_coop<false>, dim3(fgrid), dim3(WF_BLOCK), 0, stream, sc, fr, cam, w.st, qq,
-                               (int)ppw);
-        return hipGetLastError() == hipSuccess ? 0 : -1;
-    };
-    // wf_tail above the frame size: the whole call runs in the finisher (no queue iterations)
-    if (trace_kind == 1 && tail > slots) return finish_coop(0, (uint32_t)slots);
-    for (int it = 0;; ++it) {
-        const int q = it & 1;
-        if (hipMemsetAsync(w.st.counts + (q ^ 1), 0, 4, stream) != hipSuccess) return -1;
-        if (hipMemsetAsync(w.st.counts + 2 + q, 0, 4, stream) != hipSuccess) return -1; // fetch cursor
-#define WF_LAUNCH_TRACE(C)                                                                                         \
-    do {                                                                                                           \
-        if (trace_kind == 1)                                                                                       \
-            hipLaunchKernelGGL(wf_trace_coop<C>, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, w.st, q, fr.counters); \
-        else if (trace_kind == 3)                                                                                  \
-            hipLaunchKernelGGL(wf_trace_dyn<C>, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, w.st, q, fr.counters);  \
-        else                                                                                                       \
-            hipLaunchKernelGGL(wf_trace<C>, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, w.st, q, fr.counters);      \
-        hipLaunchKernelGGL(wf_shade<C>, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, fr, cam, w.st, q);              \
-    } while (0)
-        if (count) WF_LAUNCH_TRACE(true);
-        else WF_LAUNCH_TRACE(false);
-#undef WF_LAUNCH_TRACE
-        if (hipGetLastError() != hipSuccess) return -1;
-        if (hipMemcpyAsync(w.host_count, w.st.counts + (q ^ 1), 4, hipMemcpyDeviceToHost, stream) != hipSuccess)
-            return -1;
-        if (hipStreamSynchronize(stream) != hipSuccess) return -1;
-        const uint32_t live = *w.host_count;
-        if (trace_iters) {
-            timespec ts;
-            clock_gettime(CLOCK_MONOTONIC, &ts);
-            fprintf(stderr, "[wf] it %d live %u t %.4f\n", it, live, ts.tv_sec + ts.tv_nsec * 1e-9);
-        }
-        if (live == 0) break;
-        if (live < tail) {
-            if (trace_kind == 1) return finish_coop(q ^ 1, live);
+    // run the `live` paths of queue qq to the end of the call in the finisher
+    auto finish = [&](int qq, uint32_t live) -> int {
+        if (!mark(2)) return -1;
+        if (trace_kind == 1) {
+            // paths per wave: spread over up to finish_waves waves, within the spill area (grid * WF_BLOCK threads)
+            const uint32_t max_waves = (uint32_t)grid * (WF_BLOCK / 64);
+            uint32_t ppw = (live + finish_waves - 1) / finish_waves;
+            ppw = ppw < 1 ? 1 : (ppw > 64 ? 64 : ppw);
+            uint32_t waves = (live + ppw - 1) / ppw;
+            if (waves > finish_waves) waves = finish_waves;
+            if (waves > max_waves) waves = max_waves; // persistent: lanes fetch paths until the queue is empty
+            if (hipMemsetAsync(w.st.counts + 4, 0, 4, stream) != hipSuccess) return -1;
+            const int fgrid = (int)((waves + WF_BLOCK / 64 - 1) / (WF_BLOCK / 64));
+            if (count)
+                hipLaunchKernelGGL(wf_finish_coop<true>, dim3(fgrid), dim3(WF_BLOCK), 0, stream, sc, fr, cam, w.st,
+                                   qq, (int)ppw);
+            else
+                hipLaunchKernelGGL(wf_finish_coop<false>, dim3(fgrid), dim3(WF_BLOCK), 0, stream, sc, fr, cam, w.st,
+                                   qq, (int)ppw);
+        } else {
             const int fgrid = (int)((live + WF_BLOCK - 1) / WF_BLOCK);
-            if (count) hipLaunchKernelGGL(wf_finish<true>, dim3(fgrid), dim3(WF_BLOCK), 0, stream, sc, fr, cam, w.st, q ^ 1);
-            else hipLaunchKernelGGL(wf_finish<false>, dim3(fgrid), dim3(WF_BLOCK), 0, stream, sc, fr, cam, w.st, q ^ 1);
-            if (hipGetLastError() != hipSuccess) return -1;
-            break;
+            if (count) hipLaunchKernelGGL(wf_finish<true>, dim3(fgrid), dim3(WF_BLOCK), 0, stream, sc, fr, cam, w.st, qq);
+            else hipLaunchKernelGGL(wf_finish<false>, dim3(fgrid), dim3(WF_BLOCK), 0, stream, sc, fr, cam, w.st, qq);
         }
+        if (hipGetLastError() != hipSuccess || !mark(3)) return -1;
+        P.finish_launches = 1;
+        return 0;
+    };
+    int rc = 0;
+    if (trace_kind == 1 && tail > slots) {
+        // wf_tail above the frame size: the whole call runs in the finisher (no queue iterations)
+        rc = finish(0, (uint32_t)slots);
+    } else {
+        for (int it = 0;; ++it) {
+            const int q = it & 1;
+            if (hipMemsetAsync(w.st.counts + (q ^ 1), 0, 4, stream) != hipSuccess) return -1;
+            if (hipMemsetAsync(w.st.counts + 2 + q, 0, 4, stream) != hipSuccess) return -1; // fetch cursor
+            if (!mark(4)) return -1;
+            if (trace_kind == 1) {
+                if (count) hipLaunchKernelGGL(wf_trace_coop<true>, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, w.st, q, fr.counters);
+                else hipLaunchKernelGGL(wf_trace_coop<false>, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, w.st, q, fr.counters);
+            } else if (trace_kind == 3) {
+                if (count) hipLaunchKernelGGL(wf_trace_dyn<true>, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, w.st, q, fr.counters);
+                else hipLaunchKernelGGL(wf_trace_dyn<false>, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, w.st, q, fr.counters);
+            } else {
+                if (count) hipLaunchKernelGGL(wf_trace<true>, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, w.st, q, fr.counters);
+                else hipLaunchKernelGGL(wf_trace<false>, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, w.st, q, fr.counters);
+            }
+            if (!mark(5)) return -1;
+            if (count) hipLaunchKernelGGL(wf_shade<true>, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, fr, cam, w.st, q);
+            else hipLaunchKernelGGL(wf_shade<false>, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, fr, cam, w.st, q);
+            if (hipGetLastError() != hipSuccess) return -1;
+            if (!mark(2)) return -1;
+            if (hipMemcpyAsync(w.host_count, w.st.counts + (q ^ 1), 4, hipMemcpyDeviceToHost, stream) != hipSuccess)
+                return -1;
+            if (hipStreamSynchronize(stream) != hipSuccess) return -1;
+            const uint32_t live = *w.host_count;
+            P.iterations = it + 1;
+            if (prof) {
+                P.trace_ms += elapsed_ms(w.ev[4], w.ev[5]);
+                P.shade_ms += elapsed_ms(w.ev[5], w.ev[2]);
+            }
+            if (trace_iters) {
+                timespec ts;
+                clock_gettime(CLOCK_MONOTONIC, &ts);
+                fprintf(stderr, "[wf] it %d live %u t %.4f\n", it, live, ts.tv_sec + ts.tv_nsec * 1e-9);
+            }
+            if (live == 0) break;
+            if (live < tail) {
+                rc = finish(q ^ 1, live);
+                break;
+            }
+        }
+    }
+    if (rc != 0) return rc;
+    if (prof) {
+        if (!mark(4) || hipEventSynchronize(w.ev[4]) != hipSuccess) return -1;
+        P.trace_launches = P.shade_launches = P.iterations;
+        P.start_ms = elapsed_ms(w.ev[0], w.ev[1]);
+        if (P.finish_launches) P.finish_ms = elapsed_ms(w.ev[2], w.ev[3]);
+        P.call_ms = elapsed_ms(w.ev[0], w.ev[4]);
+        w.prof = P;
     }
     return 0;
 }

@@ -51,12 +51,26 @@ class RtOptions(ctypes.Structure):
                 ("adaptive", ctypes.c_int), ("min_samples", ctypes.c_int), ("tolerance", ctypes.c_float),
                 ("max_depth", ctypes.c_int), ("kernel", ctypes.c_int), ("stream", ctypes.c_void_p),
                 ("counters_device", ctypes.c_void_p), ("wave_times_device", ctypes.c_void_p),
-                ("wf_tail", ctypes.c_int), ("wf_finish_waves", ctypes.c_int)]
+                ("wf_tail", ctypes.c_int), ("wf_finish_waves", ctypes.c_int), ("profile", ctypes.c_int)]
+
+
+class RtProfile(ctypes.Structure):
+    _fields_ = [("iterations", ctypes.c_int), ("trace_launches", ctypes.c_int), ("shade_launches", ctypes.c_int),
+                ("finish_launches", ctypes.c_int), ("start_ms", ctypes.c_float), ("trace_ms", ctypes.c_float),
+                ("shade_ms", ctypes.c_float), ("finish_ms", ctypes.c_float), ("call_ms", ctypes.c_float)]
+
+
+def last_profile():
+    """Kernel timing of the last rt_render with options(profile=True) on this device."""
+    p = RtProfile()
+    check(lib().rt_last_profile(ctypes.byref(p)))
+    return {k: getattr(p, k) for k, _ in RtProfile._fields_}
 
 
 TRIANGLE_BYTES = 152
 NODE_BYTES = 20
 COUNTER_NAMES = ["node", "tri", "hit", "texel", "nee", "sample", "skip", "ray", "watchdog", "maxdepth"]
+FINISH_COUNTER_NAMES = ["finish_node", "finish_tri", "finish_ray"]
 N_COUNTERS = 16
 
 _lib = None
@@ -269,7 +283,7 @@ KERNEL_WAVEFRONT = 1
 
 
 def options(width, height, passes=1, adaptive=True, min_samples=100, tolerance=0.05, max_depth=0, stream=None,
-            counters=None, kernel=KERNEL_MEGA, wf_tail=0, wf_finish_waves=0):
+            counters=None, kernel=KERNEL_MEGA, wf_tail=0, wf_finish_waves=0, profile=False):
     o = RtOptions()
     lib().rt_default_options(ctypes.byref(o))
     o.width, o.height, o.passes = width, height, passes
@@ -277,7 +291,7 @@ def options(width, height, passes=1, adaptive=True, min_samples=100, tolerance=0
     o.kernel = kernel
     o.stream = stream
     o.counters_device = counters
-    o.wf_tail, o.wf_finish_waves = wf_tail, wf_finish_waves
+    o.wf_tail, o.wf_finish_waves, o.profile = wf_tail, wf_finish_waves, int(profile)
     return o
 
 
@@ -296,10 +310,15 @@ class DeviceCounters:
     def zero(self):
         check(lib().rt_memset(self.p, 0, N_COUNTERS * 8))
 
-    def read(self):
+    def read(self, finisher=False):
+        """The reference-comparable counters; finisher=True adds the wavefront
+        finisher's share of node/tri/ray (RT_CNT_FIN_*)."""
         a = np.zeros(N_COUNTERS, dtype=np.uint64)
         check(lib().rt_download(_ptr(a), self.p, a.nbytes))
-        return {k: int(a[i]) for i, k in enumerate(COUNTER_NAMES)}
+        out = {k: int(a[i]) for i, k in enumerate(COUNTER_NAMES)}
+        if finisher:
+            out.update({k: int(a[10 + i]) for i, k in enumerate(FINISH_COUNTER_NAMES)})
+        return out
 
     def __del__(self):
         try:
