@@ -262,6 +262,10 @@ typedef struct RtOptions {
     int wf_tail;
     int wf_finish_waves;
     int profile;         /* 1: time the wavefront kernels with HIP events (rt_last_profile) */
+    /* cooperative traversal tuning (0 = default): node fetches per descent
+     * round, and pending lanes (of 64) before a wave's leaf test runs */
+    int wf_descent_cap;
+    int wf_postpone;
 } RtOptions;
 
 /* Per-call kernel timing of the last rt_render on this device with

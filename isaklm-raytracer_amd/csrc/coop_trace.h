@@ -42,12 +42,26 @@ __device__ __forceinline__ bool coop_bary(const RtDevScene &sc, uint32_t k, Vec3
 
 // per-lane traversal state
 struct CoopRay {
-    bool live;
+    bool live;                  // the lane holds an unfinished ray
+    bool pend;                  // ... which has reached a non-empty leaf, waiting for the wave's leaf test
     Vec3D o, d;
     float entry, exit_, root_exit;
     uint32_t node;
     int sp;
+    uint32_t leaf_begin;
+    int leaf_count;
 };
+
+__device__ __forceinline__ void coop_idle(CoopRay &r)
+{
+    r.live = r.pend = false;
+    r.o = r.d = rt_v3(0, 0, 0);
+    r.entry = r.exit_ = r.root_exit = 0.0f;
+    r.node = 0;
+    r.sp = 0;
+    r.leaf_begin = 0;
+    r.leaf_count = 0;
+}
 
 // start a ray: slab test on the scene box; false = miss
 __device__ __forceinline__ bool coop_begin(const RtDevScene &sc, CoopRay &r, Vec3D o, Vec3D d)
@@ -56,57 +70,87 @@ __device__ __forceinline__ bool coop_begin(const RtDevScene &sc, CoopRay &r, Vec
     r.d = d;
     r.node = 0;
     r.sp = 0;
+    r.pend = false;
     r.live = bbox_hit(sc, o, d, r.entry, r.exit_);
     r.root_exit = r.exit_;
     return r.live;
 }
 
-// One traversal step for every live lane of the wave (call with all 64 lanes
-// active).  Returns true for a lane whose ray finished in this step, with
-// tri >= 0 and the barycentrics of the hit, or tri = -1 for a miss.
+// pop the next subtree (rt/trace_ray.cuh:308-316); exit t = entry of the entry below
+template <typename STK>
+__device__ __forceinline__ void coop_pop(CoopRay &r, STK &stk)
+{
+    --r.sp;
+    r.node = stk.node_at(r.sp);
+    r.entry = stk.entry_at(r.sp);
+    r.exit_ = r.sp > 0 ? stk.entry_at(r.sp - 1) : r.root_exit;
+}
+
+// Descent (rt/trace_ray.cuh:273-306) of a live, non-pending lane for at most
+// `cap` node fetches, stopping at the first non-empty leaf (r.pend).  Empty
+// leaves are popped on the spot.  Returns true when the ray ended (a miss:
+// an empty leaf with an empty stack).  Capping the descent lets lanes that
+// reach a leaf early be tested with the next batch instead of idling until
+// the wave's deepest descent is done (postponed leaf testing).
 template <bool COUNT, typename STK>
-__device__ __forceinline__ bool coop_step(const RtDevScene &sc, CoopRay &r, STK &stk, unsigned long long *wkey,
-                                          uint2 *list, int &tri, float &hbx, float &hby, float &hbz, Cnt &c)
+__device__ __forceinline__ bool coop_descend(const RtDevScene &sc, CoopRay &r, STK &stk, int cap, Cnt &c)
+{
+    // scalar copies: a select between struct members would become a
+    // dynamically indexed (scratch) load
+    const float ox = r.o.x, oy = r.o.y, oz = r.o.z, dx = r.d.x, dy = r.d.y, dz = r.d.z;
+    for (int k = 0; k < cap; ++k) {
+        const uint2 nd = *reinterpret_cast<const uint2 *>(sc.nodes + 2 * (size_t)r.node);
+        if (COUNT) c.v[RT_CNT_NODE]++;
+        if ((nd.y & 3u) == RT_LEAF_TAG) {
+            const int cnt = (int)(nd.y >> 2);
+            if (cnt > 0) {
+                r.pend = true;
+                r.leaf_begin = nd.x;
+                r.leaf_count = cnt;
+                if (COUNT) c.v[RT_CNT_TRI] += (unsigned long long)cnt;
+                return false;
+            }
+            if (r.sp == 0) {
+                r.live = false;
+                return true;
+            }
+            coop_pop(r, stk);
+            continue;
+        }
+        const uint32_t axis = nd.y & 3u;
+        const float split = as_float(nd.x);
+        const float oax = axis == 0 ? ox : (axis == 1 ? oy : oz);
+        const float dax = axis == 0 ? dx : (axis == 1 ? dy : dz);
+        uint32_t near_c = r.node + 1, far_c = nd.y >> 2;
+        if (oax >= split) { // ray_behind_plane (:174-188)
+            near_c = nd.y >> 2;
+            far_c = r.node + 1;
+        }
+        const float t = (split - oax) / dax; // intersect_plane (:190-210)
+        if (t >= r.exit_ || t < 0) {
+            r.node = near_c;
+        } else if (t <= r.entry) {
+            r.node = far_c;
+        } else {
+            stk.put(r.sp, far_c, t);
+            ++r.sp;
+            r.node = near_c;
+            r.exit_ = t;
+        }
+    }
+    return false;
+}
+
+// The wave-cooperative test of every pending lane's leaf (call with all 64
+// lanes active).  Returns true for a lane whose ray finished here, with
+// tri >= 0 and the barycentrics of the hit, or tri = -1 for a miss; other
+// pending lanes pop and go back to descending.
+template <bool COUNT, typename STK>
+__device__ __forceinline__ bool coop_leaves(const RtDevScene &sc, CoopRay &r, STK &stk, unsigned long long *wkey,
+                                            uint2 *list, int &tri, float &hbx, float &hby, float &hbz, Cnt &c)
 {
     const int lane = __lane_id();
-    // ---- descend to a leaf (rt/trace_ray.cuh:273-306), per lane
-    uint32_t leaf_begin = 0;
-    int leaf_count = 0;
-    if (r.live) {
-        // scalar copies: a select between struct members would become a
-        // dynamically indexed (scratch) load
-        const float ox = r.o.x, oy = r.o.y, oz = r.o.z, dx = r.d.x, dy = r.d.y, dz = r.d.z;
-        uint2 nd = *reinterpret_cast<const uint2 *>(sc.nodes + 2 * (size_t)r.node);
-        if (COUNT) c.v[RT_CNT_NODE]++;
-        while ((nd.y & 3u) != RT_LEAF_TAG) {
-            const uint32_t axis = nd.y & 3u;
-            const float split = as_float(nd.x);
-            const float oax = axis == 0 ? ox : (axis == 1 ? oy : oz);
-            const float dax = axis == 0 ? dx : (axis == 1 ? dy : dz);
-            uint32_t near_c = r.node + 1, far_c = nd.y >> 2;
-            if (oax >= split) { // ray_behind_plane (:174-188)
-                near_c = nd.y >> 2;
-                far_c = r.node + 1;
-            }
-            const float t = (split - oax) / dax; // intersect_plane (:190-210)
-            if (t >= r.exit_ || t < 0) {
-                r.node = near_c;
-            } else if (t <= r.entry) {
-                r.node = far_c;
-            } else {
-                stk.put(r.sp, far_c, t);
-                ++r.sp;
-                r.node = near_c;
-                r.exit_ = t;
-            }
-            nd = *reinterpret_cast<const uint2 *>(sc.nodes + 2 * (size_t)r.node);
-            if (COUNT) c.v[RT_CNT_NODE]++;
-        }
-        leaf_begin = nd.x;
-        leaf_count = (int)(nd.y >> 2);
-        if (COUNT) c.v[RT_CNT_TRI] += (unsigned long long)leaf_count;
-    }
-    // ---- wave-cooperative leaf tests
+    const int leaf_count = r.pend ? r.leaf_count : 0;
     int start = leaf_count; // inclusive scan -> exclusive
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
@@ -126,7 +170,7 @@ __device__ __forceinline__ bool coop_step(const RtDevScene &sc, CoopRay &r, STK 
                 const int sv = __shfl(start, j + step);
                 if (sv <= p) j += step;
             }
-            const uint32_t k = (uint32_t)__shfl((int)leaf_begin, j) + (uint32_t)(p - __shfl(start, j));
+            const uint32_t k = (uint32_t)__shfl((int)r.leaf_begin, j) + (uint32_t)(p - __shfl(start, j));
             const Vec3D oo = rt_v3(__shfl(r.o.x, j), __shfl(r.o.y, j), __shfl(r.o.z, j));
             const Vec3D dd = rt_v3(__shfl(r.d.x, j), __shfl(r.d.y, j), __shfl(r.d.z, j));
             const float ex = __shfl(r.exit_, j);
@@ -167,7 +211,8 @@ __device__ __forceinline__ bool coop_step(const RtDevScene &sc, CoopRay &r, STK 
     // ---- per-lane result: winner, or pop, or miss
     const unsigned long long key = wkey[lane];
     bool done = false;
-    if (r.live) {
+    if (r.pend) {
+        r.pend = false;
         if (key != ~0ull) {
             const uint32_t k = (uint32_t)key;
             coop_bary(sc, k, r.o, r.d, __uint_as_float((uint32_t)(key >> 32)), hbx, hby, hbz, tri);
@@ -179,12 +224,27 @@ __device__ __forceinline__ bool coop_step(const RtDevScene &sc, CoopRay &r, STK 
             r.live = false;
             done = true;
         } else {
-            --r.sp;
-            r.node = stk.node_at(r.sp);
-            r.entry = stk.entry_at(r.sp);
-            r.exit_ = r.sp > 0 ? stk.entry_at(r.sp - 1) : r.root_exit;
+            coop_pop(r, stk);
         }
     }
+    return done;
+}
+
+// One round for the wave: capped descent for descending lanes, then the
+// cooperative leaf test once at least `postpone` lanes are pending (or no
+// lane is still descending).  Call with all 64 lanes active; returns true for
+// a lane whose ray finished in this round (tri / barycentrics as above).
+template <bool COUNT, typename STK>
+__device__ __forceinline__ bool coop_round(const RtDevScene &sc, CoopRay &r, STK &stk, unsigned long long *wkey,
+                                           uint2 *list, int cap, int postpone, int &tri, float &hbx, float &hby,
+                                           float &hbz, Cnt &c)
+{
+    bool done = false;
+    tri = -1;
+    if (r.live && !r.pend) done = coop_descend<COUNT>(sc, r, stk, cap, c);
+    const unsigned long long pm = __ballot(r.pend), lm = __ballot(r.live);
+    if (pm && (__popcll(pm) >= postpone || pm == lm))
+        if (coop_leaves<COUNT>(sc, r, stk, wkey, list, tri, hbx, hby, hbz, c)) done = true;
     return done;
 }
 

@@ -28,6 +28,8 @@ using namespace rtk;
 #define WF_LDS_STACK 8  // stack entries in LDS; deeper ones spill to HBM (rare)
 #define WF_TAIL_DEFAULT 65536u       // RtOptions.wf_tail
 #define WF_FINISH_WAVES_DEFAULT 2048u // RtOptions.wf_finish_waves
+#define WF_DESCENT_CAP_DEFAULT 8      // RtOptions.wf_descent_cap
+#define WF_POSTPONE_DEFAULT 32        // RtOptions.wf_postpone
 
 struct WfState {
     int *passes_left;
@@ -314,10 +316,12 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_trace_dyn(RtDevScene sc, WfState 
 #include "coop_trace.h"
 
 // Wave-cooperative trace with dynamic ray fetch (coop_trace.h): lanes whose
-// ray finished take the next queued ray at the next leaf boundary.
+// ray finished take the next queued ray at the next round; descents are
+// capped at `cap` node fetches per round and the leaf test waits for
+// `postpone` pending lanes.
 template <bool COUNT>
 __global__ void __launch_bounds__(WF_BLOCK) wf_trace_coop(RtDevScene sc, WfState st, int q,
-                                                          unsigned long long *counters)
+                                                          unsigned long long *counters, int cap, int postpone)
 {
     __shared__ uint32_t s_node[WF_LDS_STACK * WF_BLOCK];
     __shared__ float s_entry[WF_LDS_STACK * WF_BLOCK];
@@ -337,11 +341,7 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_trace_coop(RtDevScene sc, WfState
     uint32_t *fetch = st.counts + 2 + q;
 
     CoopRay r;
-    r.live = false;
-    r.o = r.d = rt_v3(0, 0, 0);
-    r.entry = r.exit_ = r.root_exit = 0.0f;
-    r.node = 0;
-    r.sp = 0;
+    coop_idle(r);
     bool exhausted = false;
     uint32_t e = 0;
     while (true) {
@@ -370,7 +370,7 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_trace_coop(RtDevScene sc, WfState
         }
         int tri = -1;
         float bx = 0.0f, by = 0.0f, bz = 0.0f;
-        if (coop_step<COUNT>(sc, r, stk, wkey, list, tri, bx, by, bz, c))
+        if (coop_round<COUNT>(sc, r, stk, wkey, list, cap, postpone, tri, bx, by, bz, c))
             *reinterpret_cast<float4 *>(st.hits + e) = make_float4(__int_as_float(tri), bx, by, bz);
     }
     if (COUNT) flush_counters(c, counters);
@@ -581,14 +581,14 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_finish(RtDevScene sc, RtDevFrame 
 
 // Cooperative finisher: runs queued paths to the end of their passes in
 // registers (shade_step right after each ray query), megakernel style, while
-// the whole wave tests leaf entries for its live rays together (coop_step).
+// the whole wave tests leaf entries for its live rays together (coop_round).
 // Each wave keeps up to `ppw` (1..64) paths in flight, one per lane; a lane
 // whose path is done takes the next queue entry (wave-aggregated atomic on
 // counts[4]).  With ppw = 1 a lone long glass path gets its leaves tested 64
 // entries at a time instead of one.
 template <bool COUNT>
 __global__ void __launch_bounds__(WF_BLOCK) wf_finish_coop(RtDevScene sc, RtDevFrame fr, RtDevCamera cam, WfState st,
-                                                           int q, int ppw)
+                                                           int q, int ppw, int cap, int postpone)
 {
     __shared__ uint32_t s_node[WF_LDS_STACK * WF_BLOCK];
     __shared__ float s_entry[WF_LDS_STACK * WF_BLOCK];
@@ -611,11 +611,7 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_finish_coop(RtDevScene sc, RtDevF
     p.slot = 0;
     p.ro = p.rd = rt_v3(0, 0, 0);
     CoopRay r;
-    r.live = false;
-    r.o = r.d = rt_v3(0, 0, 0);
-    r.entry = r.exit_ = r.root_exit = 0.0f;
-    r.node = 0;
-    r.sp = 0;
+    coop_idle(r);
     int hit = -1;
     float bx = 0.0f, by = 0.0f, bz = 0.0f;
     bool active = false;              // the lane holds a path
@@ -665,7 +661,7 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_finish_coop(RtDevScene sc, RtDevF
             if (__all(exhausted)) break;
             continue;
         }
-        if (coop_step<COUNT>(sc, r, stk, wkey, list, hit, bx, by, bz, c)) pending = true;
+        if (coop_round<COUNT>(sc, r, stk, wkey, list, cap, postpone, hit, bx, by, bz, c)) pending = true;
     }
     if (COUNT) {
         flush_counters(c, fr.counters);
@@ -751,7 +747,7 @@ extern "C" int rt_last_profile(RtProfile *out)
 }
 
 int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevCamera &cam, hipStream_t stream,
-                        int variant, int tail_opt, int finish_waves_opt, int profile)
+                        int variant, int tail_opt, int finish_waves_opt, int profile, int cap_opt, int postpone_opt)
 {
     // 1: wave-cooperative leaves (entries packed as k << 6 | lane: needs < 2^26 entries), 2: static, 3: per-lane fetch
     int trace_kind = variant;
@@ -781,6 +777,9 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
     const uint32_t tail = tail_opt > 0 ? (uint32_t)tail_opt : WF_TAIL_DEFAULT;
     // the cooperative finisher runs on at most this many waves (up to 64 paths in flight each)
     const uint32_t finish_waves = finish_waves_opt > 0 ? (uint32_t)finish_waves_opt : WF_FINISH_WAVES_DEFAULT;
+    // cooperative traversal: node fetches per descent round, pending lanes before a leaf test
+    const int cap = cap_opt > 0 ? cap_opt : WF_DESCENT_CAP_DEFAULT;
+    const int postpone = postpone_opt > 0 ? (postpone_opt > 64 ? 64 : postpone_opt) : WF_POSTPONE_DEFAULT;
     static const bool trace_iters = getenv("RT_WF_TRACE_ITERS") != nullptr; // debug: per-iteration queue sizes
     // run the `live` paths of queue qq to the end of the call in the finisher
     auto finish = [&](int qq, uint32_t live) -> int {
@@ -797,10 +796,10 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
             const int fgrid = (int)((waves + WF_BLOCK / 64 - 1) / (WF_BLOCK / 64));
             if (count)
                 hipLaunchKernelGGL(wf_finish_coop<true>, dim3(fgrid), dim3(WF_BLOCK), 0, stream, sc, fr, cam, w.st,
-                                   qq, (int)ppw);
+                                   qq, (int)ppw, cap, postpone);
             else
                 hipLaunchKernelGGL(wf_finish_coop<false>, dim3(fgrid), dim3(WF_BLOCK), 0, stream, sc, fr, cam, w.st,
-                                   qq, (int)ppw);
+                                   qq, (int)ppw, cap, postpone);
         } else {
             const int fgrid = (int)((live + WF_BLOCK - 1) / WF_BLOCK);
             if (count) hipLaunchKernelGGL(wf_finish<true>, dim3(fgrid), dim3(WF_BLOCK), 0, stream, sc, fr, cam, w.st, qq);
@@ -821,8 +820,8 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
             if (hipMemsetAsync(w.st.counts + 2 + q, 0, 4, stream) != hipSuccess) return -1; // fetch cursor
             if (!mark(4)) return -1;
             if (trace_kind == 1) {
-                if (count) hipLaunchKernelGGL(wf_trace_coop<true>, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, w.st, q, fr.counters);
-                else hipLaunchKernelGGL(wf_trace_coop<false>, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, w.st, q, fr.counters);
+                if (count) hipLaunchKernelGGL(wf_trace_coop<true>, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, w.st, q, fr.counters, cap, postpone);
+                else hipLaunchKernelGGL(wf_trace_coop<false>, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, w.st, q, fr.counters, cap, postpone);
             } else if (trace_kind == 3) {
                 if (count) hipLaunchKernelGGL(wf_trace_dyn<true>, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, w.st, q, fr.counters);
                 else hipLaunchKernelGGL(wf_trace_dyn<false>, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, w.st, q, fr.counters);

@@ -1,7 +1,7 @@
 """A/B kernel variants in ONE process, interleaved rounds (guide §5.4 rule 24).
 
 usage: python tools/ab.py SCENE PASSES MAX_DEPTH ROUNDS VARIANT[,VARIANT...]
-  VARIANT = KERNEL[:WF_TAIL[:WF_FINISH_WAVES]]; KERNEL 0 mega, 1 wavefront
+  VARIANT = KERNEL[:WF_TAIL[:WF_FINISH_WAVES[:DESCENT_CAP[:POSTPONE]]]]; KERNEL 0 mega, 1 wavefront
             (cooperative leaves), 2 wavefront static, 3 wavefront lane fetch
 Prints per-variant Msamples/s (median, min, max) at 1920x1080 and the work
 counters of one counted run.
@@ -25,21 +25,24 @@ def main():
     variants = sys.argv[5].split(",")
 
     def opts(v, **kw):
-        f = [int(x) for x in v.split(":")] + [0, 0]
+        f = [int(x) for x in v.split(":")] + [0, 0, 0, 0]
         return rt.options(W, H, P, adaptive=False, max_depth=maxd, kernel=f[0], wf_tail=f[1], wf_finish_waves=f[2],
-                          **kw)
+                          wf_descent_cap=f[3], wf_postpone=f[4], **kw)
 
     W, H = int(os.environ.get("AB_W", 1920)), int(os.environ.get("AB_H", 1080))
     run = helpers.GpuRun(scene)
     g = rt.GBuffer(W, H)
     times = {v: [] for v in variants}
+    profs = {v: [] for v in variants}
     for r in range(rounds):
         for v in variants:
-            opt = opts(v)
+            opt = opts(v, profile=True)
             rt.check(rt.lib().rt_synchronize())
             t = time.perf_counter()
             rt.render(run.dev, g, run.camera, 0, opt)
             times[v].append(time.perf_counter() - t)
+            if v.split(":")[0] != "0":
+                profs[v].append(rt.last_profile())
     out = {}
     for v in variants:
         cnt = rt.DeviceCounters()
@@ -50,6 +53,9 @@ def main():
         out[v] = {"msamples_s_median": round(W * H * P / np.median(ts) / 1e6, 3),
                   "msamples_s_best": round(W * H * P / ts.min() / 1e6, 3),
                   "s": [round(x, 3) for x in ts], "maxdepth": c["maxdepth"],
+                  "trace_ms": [round(p["trace_ms"]) for p in profs[v]],
+                  "finish_ms": [round(p["finish_ms"]) for p in profs[v]],
+                  "iterations": [p["iterations"] for p in profs[v]],
                   "per_sample": {k: round(c[k] / max(c["sample"], 1), 2) for k in ("ray", "node", "tri")}}
     print(json.dumps({"scene": scene, "passes": P, "max_depth": maxd, "variants": out}, indent=1))
 

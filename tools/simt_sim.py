@@ -93,6 +93,48 @@ def dynamic_sched(seqs, coop_leaf=False):
     return total
 
 
+def postponed_sched(seqs, K, T):
+    """dynamic fetch + cooperative leaves, with the descent capped at K steps
+    per round and the cooperative leaf test run only once T lanes hold a
+    leaf (or no lane is still descending)."""
+    total = 0.0
+    stream = iter(range(len(seqs)))
+    # lane: [ray, visit index, descent steps left, pending leaf size or -1]
+    lanes = []
+    for _ in range(64):
+        r = next(stream, None)
+        lanes.append([r, 0, seqs[r][0][0] if r is not None and len(seqs[r]) else 0, -1])
+
+    def advance(l):
+        while l[0] is not None and l[1] >= len(seqs[l[0]]):
+            l[0], l[1] = next(stream, None), 0
+            if l[0] is not None and len(seqs[l[0]]):
+                l[2] = seqs[l[0]][0][0]
+        return l[0] is not None
+
+    while True:
+        live = [l for l in lanes if advance(l)]
+        if not live:
+            break
+        desc = [l for l in live if l[3] < 0]
+        if desc:
+            steps = min(K, max(l[2] for l in desc))
+            total += steps * Cd
+            for l in desc:
+                l[2] -= steps
+                if l[2] <= 0:
+                    l[3] = seqs[l[0]][l[1]][1]
+        pend = [l for l in live if l[3] >= 0]
+        if pend and (len(pend) >= T or len(pend) == len(live)):
+            total += (sum((l[3] + 1) // 2 for l in pend) + 63) // 64 * Cl + Cp
+            for l in pend:
+                l[3] = -1
+                l[1] += 1
+                if l[1] < len(seqs[l[0]]):
+                    l[2] = seqs[l[0]][l[1]][0]
+    return total
+
+
 def main():
     scene = sys.argv[1] if len(sys.argv) > 1 else "room2m"
     npix = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
@@ -106,6 +148,9 @@ def main():
           f"descent/visit {np.mean([v[0] for s in seqs for v in s]):.2f}")
     print(f"utilization  static {per_lane / st:.3f}  dynamic-fetch {per_lane / dy:.3f}  "
           f"dynamic+coop-leaf {per_lane / co:.3f}")
+    for K in (2, 4, 8, 64):
+        print(f"  postponed K={K}: " + "  ".join(f"T={T} {per_lane / postponed_sched(seqs, K, T):.3f}"
+                                                for T in (16, 32, 48, 64)))
 
 
 if __name__ == "__main__":
