@@ -266,6 +266,7 @@ typedef struct RtOptions {
      * round, and pending lanes (of 64) before a wave's leaf test runs */
     int wf_descent_cap;
     int wf_postpone;
+    int wf_wide;         /* finisher: a wave's lone ray is traced by all 64 lanes (0 = on, < 0 = off) */
 } RtOptions;
 
 /* Per-call kernel timing of the last rt_render on this device with

@@ -248,4 +248,189 @@ __device__ __forceinline__ bool coop_round(const RtDevScene &sc, CoopRay &r, STK
     return done;
 }
 
+// ---------------------------------------------------------------------------
+// Wide single-ray traversal: the whole wave works on ONE ray (the tail
+// finisher's lone long glass paths, where the sequential trace is a chain of
+// ~250 dependent node fetches and ~50 leaf tests per bounce).
+//
+// The traversal's pending work is kept as an ordered frontier F in LDS (a
+// stack whose top is the next item in the sequential front-to-back order).
+// Each round the top k <= 64 items are loaded in parallel, one per lane.  The
+// leading run of leaves is the next stretch of the sequential leaf order: it
+// is tested in one cooperative batch (every entry of every leaf, 64 at a
+// time) with the key (leaf rank << 58 | bits(s) << 26 | entry), so the winner
+// is the first leaf in order that has a hit and, inside it, the smallest
+// (s, entry) — exactly trace_ray's first-leaf-wins + strict-< scan
+// (rt/trace_ray.cuh:124-141,310-313).  The inner items behind the run are
+// expanded in the same round by the sequential rule (near/far by
+// ray_behind_plane, t = (split - o)/d, t >= exit or t < 0 -> near only,
+// t <= entry -> far only, else near [entry, t] then far [t, exit]), so every
+// item carries the same interval the sequential stack would give it.  Items
+// beyond the first hit are speculative and dropped.
+//
+// Work counters stay the reference's: a fetch of an expanded inner node is
+// charged to its first child (acc) and committed only when a leaf at or
+// before the winning leaf is consumed — the nodes the sequential traversal
+// visits are exactly those at or before the winning leaf in order.
+#define WIDE_CAP 256        // frontier items per wave
+#define WIDE_RESERVE 24     // head-only growth room (tree depth <= 20)
+#define WIDE_LEAF_BUDGET 256 // entries tested per batch (at least one whole leaf)
+
+struct WideItem {
+    uint32_t node;
+    float entry, exit_;
+    uint32_t acc; // node fetches charged to this item (counters)
+};
+
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v)
+{
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+
+// Trace the wave-uniform ray (o, d) whose scene-box interval is [entry, exit_]
+// with all 64 lanes.  Returns the hit (tri >= 0, barycentrics) or tri = -1.
+// Counters are added by `counter_lane` only.
+template <bool COUNT>
+__device__ __forceinline__ void wide_trace(const RtDevScene &sc, Vec3D o, Vec3D d, float entry, float exit_,
+                                           WideItem *F, unsigned long long *wkey, uint2 *list, bool counter_lane,
+                                           int &tri, float &hbx, float &hby, float &hbz, Cnt &c)
+{
+    const int lane = __lane_id();
+    const float ox = o.x, oy = o.y, oz = o.z, dx = d.x, dy = d.y, dz = d.z;
+    if (lane == 0) F[0] = WideItem{0u, entry, exit_, 0u};
+    int n = 1;
+    tri = -1;
+    while (n > 0) {
+        int k = WIDE_CAP - WIDE_RESERVE - n; // expansions add at most one item each
+        k = k < 1 ? 1 : (k > 64 ? 64 : k);
+        k = k < n ? k : n;
+        WideItem it = WideItem{0u, 0.0f, 0.0f, 0u};
+        uint2 nd = make_uint2(0u, 0u);
+        const bool have = lane < k;
+        if (have) {
+            it = F[n - 1 - lane];
+            nd = *reinterpret_cast<const uint2 *>(sc.nodes + 2 * (size_t)it.node);
+        }
+        const bool leaf = have && (nd.y & 3u) == RT_LEAF_TAG;
+        const unsigned long long lmask = __ballot(leaf);
+        const int L = ~lmask ? __ffsll((long long)~lmask) - 1 : 64; // leading run of leaves
+        // consume leaves 0..Le-1: whole leaves within the entry budget (at least one)
+        const int cnt_all = (lane < L) ? (int)(nd.y >> 2) : 0;
+        int incl = cnt_all;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int v = __shfl_up(incl, off);
+            if (lane >= off) incl += v;
+        }
+        const int Le = __popcll(__ballot(lane < L && (lane == 0 || incl <= WIDE_LEAF_BUDGET)));
+        if (Le > 0) {
+            const int cnt = lane < Le ? cnt_all : 0;
+            const int start = incl - cnt_all; // exclusive prefix (lanes < Le)
+            const int total = __shfl(incl, Le - 1);
+            if (lane == 0) wkey[0] = ~0ull;
+            int list_n = 0;
+            for (int base = 0; base < total || list_n > 0; base += 64) {
+                if (base < total) {
+                    const int p = base + lane;
+                    int j = 0; // owner leaf: the largest lane with start_j <= p (lanes >= Le have start >= total)
+#pragma unroll
+                    for (int step = 32; step >= 1; step >>= 1) {
+                        const int sv = __shfl(start, j + step);
+                        if (sv <= p) j += step;
+                    }
+                    const uint32_t kk = nd.x; // leaf_begin of this lane
+                    const uint32_t e = (uint32_t)__shfl((int)kk, j) + (uint32_t)(p - __shfl(start, j));
+                    const float ex = __shfl(it.exit_, j);
+                    bool pass = false;
+                    float s = 0.0f;
+                    if (p < total) {
+                        const RtF4 A = ldf4(sc.isect_a + e);
+                        const float dn = dx * A.x + dy * A.y + dz * A.z;
+                        s = (A.w - (ox * A.x + oy * A.y + oz * A.z)) / dn;
+                        pass = dn != 0 && s >= 0.00001f && s < ex;
+                    }
+                    const unsigned long long pm = __ballot(pass);
+                    if (pass)
+                        list[list_n + __popcll(pm & ((1ull << lane) - 1ull))] =
+                            make_uint2((e << 6) | (uint32_t)j, __float_as_uint(s));
+                    list_n += __popcll(pm);
+                }
+                if (list_n >= 64 || (base + 64 >= total && list_n > 0)) {
+                    const int take = list_n < 64 ? list_n : 64;
+                    const uint2 itm = list[lane < take ? lane : 0];
+                    if (lane < take) {
+                        float cx, cy, cz;
+                        int t;
+                        if (coop_bary(sc, itm.x >> 6, o, d, __uint_as_float(itm.y), cx, cy, cz, t))
+                            atomicMin(wkey, ((unsigned long long)(itm.x & 63u) << 58) |
+                                                ((unsigned long long)itm.y << 26) | (unsigned long long)(itm.x >> 6));
+                    }
+                    const int rest = list_n - take;
+                    uint2 mv = make_uint2(0, 0);
+                    if (lane < rest) mv = list[take + lane];
+                    if (lane < rest) list[lane] = mv;
+                    list_n = rest;
+                }
+            }
+            const unsigned long long key = wkey[0];
+            const int jstar = key != ~0ull ? (int)(key >> 58) : Le - 1;
+            if (COUNT) { // leaves 0..jstar are the sequential traversal's next visits
+                const unsigned long long nv = wave_sum(lane <= jstar ? it.acc + 1ull : 0ull);
+                const unsigned long long tv = wave_sum(lane <= jstar ? (unsigned long long)cnt : 0ull);
+                if (counter_lane) {
+                    c.v[RT_CNT_NODE] += nv;
+                    c.v[RT_CNT_TRI] += tv;
+                }
+            }
+            if (key != ~0ull) {
+                const uint32_t e = (uint32_t)(key & ((1ull << 26) - 1ull));
+                coop_bary(sc, e, o, d, __uint_as_float((uint32_t)(key >> 26)), hbx, hby, hbz, tri);
+                if (COUNT && counter_lane) c.v[RT_CNT_HIT]++;
+                return;
+            }
+        }
+        // expand the rest of the k items (leaves behind an inner item stay as they are)
+        int c_out = 0;
+        WideItem a = it, b = it;
+        if (have && lane >= Le) {
+            c_out = 1;
+            if (!leaf) {
+                const uint32_t axis = nd.y & 3u;
+                const float split = as_float(nd.x);
+                const float oax = axis == 0 ? ox : (axis == 1 ? oy : oz);
+                const float dax = axis == 0 ? dx : (axis == 1 ? dy : dz);
+                uint32_t near_c = it.node + 1, far_c = nd.y >> 2;
+                if (oax >= split) { // ray_behind_plane (:174-188)
+                    near_c = nd.y >> 2;
+                    far_c = it.node + 1;
+                }
+                const float t = (split - oax) / dax; // intersect_plane (:190-210)
+                if (t >= it.exit_ || t < 0) {
+                    a = WideItem{near_c, it.entry, it.exit_, it.acc + 1u};
+                } else if (t <= it.entry) {
+                    a = WideItem{far_c, it.entry, it.exit_, it.acc + 1u};
+                } else {
+                    a = WideItem{near_c, it.entry, t, it.acc + 1u};
+                    b = WideItem{far_c, t, it.exit_, 0u};
+                    c_out = 2;
+                }
+            }
+        }
+        int pos = c_out;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int v = __shfl_up(pos, off);
+            if (lane >= off) pos += v;
+        }
+        const int M = __shfl(pos, 63);
+        pos -= c_out;
+        const int base = n - k;
+        if (c_out >= 1) F[base + M - 1 - pos] = a;
+        if (c_out == 2) F[base + M - 2 - pos] = b;
+        n = base + M;
+    }
+}
+
 } // namespace rtk

@@ -588,12 +588,13 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_finish(RtDevScene sc, RtDevFrame 
 // entries at a time instead of one.
 template <bool COUNT>
 __global__ void __launch_bounds__(WF_BLOCK) wf_finish_coop(RtDevScene sc, RtDevFrame fr, RtDevCamera cam, WfState st,
-                                                           int q, int ppw, int cap, int postpone)
+                                                           int q, int ppw, int cap, int postpone, int wide)
 {
     __shared__ uint32_t s_node[WF_LDS_STACK * WF_BLOCK];
     __shared__ float s_entry[WF_LDS_STACK * WF_BLOCK];
     __shared__ unsigned long long s_key[WF_BLOCK];
     __shared__ uint2 s_list[(WF_BLOCK / 64) * WF_COOP_LIST];
+    __shared__ WideItem s_wide[(WF_BLOCK / 64) * WIDE_CAP];
     const int tid = threadIdx.x;
     const int gtid = blockIdx.x * WF_BLOCK + tid;
     const int lane = __lane_id();
@@ -657,9 +658,30 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_finish_coop(RtDevScene sc, RtDevF
             }
         }
         // here every active lane has a live ray
-        if (!__any(r.live)) {
+        const unsigned long long lm = __ballot(r.live);
+        if (!lm) {
             if (__all(exhausted)) break;
             continue;
+        }
+        if (wide && __popcll(lm) == 1) { // a lone ray, not yet started: the whole wave traces it
+            const int owner = __ffsll((long long)lm) - 1;
+            if (__shfl((int)(r.node == 0 && !r.pend), owner)) {
+                const Vec3D o = rt_v3(__shfl(r.o.x, owner), __shfl(r.o.y, owner), __shfl(r.o.z, owner));
+                const Vec3D d = rt_v3(__shfl(r.d.x, owner), __shfl(r.d.y, owner), __shfl(r.d.z, owner));
+                int t;
+                float x, y, z;
+                wide_trace<COUNT>(sc, o, d, __shfl(r.entry, owner), __shfl(r.exit_, owner), s_wide + wave * WIDE_CAP,
+                                  wkey, list, lane == owner, t, x, y, z, c);
+                if (lane == owner) {
+                    hit = t;
+                    bx = x;
+                    by = y;
+                    bz = z;
+                    r.live = false;
+                    pending = true;
+                }
+                continue;
+            }
         }
         if (coop_round<COUNT>(sc, r, stk, wkey, list, cap, postpone, hit, bx, by, bz, c)) pending = true;
     }
@@ -747,7 +769,8 @@ extern "C" int rt_last_profile(RtProfile *out)
 }
 
 int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevCamera &cam, hipStream_t stream,
-                        int variant, int tail_opt, int finish_waves_opt, int profile, int cap_opt, int postpone_opt)
+                        int variant, int tail_opt, int finish_waves_opt, int profile, int cap_opt, int postpone_opt,
+                        int wide_opt)
 {
     // 1: wave-cooperative leaves (entries packed as k << 6 | lane: needs < 2^26 entries), 2: static, 3: per-lane fetch
     int trace_kind = variant;
@@ -780,6 +803,7 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
     // cooperative traversal: node fetches per descent round, pending lanes before a leaf test
     const int cap = cap_opt > 0 ? cap_opt : WF_DESCENT_CAP_DEFAULT;
     const int postpone = postpone_opt > 0 ? (postpone_opt > 64 ? 64 : postpone_opt) : WF_POSTPONE_DEFAULT;
+    const int wide = wide_opt >= 0 ? 1 : 0; // finisher: lone rays traced by the whole wave
     static const bool trace_iters = getenv("RT_WF_TRACE_ITERS") != nullptr; // debug: per-iteration queue sizes
     // run the `live` paths of queue qq to the end of the call in the finisher
     auto finish = [&](int qq, uint32_t live) -> int {
@@ -796,10 +820,10 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
             const int fgrid = (int)((waves + WF_BLOCK / 64 - 1) / (WF_BLOCK / 64));
             if (count)
                 hipLaunchKernelGGL(wf_finish_coop<true>, dim3(fgrid), dim3(WF_BLOCK), 0, stream, sc, fr, cam, w.st,
-                                   qq, (int)ppw, cap, postpone);
+                                   qq, (int)ppw, cap, postpone, wide);
             else
                 hipLaunchKernelGGL(wf_finish_coop<false>, dim3(fgrid), dim3(WF_BLOCK), 0, stream, sc, fr, cam, w.st,
-                                   qq, (int)ppw, cap, postpone);
+                                   qq, (int)ppw, cap, postpone, wide);
         } else {
             const int fgrid = (int)((live + WF_BLOCK - 1) / WF_BLOCK);
             if (count) hipLaunchKernelGGL(wf_finish<true>, dim3(fgrid), dim3(WF_BLOCK), 0, stream, sc, fr, cam, w.st, qq);

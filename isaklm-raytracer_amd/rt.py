@@ -52,7 +52,7 @@ class RtOptions(ctypes.Structure):
                 ("max_depth", ctypes.c_int), ("kernel", ctypes.c_int), ("stream", ctypes.c_void_p),
                 ("counters_device", ctypes.c_void_p), ("wave_times_device", ctypes.c_void_p),
                 ("wf_tail", ctypes.c_int), ("wf_finish_waves", ctypes.c_int), ("profile", ctypes.c_int),
-                ("wf_descent_cap", ctypes.c_int), ("wf_postpone", ctypes.c_int)]
+                ("wf_descent_cap", ctypes.c_int), ("wf_postpone", ctypes.c_int), ("wf_wide", ctypes.c_int)]
 
 
 class RtProfile(ctypes.Structure):
@@ -285,7 +285,7 @@ KERNEL_WAVEFRONT = 1
 
 def options(width, height, passes=1, adaptive=True, min_samples=100, tolerance=0.05, max_depth=0, stream=None,
             counters=None, kernel=KERNEL_MEGA, wf_tail=0, wf_finish_waves=0, profile=False, wf_descent_cap=0,
-            wf_postpone=0):
+            wf_postpone=0, wf_wide=0):
     o = RtOptions()
     lib().rt_default_options(ctypes.byref(o))
     o.width, o.height, o.passes = width, height, passes
@@ -294,7 +294,7 @@ def options(width, height, passes=1, adaptive=True, min_samples=100, tolerance=0
     o.stream = stream
     o.counters_device = counters
     o.wf_tail, o.wf_finish_waves, o.profile = wf_tail, wf_finish_waves, int(profile)
-    o.wf_descent_cap, o.wf_postpone = wf_descent_cap, wf_postpone
+    o.wf_descent_cap, o.wf_postpone, o.wf_wide = wf_descent_cap, wf_postpone, wf_wide
     return o
 
 
