@@ -238,6 +238,10 @@ enum {
     RT_CNT_FIN_NODE = 10,
     RT_CNT_FIN_TRI = 11,
     RT_CNT_FIN_RAY = 12,
+    /* cooperative traversal diagnostics: plane-test prescreen survivors and
+     * exact plane-test passes (barycentric tests) */
+    RT_CNT_CAND = 13,
+    RT_CNT_PLANE = 14,
     RT_CNT_COUNT = 16
 };
 
@@ -297,6 +301,10 @@ int rt_save_render(G_Buffer g_buffer, int width, int height, const char *png_pat
 /* the PNG encoder rt_save_render uses (replaces lodepng::encode,
  * rt/save_render.cuh:18-23): host RGBA8 rows top to bottom */
 int rt_write_png(const char *png_path, const uint8_t *rgba_host, int width, int height);
+
+/* self-test of the traversal's reciprocal-based division against IEEE '/'
+ * on n random operand pairs (host); returns the number of mismatches */
+unsigned long long rt_selftest_division(unsigned long long n, unsigned long long seed, unsigned long long *tested);
 
 #ifdef __cplusplus
 }

@@ -77,13 +77,11 @@ int upload_prepared(const rt_host::PreparedHost &h, int ntris, int nindices, rt_
     int rc = RT_OK;
     const uint32_t *nodes = nullptr;
     const int *lights = nullptr;
-    const RtF4 *a = nullptr, *b = nullptr, *c = nullptr, *d = nullptr, *sh = nullptr;
-    const uint32_t *rt = nullptr;
+    const RtF4 *a = nullptr, *sh = nullptr;
+    const RtIsectBary *bary = nullptr;
     const RtDevMaterial *mats = nullptr;
     if ((rc = upload_vec(*s, h.nodes, &nodes)) || (rc = upload_vec(*s, h.isect_a, &a)) ||
-        (rc = upload_vec(*s, h.isect_b, &b)) || (rc = upload_vec(*s, h.isect_c, &c)) ||
-        (rc = upload_vec(*s, h.isect_d, &d)) || (rc = upload_vec(*s, h.isect_rt, &rt)) ||
-        (rc = upload_vec(*s, h.shade, &sh)) ||
+        (rc = upload_vec(*s, h.isect_bary, &bary)) || (rc = upload_vec(*s, h.shade, &sh)) ||
         (rc = upload_vec(*s, h.materials, &mats)) || (rc = upload_vec(*s, h.lights, &lights))) {
         release(s);
         return rc;
@@ -91,10 +89,7 @@ int upload_prepared(const rt_host::PreparedHost &h, int ntris, int nindices, rt_
     RtDevScene &dv = s->dev;
     dv.nodes = nodes;
     dv.isect_a = a;
-    dv.isect_b = b;
-    dv.isect_c = c;
-    dv.isect_d = d;
-    dv.isect_rt = rt;
+    dv.isect_bary = bary;
     dv.shade = sh;
     dv.materials = mats;
     dv.lights = lights;

@@ -17,7 +17,7 @@
 // arithmetic.  Results are bit-identical to the sequential scan.
 #pragma once
 
-#define WF_COOP_LIST 128 // per-wave LDS list of plane-test survivors
+#define WF_COOP_LIST 128 // per-wave LDS list of plane-test candidates
 
 namespace rtk {
 
@@ -26,8 +26,9 @@ namespace rtk {
 __device__ __forceinline__ bool coop_bary(const RtDevScene &sc, uint32_t k, Vec3D o, Vec3D d, float s, float &cx,
                                           float &cy, float &cz, int &tri)
 {
-    const RtF4 B = ldf4(sc.isect_b + k), C = ldf4(sc.isect_c + k), D = ldf4(sc.isect_d + k);
-    const uint2 R = *reinterpret_cast<const uint2 *>(sc.isect_rt + 2 * (size_t)k);
+    const RtIsectBary *rec = sc.isect_bary + k;
+    const RtF4 B = ldf4(&rec->b), C = ldf4(&rec->c), D = ldf4(&rec->d);
+    const uint2 R = *reinterpret_cast<const uint2 *>(&rec->rd);
     const float rd = __uint_as_float(R.x);
     const float px = o.x + d.x * s, py = o.y + d.y * s, pz = o.z + d.z * s;
     const float v2x = px - B.x, v2y = py - B.y, v2z = pz - B.z;
@@ -40,11 +41,34 @@ __device__ __forceinline__ bool coop_bary(const RtDevScene &sc, uint32_t k, Vec3
     return cx >= 0.0f && cx <= 1.0f && cy >= 0.0f && cy <= 1.0f && cz >= 0.0f && cz <= 1.0f;
 }
 
+// A plane-test candidate in the per-wave LDS list: (entry << 6 | owner lane),
+// and the numerator / denominator of s = num / dn.
+struct CoopCand {
+    uint32_t key;
+    uint32_t num, dn;
+};
+
+// Conservative prescreen of the plane test of intersect_triangle
+// (rt/trace_ray.cuh:86-98: reject if d.n == 0 or s < 1e-5, and trace_leaf_node
+// keeps only s < max_t = leaf exit).  s' = num * rcp(dn) is within 2^-21
+// (relative) of the exact s = RN(num / dn) for |dn| >= 2^-100, so a triangle
+// is dropped here only when the exact test would drop it too: s' < 0.99999e-5
+// means s < 1e-5, s' >= 1.00001 * exit means s >= exit.  Everything else
+// (including NaN / inf / tiny dn) goes on to the exact division and test.
+__device__ __forceinline__ bool plane_maybe(float num, float dn, float ex)
+{
+    if (dn == 0.0f) return false;
+    if (!(fabsf(dn) >= 0x1p-100f)) return true;
+    const float sa = num * __builtin_amdgcn_rcpf(dn);
+    return !(sa < 0.0000099999f) && !(sa >= ex * 1.00001f);
+}
+
 // per-lane traversal state
 struct CoopRay {
     bool live;                  // the lane holds an unfinished ray
     bool pend;                  // ... which has reached a non-empty leaf, waiting for the wave's leaf test
     Vec3D o, d;
+    float yx, yy, yz;           // rt_recip_guard(d): the split distance division by reciprocal
     float entry, exit_, root_exit;
     uint32_t node;
     int sp;
@@ -56,6 +80,7 @@ __device__ __forceinline__ void coop_idle(CoopRay &r)
 {
     r.live = r.pend = false;
     r.o = r.d = rt_v3(0, 0, 0);
+    r.yx = r.yy = r.yz = 0.0f;
     r.entry = r.exit_ = r.root_exit = 0.0f;
     r.node = 0;
     r.sp = 0;
@@ -68,6 +93,9 @@ __device__ __forceinline__ bool coop_begin(const RtDevScene &sc, CoopRay &r, Vec
 {
     r.o = o;
     r.d = d;
+    r.yx = rt_recip_guard(d.x);
+    r.yy = rt_recip_guard(d.y);
+    r.yz = rt_recip_guard(d.z);
     r.node = 0;
     r.sp = 0;
     r.pend = false;
@@ -98,6 +126,7 @@ __device__ __forceinline__ bool coop_descend(const RtDevScene &sc, CoopRay &r, S
     // scalar copies: a select between struct members would become a
     // dynamically indexed (scratch) load
     const float ox = r.o.x, oy = r.o.y, oz = r.o.z, dx = r.d.x, dy = r.d.y, dz = r.d.z;
+    const float yx = r.yx, yy = r.yy, yz = r.yz;
     for (int k = 0; k < cap; ++k) {
         const uint2 nd = *reinterpret_cast<const uint2 *>(sc.nodes + 2 * (size_t)r.node);
         if (COUNT) c.v[RT_CNT_NODE]++;
@@ -121,12 +150,13 @@ __device__ __forceinline__ bool coop_descend(const RtDevScene &sc, CoopRay &r, S
         const float split = as_float(nd.x);
         const float oax = axis == 0 ? ox : (axis == 1 ? oy : oz);
         const float dax = axis == 0 ? dx : (axis == 1 ? dy : dz);
+        const float yax = axis == 0 ? yx : (axis == 1 ? yy : yz);
         uint32_t near_c = r.node + 1, far_c = nd.y >> 2;
         if (oax >= split) { // ray_behind_plane (:174-188)
             near_c = nd.y >> 2;
             far_c = r.node + 1;
         }
-        const float t = (split - oax) / dax; // intersect_plane (:190-210)
+        const float t = rt_div_by(split - oax, dax, yax); // intersect_plane (:190-210): (split - o) / d
         if (t >= r.exit_ || t < 0) {
             r.node = near_c;
         } else if (t <= r.entry) {
@@ -147,7 +177,7 @@ __device__ __forceinline__ bool coop_descend(const RtDevScene &sc, CoopRay &r, S
 // pending lanes pop and go back to descending.
 template <bool COUNT, typename STK>
 __device__ __forceinline__ bool coop_leaves(const RtDevScene &sc, CoopRay &r, STK &stk, unsigned long long *wkey,
-                                            uint2 *list, int &tri, float &hbx, float &hby, float &hbz, Cnt &c)
+                                            CoopCand *list, int &tri, float &hbx, float &hby, float &hbz, Cnt &c)
 {
     const int lane = __lane_id();
     const int leaf_count = r.pend ? r.leaf_count : 0;
@@ -174,35 +204,41 @@ __device__ __forceinline__ bool coop_leaves(const RtDevScene &sc, CoopRay &r, ST
             const Vec3D oo = rt_v3(__shfl(r.o.x, j), __shfl(r.o.y, j), __shfl(r.o.z, j));
             const Vec3D dd = rt_v3(__shfl(r.d.x, j), __shfl(r.d.y, j), __shfl(r.d.z, j));
             const float ex = __shfl(r.exit_, j);
-            bool pass = false;
-            float s = 0.0f;
+            bool cand = false;
+            float num = 0.0f, dn = 0.0f;
             if (p < total) {
                 const RtF4 A = ldf4(sc.isect_a + k); // n, d
-                const float dn = dd.x * A.x + dd.y * A.y + dd.z * A.z;
-                s = (A.w - (oo.x * A.x + oo.y * A.y + oo.z * A.z)) / dn;
-                pass = dn != 0 && s >= 0.00001f && s < ex;
+                dn = dd.x * A.x + dd.y * A.y + dd.z * A.z;
+                num = A.w - (oo.x * A.x + oo.y * A.y + oo.z * A.z);
+                cand = plane_maybe(num, dn, ex);
             }
-            const unsigned long long pm = __ballot(pass);
-            if (pass)
-                list[list_n + __popcll(pm & ((1ull << lane) - 1ull))] = make_uint2((k << 6) | (uint32_t)j,
-                                                                                   __float_as_uint(s));
+            const unsigned long long pm = __ballot(cand);
+            if (cand)
+                list[list_n + __popcll(pm & ((1ull << lane) - 1ull))] =
+                    CoopCand{(k << 6) | (uint32_t)j, __float_as_uint(num), __float_as_uint(dn)};
+            if (COUNT && cand) c.v[RT_CNT_CAND]++;
             list_n += __popcll(pm);
         }
-        // barycentric stage over up to 64 listed candidates
+        // exact plane + barycentric stage over up to 64 listed candidates
         if (list_n >= 64 || (base + 64 >= total && list_n > 0)) {
             const int take = list_n < 64 ? list_n : 64;
-            const uint2 it = list[lane < take ? lane : 0];
-            const int j = (int)(it.x & 63u);
+            const CoopCand it = list[lane < take ? lane : 0];
+            const int j = (int)(it.key & 63u);
             const Vec3D oo = rt_v3(__shfl(r.o.x, j), __shfl(r.o.y, j), __shfl(r.o.z, j));
             const Vec3D dd = rt_v3(__shfl(r.d.x, j), __shfl(r.d.y, j), __shfl(r.d.z, j));
+            const float ex = __shfl(r.exit_, j);
             if (lane < take) {
+                const float dn = __uint_as_float(it.dn);
+                const float s = __uint_as_float(it.num) / dn; // intersect_triangle (:95-98)
                 float cx, cy, cz;
                 int t;
-                if (coop_bary(sc, it.x >> 6, oo, dd, __uint_as_float(it.y), cx, cy, cz, t))
-                    atomicMin(wkey + j, ((unsigned long long)it.y << 32) | (it.x >> 6));
+                const bool plane = dn != 0 && s >= 0.00001f && s < ex;
+                if (COUNT && plane) c.v[RT_CNT_PLANE]++;
+                if (plane && coop_bary(sc, it.key >> 6, oo, dd, s, cx, cy, cz, t))
+                    atomicMin(wkey + j, ((unsigned long long)__float_as_uint(s) << 32) | (it.key >> 6));
             }
             const int rest = list_n - take; // move the rest (< 64) to the front
-            uint2 mv = make_uint2(0, 0);
+            CoopCand mv = CoopCand{0u, 0u, 0u};
             if (lane < rest) mv = list[take + lane];
             if (lane < rest) list[lane] = mv;
             list_n = rest;
@@ -236,7 +272,7 @@ __device__ __forceinline__ bool coop_leaves(const RtDevScene &sc, CoopRay &r, ST
 // a lane whose ray finished in this round (tri / barycentrics as above).
 template <bool COUNT, typename STK>
 __device__ __forceinline__ bool coop_round(const RtDevScene &sc, CoopRay &r, STK &stk, unsigned long long *wkey,
-                                           uint2 *list, int cap, int postpone, int &tri, float &hbx, float &hby,
+                                           CoopCand *list, int cap, int postpone, int &tri, float &hbx, float &hby,
                                            float &hbz, Cnt &c)
 {
     bool done = false;
@@ -294,11 +330,12 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v)
 // Counters are added by `counter_lane` only.
 template <bool COUNT>
 __device__ __forceinline__ void wide_trace(const RtDevScene &sc, Vec3D o, Vec3D d, float entry, float exit_,
-                                           WideItem *F, unsigned long long *wkey, uint2 *list, bool counter_lane,
+                                           WideItem *F, unsigned long long *wkey, CoopCand *list, bool counter_lane,
                                            int &tri, float &hbx, float &hby, float &hbz, Cnt &c)
 {
     const int lane = __lane_id();
     const float ox = o.x, oy = o.y, oz = o.z, dx = d.x, dy = d.y, dz = d.z;
+    const float yx = rt_recip_guard(dx), yy = rt_recip_guard(dy), yz = rt_recip_guard(dz);
     if (lane == 0) F[0] = WideItem{0u, entry, exit_, 0u};
     int n = 1;
     tri = -1;
@@ -343,32 +380,36 @@ __device__ __forceinline__ void wide_trace(const RtDevScene &sc, Vec3D o, Vec3D 
                     const uint32_t kk = nd.x; // leaf_begin of this lane
                     const uint32_t e = (uint32_t)__shfl((int)kk, j) + (uint32_t)(p - __shfl(start, j));
                     const float ex = __shfl(it.exit_, j);
-                    bool pass = false;
-                    float s = 0.0f;
+                    bool cand = false;
+                    float num = 0.0f, dn = 0.0f;
                     if (p < total) {
                         const RtF4 A = ldf4(sc.isect_a + e);
-                        const float dn = dx * A.x + dy * A.y + dz * A.z;
-                        s = (A.w - (ox * A.x + oy * A.y + oz * A.z)) / dn;
-                        pass = dn != 0 && s >= 0.00001f && s < ex;
+                        dn = dx * A.x + dy * A.y + dz * A.z;
+                        num = A.w - (ox * A.x + oy * A.y + oz * A.z);
+                        cand = plane_maybe(num, dn, ex);
                     }
-                    const unsigned long long pm = __ballot(pass);
-                    if (pass)
+                    const unsigned long long pm = __ballot(cand);
+                    if (cand)
                         list[list_n + __popcll(pm & ((1ull << lane) - 1ull))] =
-                            make_uint2((e << 6) | (uint32_t)j, __float_as_uint(s));
+                            CoopCand{(e << 6) | (uint32_t)j, __float_as_uint(num), __float_as_uint(dn)};
                     list_n += __popcll(pm);
                 }
                 if (list_n >= 64 || (base + 64 >= total && list_n > 0)) {
                     const int take = list_n < 64 ? list_n : 64;
-                    const uint2 itm = list[lane < take ? lane : 0];
+                    const CoopCand itm = list[lane < take ? lane : 0];
+                    const float ex = __shfl(it.exit_, (int)(itm.key & 63u));
                     if (lane < take) {
+                        const float dn = __uint_as_float(itm.dn);
+                        const float s = __uint_as_float(itm.num) / dn;
                         float cx, cy, cz;
                         int t;
-                        if (coop_bary(sc, itm.x >> 6, o, d, __uint_as_float(itm.y), cx, cy, cz, t))
-                            atomicMin(wkey, ((unsigned long long)(itm.x & 63u) << 58) |
-                                                ((unsigned long long)itm.y << 26) | (unsigned long long)(itm.x >> 6));
+                        if (dn != 0 && s >= 0.00001f && s < ex && coop_bary(sc, itm.key >> 6, o, d, s, cx, cy, cz, t))
+                            atomicMin(wkey, ((unsigned long long)(itm.key & 63u) << 58) |
+                                                ((unsigned long long)__float_as_uint(s) << 26) |
+                                                (unsigned long long)(itm.key >> 6));
                     }
                     const int rest = list_n - take;
-                    uint2 mv = make_uint2(0, 0);
+                    CoopCand mv = CoopCand{0u, 0u, 0u};
                     if (lane < rest) mv = list[take + lane];
                     if (lane < rest) list[lane] = mv;
                     list_n = rest;
@@ -401,12 +442,13 @@ __device__ __forceinline__ void wide_trace(const RtDevScene &sc, Vec3D o, Vec3D 
                 const float split = as_float(nd.x);
                 const float oax = axis == 0 ? ox : (axis == 1 ? oy : oz);
                 const float dax = axis == 0 ? dx : (axis == 1 ? dy : dz);
+                const float yax = axis == 0 ? yx : (axis == 1 ? yy : yz);
                 uint32_t near_c = it.node + 1, far_c = nd.y >> 2;
                 if (oax >= split) { // ray_behind_plane (:174-188)
                     near_c = nd.y >> 2;
                     far_c = it.node + 1;
                 }
-                const float t = (split - oax) / dax; // intersect_plane (:190-210)
+                const float t = rt_div_by(split - oax, dax, yax); // intersect_plane (:190-210)
                 if (t >= it.exit_ || t < 0) {
                     a = WideItem{near_c, it.entry, it.exit_, it.acc + 1u};
                 } else if (t <= it.entry) {

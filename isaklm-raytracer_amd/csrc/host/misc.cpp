@@ -103,3 +103,46 @@ int write_png(const char *path, const uint8_t *rgba, int w, int h)
 }
 
 } // namespace rt_host
+
+// self-test hook: rt_div_by (the traversal's division) against IEEE '/' on
+// random operands in and around its guarded range; returns mismatches
+extern "C" unsigned long long rt_selftest_division(unsigned long long n, unsigned long long seed,
+                                                   unsigned long long *tested)
+{
+    unsigned long long x = seed * 2654435761ull + 88172645463325252ull, bad = 0, t = 0;
+    auto rnd = [&]() {
+        x ^= x << 13;
+        x ^= x >> 7;
+        x ^= x << 17;
+        return (uint32_t)(x >> 11);
+    };
+    auto bits = [](uint32_t u) {
+        float f;
+        memcpy(&f, &u, 4);
+        return f;
+    };
+    for (unsigned long long i = 0; i < n; ++i) {
+        const uint32_t ua = rnd(), ub = rnd();
+        float a, b;
+        switch (i & 3) {
+        case 0: a = bits(ua); b = bits(ub); break;                                  // any bits
+        case 1: a = (float)(int32_t)ua * 1e-7f; b = (float)(int32_t)ub * 4.7e-10f; break; // scene-like
+        case 2: // exponents inside the guard window
+            a = bits((ua & 0x807fffffu) | (((ua >> 23) % 100 + 67) << 23));
+            b = bits((ub & 0x807fffffu) | (((ub >> 23) % 100 + 67) << 23));
+            break;
+        default: // powers of two and near-guard exponents
+            a = bits((ua & 0x80000000u) | (((ua >> 23) % 110 + 60) << 23) | (ua & 1u ? 0u : (ua & 0x7fffffu)));
+            b = bits((ub & 0x80000000u) | (((ub >> 23) % 110 + 60) << 23) | (ub & 1u ? 0u : (ub & 0x7fffffu)));
+        }
+        if (!(b == b) || !(a == a)) continue;
+        const float q = a / b, r = rt_div_by(a, b, rt_recip_guard(b));
+        uint32_t uq, ur;
+        memcpy(&uq, &q, 4);
+        memcpy(&ur, &r, 4);
+        ++t;
+        if (uq != ur && !(q == 0.0f && r == 0.0f)) ++bad; // the sign of a zero t is never observed
+    }
+    if (tested) *tested = t;
+    return bad;
+}

@@ -36,8 +36,8 @@ void mt19937_seeds(uint32_t *out, size_t count, uint64_t skip);
 // host image of the device layout (rt_device.h) before upload
 struct PreparedHost {
     std::vector<uint32_t> nodes;
-    std::vector<RtF4> isect_a, isect_b, isect_c, isect_d; // leaf-entry order
-    std::vector<uint32_t> isect_rt;
+    std::vector<RtF4> isect_a;          // leaf-entry order
+    std::vector<RtIsectBary> isect_bary; // leaf-entry order
     std::vector<RtF4> shade;
     std::vector<RtDevMaterial> materials;
     std::vector<int> lights; // light_count + 1

@@ -157,19 +157,18 @@ int prepare_host(const Triangle *tris, int ntris, const KD_Tree_Node *nodes, int
     // ... gathered into leaf-entry order (a leaf's tests read consecutive memory)
     const size_t ne = (size_t)(nindices > 0 ? nindices : 0);
     out.isect_a.resize(ne);
-    out.isect_b.resize(ne);
-    out.isect_c.resize(ne);
-    out.isect_d.resize(ne);
-    out.isect_rt.resize(2 * ne);
+    out.isect_bary.resize(ne);
 #pragma omp parallel for schedule(static)
     for (long long e = 0; e < (long long)ne; ++e) {
         const int t = indices[e];
         out.isect_a[e] = ta[t];
-        out.isect_b[e] = tb[t];
-        out.isect_c[e] = tc[t];
-        out.isect_d[e] = td[t];
-        out.isect_rt[2 * e] = fbits(tr[t]);
-        out.isect_rt[2 * e + 1] = (uint32_t)t;
+        RtIsectBary &r = out.isect_bary[e];
+        r.b = tb[t];
+        r.c = tc[t];
+        r.d = td[t];
+        r.rd = fbits(tr[t]);
+        r.tri = (uint32_t)t;
+        r.pad[0] = r.pad[1] = 0;
     }
 
     // --- lights: one padding entry for the xi == 1.0 draw -----

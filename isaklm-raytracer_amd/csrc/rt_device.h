@@ -10,15 +10,15 @@
 //      leaf:   x = index_offset,      y = (triangle_count << 2) | 3
 //  * intersection constants in LEAF-ENTRY order (entry e = position in the
 //    KD triangle_indicies array, so a leaf's tests read consecutive memory
-//    and need no index load first), SoA float4 streams, each value the
-//    reference's own expression evaluated once:
-//      isect_a  = {n.x, n.y, n.z, d}      n = normalize(cross(p2-p1, p3-p1)), d = dot(n, p1)
-//      isect_b  = {p1.x, p1.y, p1.z, d00}
-//      isect_c  = {v0.x, v0.y, v0.z, d01} v0 = p2-p1
-//      isect_d  = {v1.x, v1.y, v1.z, d11} v1 = p3-p1
-//      isect_rt = {bits(1/(d00*d11 - d01*d01)), triangle index}
+//    and need no index load first), each value the reference's own
+//    expression evaluated once:
+//      isect_a[e]    = {n.x, n.y, n.z, d}   n = normalize(cross(p2-p1, p3-p1)), d = dot(n, p1)
+//                      (16-B stream: every test reads it)
+//      isect_bary[e] = one 64-B record (one cache line per candidate):
+//                      {p1, d00}, {v0 = p2-p1, d01}, {v1 = p3-p1, d11},
+//                      {bits(1/(d00*d11 - d01*d01)), triangle index, -, -}
 //    A test that is rejected by the plane (dn == 0, s < 1e-5, s >= closest)
-//    reads only isect_a (16 B).
+//    reads only isect_a (16 B); about 1 in 5 goes on to the record.
 //  * shading record (hit only), 7 float4 per triangle: p1..p3, n1..n3,
 //    uv1..uv3 and the material id; materials deduplicated into a table.
 #pragma once
@@ -51,10 +51,20 @@ static_assert(sizeof(RtDevMaterial) == 64, "RtDevMaterial");
 
 struct RtF4 { float x, y, z, w; };
 
+struct RtIsectBary {            // 64 B, one per leaf entry
+    RtF4 b;                     // p1, d00
+    RtF4 c;                     // v0, d01
+    RtF4 d;                     // v1, d11
+    uint32_t rd;                // bits(1 / (d00*d11 - d01*d01))
+    uint32_t tri;               // triangle index
+    uint32_t pad[2];
+};
+static_assert(sizeof(RtIsectBary) == 64, "RtIsectBary");
+
 struct RtDevScene {
     const uint32_t *nodes;      // 2 words per node
-    const RtF4 *isect_a, *isect_b, *isect_c, *isect_d; // per leaf entry
-    const uint32_t *isect_rt;   // 2 words per leaf entry: rd bits, triangle index
+    const RtF4 *isect_a;        // per leaf entry: plane
+    const RtIsectBary *isect_bary; // per leaf entry: barycentric-test record
     const RtF4 *shade;          // 7 per triangle
     const RtDevMaterial *materials;
     const int *lights;          // light_count + 1 entries (SURVEY H4 padding)

@@ -16,10 +16,10 @@ namespace rtk {
 enum { PRIMARY = 0, DIFFUSE = 1, SPECULAR = 2, METALLIC = 3, TRANSMISSION = 4 }; // :18-25
 
 struct Cnt {
-    unsigned long long v[10]; // RT_CNT_* ; v[RT_CNT_MAXDEPTH] is a max
+    unsigned long long v[RT_CNT_COUNT]; // RT_CNT_* ; v[RT_CNT_MAXDEPTH] is a max
     __device__ void zero()
     {
-        for (int k = 0; k < 10; ++k) v[k] = 0;
+        for (int k = 0; k < RT_CNT_COUNT; ++k) v[k] = 0;
     }
     __device__ void path_end(int depth)
     {
@@ -155,16 +155,16 @@ __device__ __forceinline__ int trace(const RtDevScene &sc, const Vec3D o, const 
                 RtF4 B0, C0, D0, B1, C1, D1;
                 uint2 R0, R1;
                 if (p0) {
-                    B0 = ldf4(sc.isect_b + e); // p1, d00
-                    C0 = ldf4(sc.isect_c + e); // v0, d01
-                    D0 = ldf4(sc.isect_d + e); // v1, d11
-                    R0 = *reinterpret_cast<const uint2 *>(sc.isect_rt + 2 * (size_t)e);
+                    B0 = ldf4(&sc.isect_bary[e].b); // p1, d00
+                    C0 = ldf4(&sc.isect_bary[e].c); // v0, d01
+                    D0 = ldf4(&sc.isect_bary[e].d); // v1, d11
+                    R0 = *reinterpret_cast<const uint2 *>(&sc.isect_bary[e].rd);
                 }
                 if (p1) {
-                    B1 = ldf4(sc.isect_b + e + 1);
-                    C1 = ldf4(sc.isect_c + e + 1);
-                    D1 = ldf4(sc.isect_d + e + 1);
-                    R1 = *reinterpret_cast<const uint2 *>(sc.isect_rt + 2 * (size_t)(e + 1));
+                    B1 = ldf4(&sc.isect_bary[e + 1].b);
+                    C1 = ldf4(&sc.isect_bary[e + 1].c);
+                    D1 = ldf4(&sc.isect_bary[e + 1].d);
+                    R1 = *reinterpret_cast<const uint2 *>(&sc.isect_bary[e + 1].rd);
                 }
 #pragma unroll
                 for (int k = 0; k < 2; ++k) {
@@ -431,7 +431,7 @@ __device__ __forceinline__ Vec3D light_contribution(const RtDevScene &sc, int li
 // counters: wave-reduce and add once per wave
 __device__ __forceinline__ void flush_counters(Cnt &c, unsigned long long *out)
 {
-    for (int k = 0; k < 10; ++k) {
+    for (int k = 0; k < RT_CNT_COUNT; ++k) {
         unsigned long long v = c.v[k];
         for (int off = 32; off > 0; off >>= 1) {
             unsigned long long o = __shfl_xor(v, off);
@@ -440,8 +440,8 @@ __device__ __forceinline__ void flush_counters(Cnt &c, unsigned long long *out)
         c.v[k] = v;
     }
     if ((threadIdx.x & 63) == 0) {
-        for (int k = 0; k < 9; ++k)
-            if (c.v[k]) atomicAdd(out + k, c.v[k]);
+        for (int k = 0; k < RT_CNT_COUNT; ++k)
+            if (k != RT_CNT_MAXDEPTH && c.v[k]) atomicAdd(out + k, c.v[k]);
         atomicMax(out + RT_CNT_MAXDEPTH, c.v[RT_CNT_MAXDEPTH]);
     }
 }

@@ -32,6 +32,31 @@ RT_HD float rt_square(float x) { return x * x; }                                
 RT_HD float rt_clamp(float x, float lo, float hi) { return fmaxf(lo, fminf(hi, x)); } // :22-25
 RT_HD float rt_mod(float x, float m) { return x - m * floorf(x / m); }            // :32-35
 
+// Correctly rounded n / d for a fixed d from its reciprocal (Markstein):
+// with y = RN(1/d), q0 = RN(n*y) is within 1 ulp of n/d, the residual
+// e = n - d*q0 is exact in one fma, and RN(q0 + e*y) = RN(n/d) — the same
+// bits as the IEEE division the reference performs, in 3 VALU ops instead of
+// the ~10 of a full division.  Valid without over/underflow, which the range
+// guards (|n|, |d| in [2^-60, 2^40]) ensure; outside them (axis-parallel rays,
+// origins on a split plane) the plain division runs.  Used for the KD split
+// distance t = (split - o) / d, whose d is one of the ray's 3 components.
+// tests/test_host.py::test_division_matches_ieee checks it against '/'.
+RT_HD float rt_recip_guard(float d)
+{
+    const float a = fabsf(d);
+    return (a >= 0x1p-60f && a <= 0x1p40f) ? 1.0f / d : 0.0f; // 0: use the plain division
+}
+RT_HD float rt_div_by(float n, float d, float y)
+{
+    const float a = fabsf(n);
+    if (y != 0.0f && a >= 0x1p-60f && a <= 0x1p40f) {
+        const float q0 = n * y;
+        const float e = fmaf(-d, q0, n);
+        return fmaf(e, y, q0);
+    }
+    return n / d;
+}
+
 RT_HD Vec2D operator+(Vec2D a, Vec2D b) { return rt_v2(a.x + b.x, a.y + b.y); }   // :68-71
 RT_HD Vec2D operator*(Vec2D v, float s) { return rt_v2(v.x * s, v.y * s); }       // :78-81
 RT_HD Vec3D operator+(Vec3D a, Vec3D b) { return rt_v3(a.x + b.x, a.y + b.y, a.z + b.z); } // :117-120

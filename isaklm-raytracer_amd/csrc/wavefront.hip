@@ -260,16 +260,16 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_trace_dyn(RtDevScene sc, WfState 
                 RtF4 B0, C0, D0, B1, C1, D1;
                 uint2 R0, R1;
                 if (p0) {
-                    B0 = ldf4(sc.isect_b + k);
-                    C0 = ldf4(sc.isect_c + k);
-                    D0 = ldf4(sc.isect_d + k);
-                    R0 = *reinterpret_cast<const uint2 *>(sc.isect_rt + 2 * (size_t)k);
+                    B0 = ldf4(&sc.isect_bary[k].b);
+                    C0 = ldf4(&sc.isect_bary[k].c);
+                    D0 = ldf4(&sc.isect_bary[k].d);
+                    R0 = *reinterpret_cast<const uint2 *>(&sc.isect_bary[k].rd);
                 }
                 if (p1) {
-                    B1 = ldf4(sc.isect_b + k + 1);
-                    C1 = ldf4(sc.isect_c + k + 1);
-                    D1 = ldf4(sc.isect_d + k + 1);
-                    R1 = *reinterpret_cast<const uint2 *>(sc.isect_rt + 2 * (size_t)(k + 1));
+                    B1 = ldf4(&sc.isect_bary[k + 1].b);
+                    C1 = ldf4(&sc.isect_bary[k + 1].c);
+                    D1 = ldf4(&sc.isect_bary[k + 1].d);
+                    R1 = *reinterpret_cast<const uint2 *>(&sc.isect_bary[k + 1].rd);
                 }
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
@@ -320,20 +320,20 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_trace_dyn(RtDevScene sc, WfState 
 // capped at `cap` node fetches per round and the leaf test waits for
 // `postpone` pending lanes.
 template <bool COUNT>
-__global__ void __launch_bounds__(WF_BLOCK) wf_trace_coop(RtDevScene sc, WfState st, int q,
+__global__ void __launch_bounds__(WF_BLOCK, 6) wf_trace_coop(RtDevScene sc, WfState st, int q,
                                                           unsigned long long *counters, int cap, int postpone)
 {
     __shared__ uint32_t s_node[WF_LDS_STACK * WF_BLOCK];
     __shared__ float s_entry[WF_LDS_STACK * WF_BLOCK];
     __shared__ unsigned long long s_key[WF_BLOCK];
-    __shared__ uint2 s_list[(WF_BLOCK / 64) * WF_COOP_LIST];
+    __shared__ CoopCand s_list[(WF_BLOCK / 64) * WF_COOP_LIST];
     const int tid = threadIdx.x;
     const int gtid = blockIdx.x * WF_BLOCK + tid;
     const int lane = __lane_id();
     const int wave = tid >> 6;
     Stack<WF_LDS_STACK> stk{s_node + tid, s_entry + tid, WF_BLOCK, st.spill + gtid, st.spill_threads};
     unsigned long long *wkey = s_key + wave * 64;
-    uint2 *list = s_list + wave * WF_COOP_LIST;
+    CoopCand *list = s_list + wave * WF_COOP_LIST;
     Cnt c;
     if (COUNT) c.zero();
     const uint32_t n = st.counts[q];
@@ -593,7 +593,7 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_finish_coop(RtDevScene sc, RtDevF
     __shared__ uint32_t s_node[WF_LDS_STACK * WF_BLOCK];
     __shared__ float s_entry[WF_LDS_STACK * WF_BLOCK];
     __shared__ unsigned long long s_key[WF_BLOCK];
-    __shared__ uint2 s_list[(WF_BLOCK / 64) * WF_COOP_LIST];
+    __shared__ CoopCand s_list[(WF_BLOCK / 64) * WF_COOP_LIST];
     __shared__ WideItem s_wide[(WF_BLOCK / 64) * WIDE_CAP];
     const int tid = threadIdx.x;
     const int gtid = blockIdx.x * WF_BLOCK + tid;
@@ -601,7 +601,7 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_finish_coop(RtDevScene sc, RtDevF
     const int wave = tid >> 6;
     Stack<WF_LDS_STACK> stk{s_node + tid, s_entry + tid, WF_BLOCK, st.spill + gtid, st.spill_threads};
     unsigned long long *wkey = s_key + wave * 64;
-    uint2 *list = s_list + wave * WF_COOP_LIST;
+    CoopCand *list = s_list + wave * WF_COOP_LIST;
     Cnt c;
     if (COUNT) c.zero();
     const uint32_t n = st.counts[q];

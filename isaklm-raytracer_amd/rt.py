@@ -71,7 +71,7 @@ def last_profile():
 TRIANGLE_BYTES = 152
 NODE_BYTES = 20
 COUNTER_NAMES = ["node", "tri", "hit", "texel", "nee", "sample", "skip", "ray", "watchdog", "maxdepth"]
-FINISH_COUNTER_NAMES = ["finish_node", "finish_tri", "finish_ray"]
+FINISH_COUNTER_NAMES = ["finish_node", "finish_tri", "finish_ray", "cand", "plane"]
 N_COUNTERS = 16
 
 _lib = None

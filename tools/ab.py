@@ -48,7 +48,7 @@ def main():
         cnt = rt.DeviceCounters()
         opt = opts(v, counters=cnt.p)
         rt.render(run.dev, g, run.camera, 0, opt)
-        c = cnt.read()
+        c = cnt.read(finisher=True)
         ts = np.array(times[v])
         out[v] = {"msamples_s_median": round(W * H * P / np.median(ts) / 1e6, 3),
                   "msamples_s_best": round(W * H * P / ts.min() / 1e6, 3),
@@ -56,7 +56,7 @@ def main():
                   "trace_ms": [round(p["trace_ms"]) for p in profs[v]],
                   "finish_ms": [round(p["finish_ms"]) for p in profs[v]],
                   "iterations": [p["iterations"] for p in profs[v]],
-                  "per_sample": {k: round(c[k] / max(c["sample"], 1), 2) for k in ("ray", "node", "tri")}}
+                  "per_sample": {k: round(c[k] / max(c["sample"], 1), 2) for k in ("ray", "node", "tri", "cand", "plane")}}
     print(json.dumps({"scene": scene, "passes": P, "max_depth": maxd, "variants": out}, indent=1))
 
 
