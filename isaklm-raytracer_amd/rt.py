@@ -13,6 +13,8 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libisaklm_rt.so")
+# tooling only (tools/ab.py A/B of kernel builds): load another build of the same library
+LIB_PATH = os.environ.get("ISAKLM_RT_LIB_OVERRIDE", LIB_PATH)
 
 
 class Vec3D(ctypes.Structure):
