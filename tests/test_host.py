@@ -149,3 +149,17 @@ def test_png_writer_roundtrip(tmp_path, w, h):
     L.rt_write_png.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
     rt.check(L.rt_write_png(path.encode(), img.ctypes.data, w, h))
     np.testing.assert_array_equal(_decode_png(path), img)
+
+
+def test_division_matches_ieee():
+    """rt_div_by (reciprocal + Markstein correction, used for the KD split
+    distance on the GPU) gives the bits of IEEE '/' on 2e7 random operand
+    pairs in and around its guarded range (the same inline function is
+    compiled for the device)."""
+    f = rt.lib().rt_selftest_division
+    f.restype = ctypes.c_ulonglong
+    f.argtypes = [ctypes.c_ulonglong, ctypes.c_ulonglong, ctypes.POINTER(ctypes.c_ulonglong)]
+    tested = ctypes.c_ulonglong()
+    bad = f(20_000_000, 7, ctypes.byref(tested))
+    assert tested.value > 19_000_000
+    assert bad == 0
