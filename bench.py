@@ -105,6 +105,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel", choices=["mega", "wavefront"], default="wavefront")
+    ap.add_argument("--shard-mode", choices=["spp", "rows"], default="spp",
+                    help="N>1: spp slices (north star, seeds skipped per rank) or row-interleaved shards "
+                         "(bit-identical to one GPU)")
     ap.add_argument("--scene-dir", default=os.environ.get("RT_SCENE_DIR", os.path.join(ROOT, "build", "scenes")))
     args = ap.parse_args()
 
@@ -135,12 +138,14 @@ def main():
 
     W, H, P = args.width, args.height, args.passes
     n = W * H
-    gb = TorchGBuffer(torch, n, shard.seed_skip(rank, W, H))
+    rows = args.shard_mode == "rows" and world > 1
+    gb = TorchGBuffer(torch, n, 0 if rows else shard.seed_skip(rank, W, H))
     stream = torch.cuda.current_stream()
     kernel = rt.KERNEL_WAVEFRONT if args.kernel == "wavefront" else rt.KERNEL_MEGA
     wavefront = kernel == rt.KERNEL_WAVEFRONT
+    shard_kw = dict(shard_id=rank, num_shards=world) if rows else {}
     opt = rt.options(W, H, P, adaptive=False, stream=ctypes.c_void_p(stream.cuda_stream), kernel=kernel,
-                     profile=wavefront)
+                     profile=wavefront, **shard_kw)
     profiles = []
 
     def step(i):
@@ -177,16 +182,16 @@ def main():
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
     kernel_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
-    total_samples = world * n * P * args.steps
+    total_samples = (1 if rows else world) * n * P * args.steps
     value = total_samples / elapsed / 1e6
 
     # samples actually accumulated (every pixel, every pass: adaptive off)
-    expect = world * P * (args.warmup + args.steps)
+    expect = (1 if rows else world) * P * (args.warmup + args.steps)
     got = int(gb.cnt.sum().item()) if rank == 0 else None
 
     # work counters on one extra (untimed) step -> algorithmic bytes per call
     counters = rt.DeviceCounters()
-    copt = rt.options(W, H, P, adaptive=False, counters=counters.p, kernel=kernel, profile=wavefront)
+    copt = rt.options(W, H, P, adaptive=False, counters=counters.p, kernel=kernel, profile=wavefront, **shard_kw)
     rt.render(dscene, gb, host.camera, 1, copt)
     c = counters.read(finisher=True)
     bytes_per_call = algorithmic_bytes(c)
@@ -230,7 +235,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if rows else "weak",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic",
@@ -239,7 +244,8 @@ def main():
                         f"{P} spp per step, adaptive off",
             "scene": args.scene, "width": W, "height": H, "spp_per_step": P,
             "triangles": info["triangles"], "kd_nodes": info["nodes"], "kd_indices": info["indices"],
-            "parallelism": f"spp-sliced x{world} + RCCL reduce" if world > 1 else "single GPU",
+            "parallelism": (f"{'row-interleaved' if rows else 'spp-sliced'} x{world} + RCCL reduce" if world > 1
+                            else "single GPU"),
         },
         "roofline": {
             "bound": "hbm",

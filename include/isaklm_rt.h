@@ -271,6 +271,16 @@ typedef struct RtOptions {
     int wf_descent_cap;
     int wf_postpone;
     int wf_wide;         /* finisher: a wave's lone ray is traced by all 64 lanes (0 = on, < 0 = off) */
+    /* row-interleaved sharding (the parity-exact option): with
+     * num_shards > 1 only rows y % num_shards == shard_id are rendered (the
+     * others are left untouched); every shard uses the single-stream seeds,
+     * so each owned pixel is bit-identical to the one-GPU render, adaptive
+     * sampling included, and a sum of the shards' zero-initialised buffers
+     * (rt_reduce_shards) is the one-GPU frame.  The spp-slice sharding of the
+     * north star needs no option: seed shard g's G_Buffer from mt19937 outputs
+     * [g*W*H, (g+1)*W*H) (rt_gbuffer_seeds skip). */
+    int shard_id;
+    int num_shards;
 } RtOptions;
 
 /* Per-call kernel timing of the last rt_render on this device with
@@ -301,6 +311,20 @@ int rt_save_render(G_Buffer g_buffer, int width, int height, const char *png_pat
 /* the PNG encoder rt_save_render uses (replaces lodepng::encode,
  * rt/save_render.cuh:18-23): host RGBA8 rows top to bottom */
 int rt_write_png(const char *png_path, const uint8_t *rgba_host, int width, int height);
+
+/* ---------------- multi-GPU shards ----------------
+ * One process per GPU.  Rank 0 makes an id (rt_comm_unique_id), ships its
+ * RT_COMM_ID_BYTES to the other ranks out of band, every rank calls
+ * rt_comm_create, renders its shard (spp slice: seeds skipped by g*W*H; or
+ * rows: RtOptions.shard_id / num_shards), then rt_reduce_shards sums fb, sq
+ * and count of every rank into `root` (one RCCL reduce per array, grouped;
+ * stream NULL = synchronous). */
+#define RT_COMM_ID_BYTES 128
+typedef struct RtComm *rt_comm_t;
+int rt_comm_unique_id(void *id_out);
+int rt_comm_create(int nranks, int rank, const void *id, rt_comm_t *out);
+int rt_comm_destroy(rt_comm_t comm);
+int rt_reduce_shards(rt_comm_t comm, G_Buffer g_buffer, int width, int height, int root, void *stream);
 
 /* self-test of the traversal's reciprocal-based division against IEEE '/'
  * on n random operand pairs (host); returns the number of mismatches */

@@ -20,7 +20,7 @@ ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
 HOST_SOURCES = ["host/mesh_loading.cpp", "host/kd_build.cpp", "host/scene_prepare.cpp", "host/misc.cpp",
                 "host/scenes.cpp"]
-HIP_SOURCES = ["path_kernel.hip", "wavefront.hip", "abi.hip"]
+HIP_SOURCES = ["path_kernel.hip", "wavefront.hip", "abi.hip", "shards.hip"]
 HEADERS = ["rt_libm.h", "rt_vecmath.h", "rt_device.h", "rt_kernels.h", "host/rt_host.h"]
 
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-I" + INCLUDE, "-I" + CSRC]
@@ -84,7 +84,7 @@ def build(verbose=False, extra_hip_flags=()):
         objs.append(o)
     if _stale(LIB, objs):
         _run(["g++", "-shared", "-o", LIB] + objs +
-             ["-L" + os.path.join(ROCM, "lib"), "-lamdhip64", "-fopenmp",
+             ["-L" + os.path.join(ROCM, "lib"), "-lamdhip64", "-lrccl", "-fopenmp",
               "-Wl,-rpath," + os.path.join(ROCM, "lib")], verbose)
     with open(STAMP, "w") as fh:
         fh.write(digest + "\n")

@@ -368,6 +368,10 @@ int rt_render(rt_scene_t scene, G_Buffer g, Camera cam, int sample_count, const 
         rt_set_error("rt_render: bad frame size / passes");
         return RT_E_INVALID;
     }
+    if (o.num_shards > 1 && (o.shard_id < 0 || o.shard_id >= o.num_shards)) {
+        rt_set_error("rt_render: shard_id %d out of [0, %d)", o.shard_id, o.num_shards);
+        return RT_E_INVALID;
+    }
     RtDevFrame fr;
     fr.fb = g.frame_buffer;
     fr.sq = g.squared_luminance;
@@ -384,6 +388,8 @@ int rt_render(rt_scene_t scene, G_Buffer g, Camera cam, int sample_count, const 
     fr.z_const = rt_adaptive_z(o.tolerance);
     fr.max_depth = o.max_depth;
     fr.reset = sample_count == 0;
+    fr.shard_id = o.num_shards > 1 ? o.shard_id : 0;
+    fr.num_shards = o.num_shards > 1 ? o.num_shards : 1;
     fr.counters = o.counters_device;
     fr.wave_times = o.wave_times_device;
 

@@ -38,7 +38,7 @@ __global__ void __launch_bounds__(RT_BLOCK, STACK <= RT_STACK_SMALL ? 4 : 2) rt_
     const int wave = tid >> 6, lane = tid & 63;
     const int x = (tile % tiles_x) * 16 + (wave & 1) * 8 + (lane & 7);
     const int y = (tile / tiles_x) * 16 + (wave >> 1) * 8 + (lane >> 3);
-    const bool valid = x < fr.width && y < fr.height;
+    const bool valid = x < fr.width && y < fr.height && rt_row_owned(fr, y);
     const int pi = valid ? y * fr.width + x : 0;
     Stack<STACK> stk{s_node + tid, s_entry + tid, RT_BLOCK, nullptr, 0};
 

@@ -96,4 +96,5 @@ struct RtDevFrame {
     int reset;                  // sample_count == 0
     unsigned long long *counters;
     unsigned long long *wave_times; // debug: per-wave s_memrealtime [start, end] (counting variant)
+    int shard_id, num_shards;   // row-interleaved sharding: render rows y % num_shards == shard_id
 };

@@ -29,6 +29,12 @@ struct Cnt {
 
 __device__ __forceinline__ float as_float(uint32_t u) { return __uint_as_float(u); }
 
+// the pixel rows this call renders (RtOptions.num_shards > 1: row-interleaved shards)
+__device__ __forceinline__ bool rt_row_owned(const RtDevFrame &fr, int y)
+{
+    return fr.num_shards <= 1 || y % fr.num_shards == fr.shard_id;
+}
+
 // get_random_unilateral (rt/path_tracing.cuh:34-43)
 __device__ __forceinline__ float rng_next(uint32_t &st)
 {

@@ -100,7 +100,7 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_start(RtDevFrame fr, RtDevCamera 
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int x = (tile % tiles_x) * 16 + (wave & 1) * 8 + (lane & 7);
     const int y = (tile / tiles_x) * 16 + (wave >> 1) * 8 + (lane >> 3);
-    const bool valid = x < fr.width && y < fr.height;
+    const bool valid = x < fr.width && y < fr.height && rt_row_owned(fr, y);
     const int slot = valid ? y * fr.width + x : 0;
     bool want = false;
     Vec3D ro = rt_v3(0, 0, 0), rd = rt_v3(0, 0, 0);

@@ -54,7 +54,8 @@ class RtOptions(ctypes.Structure):
                 ("max_depth", ctypes.c_int), ("kernel", ctypes.c_int), ("stream", ctypes.c_void_p),
                 ("counters_device", ctypes.c_void_p), ("wave_times_device", ctypes.c_void_p),
                 ("wf_tail", ctypes.c_int), ("wf_finish_waves", ctypes.c_int), ("profile", ctypes.c_int),
-                ("wf_descent_cap", ctypes.c_int), ("wf_postpone", ctypes.c_int), ("wf_wide", ctypes.c_int)]
+                ("wf_descent_cap", ctypes.c_int), ("wf_postpone", ctypes.c_int), ("wf_wide", ctypes.c_int),
+                ("shard_id", ctypes.c_int), ("num_shards", ctypes.c_int)]
 
 
 class RtProfile(ctypes.Structure):
@@ -287,7 +288,7 @@ KERNEL_WAVEFRONT = 1
 
 def options(width, height, passes=1, adaptive=True, min_samples=100, tolerance=0.05, max_depth=0, stream=None,
             counters=None, kernel=KERNEL_MEGA, wf_tail=0, wf_finish_waves=0, profile=False, wf_descent_cap=0,
-            wf_postpone=0, wf_wide=0):
+            wf_postpone=0, wf_wide=0, shard_id=0, num_shards=1):
     o = RtOptions()
     lib().rt_default_options(ctypes.byref(o))
     o.width, o.height, o.passes = width, height, passes
@@ -297,6 +298,7 @@ def options(width, height, passes=1, adaptive=True, min_samples=100, tolerance=0
     o.counters_device = counters
     o.wf_tail, o.wf_finish_waves, o.profile = wf_tail, wf_finish_waves, int(profile)
     o.wf_descent_cap, o.wf_postpone, o.wf_wide = wf_descent_cap, wf_postpone, wf_wide
+    o.shard_id, o.num_shards = shard_id, num_shards
     return o
 
 
@@ -349,3 +351,34 @@ def tonemap(gbuf):
 
 def save_render(gbuf, path):
     check(lib().rt_save_render(gbuf.g, gbuf.width, gbuf.height, path.encode()))
+
+
+COMM_ID_BYTES = 128
+
+
+class Comm:
+    """RCCL communicator of the C-ABI (rt_comm_*): rt_reduce_shards sums the
+    shards' fb / sq / count into `root`."""
+
+    @staticmethod
+    def unique_id():
+        buf = ctypes.create_string_buffer(COMM_ID_BYTES)
+        check(lib().rt_comm_unique_id(buf))
+        return buf.raw
+
+    def __init__(self, nranks, rank, uid):
+        L = lib()
+        L.rt_comm_create.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p)]
+        L.rt_comm_destroy.argtypes = [ctypes.c_void_p]
+        L.rt_reduce_shards.argtypes = [ctypes.c_void_p, G_Buffer, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                       ctypes.c_void_p]
+        self.h = ctypes.c_void_p()
+        check(L.rt_comm_create(nranks, rank, uid, ctypes.byref(self.h)))
+
+    def reduce(self, gbuf_g, width, height, root=0, stream=None):
+        check(lib().rt_reduce_shards(self.h, gbuf_g, width, height, root, stream))
+
+    def close(self):
+        if self.h:
+            check(lib().rt_comm_destroy(self.h))
+            self.h = ctypes.c_void_p()
