@@ -73,3 +73,51 @@ def test_two_rank_gloo_reduce_matches_emulation():
     # rank 0's slice alone is the single-stream reference for its passes
     single, _ = helpers.oracle_render(path, W, H, PASSES)
     np.testing.assert_array_equal(a[0].view(np.uint32), single[0].view(np.uint32))
+
+
+def _render_rows(path, rank, world):
+    """Row-interleaved shard (RtOptions.shard_id/num_shards): the rank's rows with
+    the single-stream seeds, adaptive on; other rows stay zero."""
+    pix = np.array([i for i in range(W * H) if (i // W) % world == rank], np.int32)
+    (fb, sq, cnt, rng), _ = helpers.oracle_render(path, W, H, PASSES, calls=2, adaptive=True, min_samples=2,
+                                                  pixels=pix)
+    return fb, sq, cnt
+
+
+def _rows_worker(rank, world, port, path, q):
+    import torch
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        fb, sq, cnt = _render_rows(path, rank, world)
+        t_fb, t_sq, t_cnt = torch.from_numpy(fb.copy()), torch.from_numpy(sq.copy()), torch.from_numpy(cnt.copy())
+        shard.reduce_to_root(dist, t_fb, t_sq, t_cnt, root=0)
+        if rank == 0:
+            q.put((t_fb.numpy().copy(), t_sq.numpy().copy(), t_cnt.numpy().copy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_row_shards_equal_single_stream():
+    """SURVEY §8e's parity-exact option: row shards reduced over gloo are the
+    one-process frame bit for bit, adaptive sampling included."""
+    import torch.multiprocessing as mp
+
+    path = helpers.scene_path("cornell")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rows_worker, args=(r, 2, port, path, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    single, _ = helpers.oracle_render(path, W, H, PASSES, calls=2, adaptive=True, min_samples=2)
+    np.testing.assert_array_equal(got[0].view(np.uint32), single[0].view(np.uint32))
+    np.testing.assert_array_equal(got[1].view(np.uint32), single[1].view(np.uint32))
+    np.testing.assert_array_equal(got[2], single[2])
