@@ -105,6 +105,10 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel", choices=["mega", "wavefront"], default="wavefront")
+    ap.add_argument("--adaptive", action="store_true", help="adaptive sampling (configs[4]); value stays nominal "
+                    "W*H*spp/s, value_actual = accumulated samples/s")
+    ap.add_argument("--min-samples", type=int, default=100)
+    ap.add_argument("--max-depth", type=int, default=0, help="0 = unbounded (reference)")
     ap.add_argument("--shard-mode", choices=["spp", "rows"], default="spp",
                     help="N>1: spp slices (north star, seeds skipped per rank) or row-interleaved shards "
                          "(bit-identical to one GPU)")
@@ -144,8 +148,9 @@ def main():
     kernel = rt.KERNEL_WAVEFRONT if args.kernel == "wavefront" else rt.KERNEL_MEGA
     wavefront = kernel == rt.KERNEL_WAVEFRONT
     shard_kw = dict(shard_id=rank, num_shards=world) if rows else {}
-    opt = rt.options(W, H, P, adaptive=False, stream=ctypes.c_void_p(stream.cuda_stream), kernel=kernel,
-                     profile=wavefront, **shard_kw)
+    render_kw = dict(adaptive=args.adaptive, min_samples=args.min_samples, max_depth=args.max_depth, kernel=kernel,
+                     **shard_kw)
+    opt = rt.options(W, H, P, stream=ctypes.c_void_p(stream.cuda_stream), profile=wavefront, **render_kw)
     profiles = []
 
     def step(i):
@@ -157,7 +162,9 @@ def main():
         step(i)
     profiles.clear()
     torch.cuda.synchronize()
+    cnt_before = gb.cnt.sum(dtype=torch.int64)  # accumulated samples before the timed steps (adaptive: actual)
     if dist:
+        dist.all_reduce(cnt_before)
         dist.barrier()
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
@@ -184,6 +191,7 @@ def main():
     kernel_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
     total_samples = (1 if rows else world) * n * P * args.steps
     value = total_samples / elapsed / 1e6
+    actual_samples = int((gb.cnt.sum(dtype=torch.int64) - cnt_before).item()) if rank == 0 else None
 
     # samples actually accumulated (every pixel, every pass: adaptive off)
     expect = (1 if rows else world) * P * (args.warmup + args.steps)
@@ -191,7 +199,7 @@ def main():
 
     # work counters on one extra (untimed) step -> algorithmic bytes per call
     counters = rt.DeviceCounters()
-    copt = rt.options(W, H, P, adaptive=False, counters=counters.p, kernel=kernel, profile=wavefront, **shard_kw)
+    copt = rt.options(W, H, P, counters=counters.p, profile=wavefront, **render_kw)
     rt.render(dscene, gb, host.camera, 1, copt)
     c = counters.read(finisher=True)
     bytes_per_call = algorithmic_bytes(c)
@@ -240,8 +248,12 @@ def main():
         "dtype": "f32",
         "data": "synthetic",
         "config": {
-            "workload": f"BASELINE configs[2]: README-like 2M-triangle synthetic room '{args.scene}', {W}x{H}, "
-                        f"{P} spp per step, adaptive off",
+            "workload": (f"BASELINE configs[2]: README-like 2M-triangle synthetic room '{args.scene}', {W}x{H}, "
+                         f"{P} spp per step, adaptive off" if not args.adaptive and args.max_depth == 0 else
+                         f"scene '{args.scene}', {W}x{H}, {P} spp per step, adaptive "
+                         f"{'on (min ' + str(args.min_samples) + ')' if args.adaptive else 'off'}, "
+                         f"max depth {args.max_depth or 'unbounded'}"),
+            "adaptive": args.adaptive, "max_depth": args.max_depth,
             "scene": args.scene, "width": W, "height": H, "spp_per_step": P,
             "triangles": info["triangles"], "kd_nodes": info["nodes"], "kd_indices": info["indices"],
             "parallelism": (f"{'row-interleaved' if rows else 'spp-sliced'} x{world} + RCCL reduce" if world > 1
@@ -261,7 +273,9 @@ def main():
             "bytes_per_sample": round(bytes_per_call / max(c["sample"], 1), 1),
         },
         "per_sample": {k: round(c[k] / max(c["sample"], 1), 3) for k in ("ray", "node", "tri", "hit", "nee")},
-        "samples_check": {"accumulated": got, "expected": expect * n},
+        "samples_check": {"accumulated": got, "expected": None if args.adaptive else expect * n},
+        "actual_samples": actual_samples,
+        "value_actual": round(actual_samples / elapsed / 1e6, 3),
         "setup_s": round(setup_s, 2),
     }
     if world == 1 and not args.no_cpu_baseline:
