@@ -242,7 +242,16 @@ enum {
      * exact plane-test passes (barycentric tests) */
     RT_CNT_CAND = 13,
     RT_CNT_PLANE = 14,
-    RT_CNT_COUNT = 16
+    /* cooperative trace, counting build only: wave-time (shader clocks,
+     * summed over waves) in descent / leaf tests / ray fetch, and the number
+     * of rounds, 64-entry plane chunks and barycentric batches */
+    RT_CNT_T_DESCEND = 16,
+    RT_CNT_T_LEAVES = 17,
+    RT_CNT_T_FETCH = 18,
+    RT_CNT_ROUNDS = 19,
+    RT_CNT_CHUNKS = 20,
+    RT_CNT_BARY = 21,
+    RT_CNT_COUNT = 32
 };
 
 #define RT_KERNEL_MEGA 0

@@ -193,6 +193,7 @@ __device__ __forceinline__ bool coop_leaves(const RtDevScene &sc, CoopRay &r, ST
     int list_n = 0;
     for (int base = 0; base < total || list_n > 0; base += 64) {
         if (base < total) {
+            if (COUNT && lane == 0) c.v[RT_CNT_CHUNKS]++;
             const int p = base + lane;
             int j = 0; // owner: the largest lane with start_j <= p
 #pragma unroll
@@ -221,6 +222,7 @@ __device__ __forceinline__ bool coop_leaves(const RtDevScene &sc, CoopRay &r, ST
         }
         // exact plane + barycentric stage over up to 64 listed candidates
         if (list_n >= 64 || (base + 64 >= total && list_n > 0)) {
+            if (COUNT && lane == 0) c.v[RT_CNT_BARY]++;
             const int take = list_n < 64 ? list_n : 64;
             const CoopCand it = list[lane < take ? lane : 0];
             const int j = (int)(it.key & 63u);
@@ -277,10 +279,18 @@ __device__ __forceinline__ bool coop_round(const RtDevScene &sc, CoopRay &r, STK
 {
     bool done = false;
     tri = -1;
+    const unsigned long long t0 = COUNT ? __builtin_amdgcn_s_memtime() : 0ull;
     if (r.live && !r.pend) done = coop_descend<COUNT>(sc, r, stk, cap, c);
     const unsigned long long pm = __ballot(r.pend), lm = __ballot(r.live);
+    const unsigned long long t1 = COUNT ? __builtin_amdgcn_s_memtime() : 0ull;
     if (pm && (__popcll(pm) >= postpone || pm == lm))
         if (coop_leaves<COUNT>(sc, r, stk, wkey, list, tri, hbx, hby, hbz, c)) done = true;
+    if (COUNT && __lane_id() == 0) {
+        const unsigned long long t2 = __builtin_amdgcn_s_memtime();
+        c.v[RT_CNT_T_DESCEND] += t1 - t0;
+        c.v[RT_CNT_T_LEAVES] += t2 - t1;
+        c.v[RT_CNT_ROUNDS]++;
+    }
     return done;
 }
 

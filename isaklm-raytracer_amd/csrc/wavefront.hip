@@ -345,6 +345,7 @@ __global__ void __launch_bounds__(WF_BLOCK, 6) wf_trace_coop(RtDevScene sc, WfSt
     bool exhausted = false;
     uint32_t e = 0;
     while (true) {
+        const unsigned long long tf = COUNT ? __builtin_amdgcn_s_memtime() : 0ull;
         // ---- refill idle lanes (dynamic ray fetch)
         const bool need = !r.live && !exhausted;
         const unsigned long long m = __ballot(need);
@@ -364,6 +365,7 @@ __global__ void __launch_bounds__(WF_BLOCK, 6) wf_trace_coop(RtDevScene sc, WfSt
                 }
             }
         }
+        if (COUNT && lane == 0) c.v[RT_CNT_T_FETCH] += __builtin_amdgcn_s_memtime() - tf;
         if (!__any(r.live)) {
             if (__all(exhausted)) break;
             continue;

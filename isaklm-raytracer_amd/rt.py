@@ -74,8 +74,9 @@ def last_profile():
 TRIANGLE_BYTES = 152
 NODE_BYTES = 20
 COUNTER_NAMES = ["node", "tri", "hit", "texel", "nee", "sample", "skip", "ray", "watchdog", "maxdepth"]
-FINISH_COUNTER_NAMES = ["finish_node", "finish_tri", "finish_ray", "cand", "plane"]
-N_COUNTERS = 16
+FINISH_COUNTER_NAMES = ["finish_node", "finish_tri", "finish_ray", "cand", "plane", "", "t_descend", "t_leaves",
+                        "t_fetch", "rounds", "chunks", "bary"]
+N_COUNTERS = 32
 
 _lib = None
 
@@ -324,7 +325,7 @@ class DeviceCounters:
         check(lib().rt_download(_ptr(a), self.p, a.nbytes))
         out = {k: int(a[i]) for i, k in enumerate(COUNTER_NAMES)}
         if finisher:
-            out.update({k: int(a[10 + i]) for i, k in enumerate(FINISH_COUNTER_NAMES)})
+            out.update({k: int(a[10 + i]) for i, k in enumerate(FINISH_COUNTER_NAMES) if k})
         return out
 
     def __del__(self):

@@ -56,7 +56,9 @@ def main():
                   "trace_ms": [round(p["trace_ms"]) for p in profs[v]],
                   "finish_ms": [round(p["finish_ms"]) for p in profs[v]],
                   "iterations": [p["iterations"] for p in profs[v]],
-                  "per_sample": {k: round(c[k] / max(c["sample"], 1), 2) for k in ("ray", "node", "tri", "cand", "plane")}}
+                  "per_sample": {k: round(c[k] / max(c["sample"], 1), 2) for k in ("ray", "node", "tri", "cand", "plane", "rounds", "chunks", "bary")},
+                  "wave_time_split": {k: round(c[k] / max(c["t_descend"] + c["t_leaves"] + c["t_fetch"], 1), 3)
+                                      for k in ("t_descend", "t_leaves", "t_fetch")}}
     print(json.dumps({"scene": scene, "passes": P, "max_depth": maxd, "variants": out}, indent=1))
 
 
