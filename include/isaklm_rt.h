@@ -251,6 +251,10 @@ enum {
     RT_CNT_ROUNDS = 19,
     RT_CNT_CHUNKS = 20,
     RT_CNT_BARY = 21,
+    /* finisher, counting build only: wide_trace calls / rounds / wave-time */
+    RT_CNT_WIDE_CALLS = 22,
+    RT_CNT_WIDE_ROUNDS = 23,
+    RT_CNT_T_WIDE = 24,
     RT_CNT_COUNT = 32
 };
 

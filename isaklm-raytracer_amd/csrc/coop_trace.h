@@ -63,6 +63,13 @@ __device__ __forceinline__ bool plane_maybe(float num, float dn, float ex)
     return !(sa < 0.0000099999f) && !(sa >= ex * 1.00001f);
 }
 
+// per-wave LDS scratch of the cooperative leaf test
+struct CoopLds {
+    unsigned long long *key; // 64: per-lane winner key (atomicMin)
+    CoopCand *list;          // WF_COOP_LIST plane-test candidates
+    int *mark;               // 64: chunk_owner marks
+};
+
 // per-lane traversal state
 struct CoopRay {
     bool live;                  // the lane holds an unfinished ray
@@ -176,32 +183,26 @@ __device__ __forceinline__ bool coop_descend(const RtDevScene &sc, CoopRay &r, S
 // tri >= 0 and the barycentrics of the hit, or tri = -1 for a miss; other
 // pending lanes pop and go back to descending.
 template <bool COUNT, typename STK>
-__device__ __forceinline__ bool coop_leaves(const RtDevScene &sc, CoopRay &r, STK &stk, unsigned long long *wkey,
-                                            CoopCand *list, int &tri, float &hbx, float &hby, float &hbz, Cnt &c)
+__device__ __forceinline__ bool coop_leaves(const RtDevScene &sc, CoopRay &r, STK &stk, const CoopLds &w, int &tri,
+                                            float &hbx, float &hby, float &hbz, Cnt &c)
 {
     const int lane = __lane_id();
+    unsigned long long *wkey = w.key;
+    CoopCand *list = w.list;
     const int leaf_count = r.pend ? r.leaf_count : 0;
-    int start = leaf_count; // inclusive scan -> exclusive
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const int v = __shfl_up(start, off);
-        if (lane >= off) start += v;
-    }
-    const int total = __shfl(start, 63);
-    start -= leaf_count;
+    const int incl = wave_incl_add(leaf_count);
+    const int total = lane63(incl);
+    const int start = incl - leaf_count; // exclusive prefix: lane j's pairs are [start, start + leaf_count)
+    const uint32_t kbase = r.leaf_begin - (uint32_t)start; // entry of pair p = kbase_j + p
     wkey[lane] = ~0ull;
-    int list_n = 0;
+    int list_n = 0, carry = -1;
     for (int base = 0; base < total || list_n > 0; base += 64) {
         if (base < total) {
             if (COUNT && lane == 0) c.v[RT_CNT_CHUNKS]++;
             const int p = base + lane;
-            int j = 0; // owner: the largest lane with start_j <= p
-#pragma unroll
-            for (int step = 32; step >= 1; step >>= 1) {
-                const int sv = __shfl(start, j + step);
-                if (sv <= p) j += step;
-            }
-            const uint32_t k = (uint32_t)__shfl((int)r.leaf_begin, j) + (uint32_t)(p - __shfl(start, j));
+            const int j = chunk_owner(w.mark, start, leaf_count, base, carry); // owner lane of pair p
+            carry = lane63(j);
+            const uint32_t k = (uint32_t)__shfl((int)kbase, j) + (uint32_t)p;
             const Vec3D oo = rt_v3(__shfl(r.o.x, j), __shfl(r.o.y, j), __shfl(r.o.z, j));
             const Vec3D dd = rt_v3(__shfl(r.d.x, j), __shfl(r.d.y, j), __shfl(r.d.z, j));
             const float ex = __shfl(r.exit_, j);
@@ -273,9 +274,8 @@ __device__ __forceinline__ bool coop_leaves(const RtDevScene &sc, CoopRay &r, ST
 // lane is still descending).  Call with all 64 lanes active; returns true for
 // a lane whose ray finished in this round (tri / barycentrics as above).
 template <bool COUNT, typename STK>
-__device__ __forceinline__ bool coop_round(const RtDevScene &sc, CoopRay &r, STK &stk, unsigned long long *wkey,
-                                           CoopCand *list, int cap, int postpone, int &tri, float &hbx, float &hby,
-                                           float &hbz, Cnt &c)
+__device__ __forceinline__ bool coop_round(const RtDevScene &sc, CoopRay &r, STK &stk, const CoopLds &w, int cap,
+                                           int postpone, int &tri, float &hbx, float &hby, float &hbz, Cnt &c)
 {
     bool done = false;
     tri = -1;
@@ -284,7 +284,7 @@ __device__ __forceinline__ bool coop_round(const RtDevScene &sc, CoopRay &r, STK
     const unsigned long long pm = __ballot(r.pend), lm = __ballot(r.live);
     const unsigned long long t1 = COUNT ? __builtin_amdgcn_s_memtime() : 0ull;
     if (pm && (__popcll(pm) >= postpone || pm == lm))
-        if (coop_leaves<COUNT>(sc, r, stk, wkey, list, tri, hbx, hby, hbz, c)) done = true;
+        if (coop_leaves<COUNT>(sc, r, stk, w, tri, hbx, hby, hbz, c)) done = true;
     if (COUNT && __lane_id() == 0) {
         const unsigned long long t2 = __builtin_amdgcn_s_memtime();
         c.v[RT_CNT_T_DESCEND] += t1 - t0;
@@ -340,16 +340,21 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v)
 // Counters are added by `counter_lane` only.
 template <bool COUNT>
 __device__ __forceinline__ void wide_trace(const RtDevScene &sc, Vec3D o, Vec3D d, float entry, float exit_,
-                                           WideItem *F, unsigned long long *wkey, CoopCand *list, bool counter_lane,
-                                           int &tri, float &hbx, float &hby, float &hbz, Cnt &c)
+                                           WideItem *F, const CoopLds &w, bool counter_lane, int &tri, float &hbx,
+                                           float &hby, float &hbz, Cnt &c)
 {
+    unsigned long long *wkey = w.key;
+    CoopCand *list = w.list;
     const int lane = __lane_id();
     const float ox = o.x, oy = o.y, oz = o.z, dx = d.x, dy = d.y, dz = d.z;
     const float yx = rt_recip_guard(dx), yy = rt_recip_guard(dy), yz = rt_recip_guard(dz);
     if (lane == 0) F[0] = WideItem{0u, entry, exit_, 0u};
     int n = 1;
     tri = -1;
+    const unsigned long long t0 = COUNT ? __builtin_amdgcn_s_memtime() : 0ull;
+    if (COUNT && counter_lane) c.v[RT_CNT_WIDE_CALLS]++;
     while (n > 0) {
+        if (COUNT && counter_lane) c.v[RT_CNT_WIDE_ROUNDS]++;
         int k = WIDE_CAP - WIDE_RESERVE - n; // expansions add at most one item each
         k = k < 1 ? 1 : (k > 64 ? 64 : k);
         k = k < n ? k : n;
@@ -365,30 +370,21 @@ __device__ __forceinline__ void wide_trace(const RtDevScene &sc, Vec3D o, Vec3D 
         const int L = ~lmask ? __ffsll((long long)~lmask) - 1 : 64; // leading run of leaves
         // consume leaves 0..Le-1: whole leaves within the entry budget (at least one)
         const int cnt_all = (lane < L) ? (int)(nd.y >> 2) : 0;
-        int incl = cnt_all;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const int v = __shfl_up(incl, off);
-            if (lane >= off) incl += v;
-        }
+        const int incl = wave_incl_add(cnt_all);
         const int Le = __popcll(__ballot(lane < L && (lane == 0 || incl <= WIDE_LEAF_BUDGET)));
         if (Le > 0) {
             const int cnt = lane < Le ? cnt_all : 0;
             const int start = incl - cnt_all; // exclusive prefix (lanes < Le)
-            const int total = __shfl(incl, Le - 1);
+            const int total = __builtin_amdgcn_readlane(incl, Le - 1);
+            const uint32_t kbase = nd.x - (uint32_t)start; // leaf_begin - start: entry of pair p = kbase_j + p
             if (lane == 0) wkey[0] = ~0ull;
-            int list_n = 0;
+            int list_n = 0, carry = -1;
             for (int base = 0; base < total || list_n > 0; base += 64) {
                 if (base < total) {
                     const int p = base + lane;
-                    int j = 0; // owner leaf: the largest lane with start_j <= p (lanes >= Le have start >= total)
-#pragma unroll
-                    for (int step = 32; step >= 1; step >>= 1) {
-                        const int sv = __shfl(start, j + step);
-                        if (sv <= p) j += step;
-                    }
-                    const uint32_t kk = nd.x; // leaf_begin of this lane
-                    const uint32_t e = (uint32_t)__shfl((int)kk, j) + (uint32_t)(p - __shfl(start, j));
+                    const int j = chunk_owner(w.mark, start, cnt, base, carry); // owner leaf lane of pair p
+                    carry = lane63(j);
+                    const uint32_t e = (uint32_t)__shfl((int)kbase, j) + (uint32_t)p;
                     const float ex = __shfl(it.exit_, j);
                     bool cand = false;
                     float num = 0.0f, dn = 0.0f;
@@ -438,7 +434,10 @@ __device__ __forceinline__ void wide_trace(const RtDevScene &sc, Vec3D o, Vec3D 
             if (key != ~0ull) {
                 const uint32_t e = (uint32_t)(key & ((1ull << 26) - 1ull));
                 coop_bary(sc, e, o, d, __uint_as_float((uint32_t)(key >> 26)), hbx, hby, hbz, tri);
-                if (COUNT && counter_lane) c.v[RT_CNT_HIT]++;
+                if (COUNT && counter_lane) {
+                    c.v[RT_CNT_HIT]++;
+                    c.v[RT_CNT_T_WIDE] += __builtin_amdgcn_s_memtime() - t0;
+                }
                 return;
             }
         }
@@ -470,19 +469,15 @@ __device__ __forceinline__ void wide_trace(const RtDevScene &sc, Vec3D o, Vec3D 
                 }
             }
         }
-        int pos = c_out;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const int v = __shfl_up(pos, off);
-            if (lane >= off) pos += v;
-        }
-        const int M = __shfl(pos, 63);
+        int pos = wave_incl_add(c_out);
+        const int M = lane63(pos);
         pos -= c_out;
         const int base = n - k;
         if (c_out >= 1) F[base + M - 1 - pos] = a;
         if (c_out == 2) F[base + M - 2 - pos] = b;
         n = base + M;
     }
+    if (COUNT && counter_lane) c.v[RT_CNT_T_WIDE] += __builtin_amdgcn_s_memtime() - t0;
 }
 
 } // namespace rtk

@@ -465,6 +465,48 @@ __device__ __forceinline__ void flush_finish_counters(const Cnt &c, unsigned lon
 // per-wave [start, end] s_memrealtime stamps (100 MHz) into a debug buffer
 __device__ __forceinline__ unsigned long long realtime() { return __builtin_amdgcn_s_memrealtime(); }
 
+// Wave64 inclusive scans on DPP (CDNA row_shr 1/2/4/8 inside 16-lane rows,
+// then row_bcast:15 into rows 1,3 and row_bcast:31 into rows 2,3): six
+// dependent VALU ops instead of a chain of six ds_bpermute round trips.
+// Lanes whose DPP source is outside the row (or whose row is masked off)
+// read the identity through `old`.
+__device__ __forceinline__ int wave_incl_add(int v)
+{
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false); // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false); // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false); // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false); // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false); // row_bcast:15
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false); // row_bcast:31
+    return v;
+}
+__device__ __forceinline__ int wave_incl_max(int v) // identity -1
+{
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x111, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x112, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x114, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x118, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x142, 0xa, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x143, 0xc, 0xf, false));
+    return v;
+}
+__device__ __forceinline__ int lane63(int v) { return __builtin_amdgcn_readlane(v, 63); }
+
+// Owner lane of every position of a 64-wide chunk [base, base + 64) of a
+// segmented range (lane j owns [start_j, start_j + count_j)): lanes whose
+// segment starts inside the chunk mark their start in `mark` (64 ints of
+// LDS per wave), a max-scan spreads the marks, and `carry` (the owner of
+// position base - 1) covers segments that began in an earlier chunk.
+__device__ __forceinline__ int chunk_owner(int *mark_, int start, int count, int base, int carry)
+{
+    volatile int *mark = mark_; // cross-lane: keep the three LDS accesses in program order
+    const int lane = __lane_id();
+    mark[lane] = -1;
+    if (count > 0 && start >= base && start < base + 64) mark[start - base] = lane;
+    const int m = wave_incl_max(mark[lane]);
+    return max(m, carry);
+}
+
 // block -> 16x16 tile, remapped so each XCD (blocks b, b+8, ...) owns one
 // contiguous band of tiles; bijective for any block count
 __device__ __forceinline__ int xcd_tile(int b, int nb)

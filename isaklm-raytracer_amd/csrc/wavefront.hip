@@ -327,6 +327,7 @@ __global__ void __launch_bounds__(WF_BLOCK, 6) wf_trace_coop(RtDevScene sc, WfSt
     __shared__ float s_entry[WF_LDS_STACK * WF_BLOCK];
     __shared__ unsigned long long s_key[WF_BLOCK];
     __shared__ CoopCand s_list[(WF_BLOCK / 64) * WF_COOP_LIST];
+    __shared__ int s_mark[WF_BLOCK];
     const int tid = threadIdx.x;
     const int gtid = blockIdx.x * WF_BLOCK + tid;
     const int lane = __lane_id();
@@ -334,6 +335,7 @@ __global__ void __launch_bounds__(WF_BLOCK, 6) wf_trace_coop(RtDevScene sc, WfSt
     Stack<WF_LDS_STACK> stk{s_node + tid, s_entry + tid, WF_BLOCK, st.spill + gtid, st.spill_threads};
     unsigned long long *wkey = s_key + wave * 64;
     CoopCand *list = s_list + wave * WF_COOP_LIST;
+    const CoopLds w{wkey, list, s_mark + wave * 64};
     Cnt c;
     if (COUNT) c.zero();
     const uint32_t n = st.counts[q];
@@ -372,7 +374,7 @@ __global__ void __launch_bounds__(WF_BLOCK, 6) wf_trace_coop(RtDevScene sc, WfSt
         }
         int tri = -1;
         float bx = 0.0f, by = 0.0f, bz = 0.0f;
-        if (coop_round<COUNT>(sc, r, stk, wkey, list, cap, postpone, tri, bx, by, bz, c))
+        if (coop_round<COUNT>(sc, r, stk, w, cap, postpone, tri, bx, by, bz, c))
             *reinterpret_cast<float4 *>(st.hits + e) = make_float4(__int_as_float(tri), bx, by, bz);
     }
     if (COUNT) flush_counters(c, counters);
@@ -596,6 +598,7 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_finish_coop(RtDevScene sc, RtDevF
     __shared__ float s_entry[WF_LDS_STACK * WF_BLOCK];
     __shared__ unsigned long long s_key[WF_BLOCK];
     __shared__ CoopCand s_list[(WF_BLOCK / 64) * WF_COOP_LIST];
+    __shared__ int s_mark[WF_BLOCK];
     __shared__ WideItem s_wide[(WF_BLOCK / 64) * WIDE_CAP];
     const int tid = threadIdx.x;
     const int gtid = blockIdx.x * WF_BLOCK + tid;
@@ -604,6 +607,7 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_finish_coop(RtDevScene sc, RtDevF
     Stack<WF_LDS_STACK> stk{s_node + tid, s_entry + tid, WF_BLOCK, st.spill + gtid, st.spill_threads};
     unsigned long long *wkey = s_key + wave * 64;
     CoopCand *list = s_list + wave * WF_COOP_LIST;
+    const CoopLds w{wkey, list, s_mark + wave * 64};
     Cnt c;
     if (COUNT) c.zero();
     const uint32_t n = st.counts[q];
@@ -673,7 +677,7 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_finish_coop(RtDevScene sc, RtDevF
                 int t;
                 float x, y, z;
                 wide_trace<COUNT>(sc, o, d, __shfl(r.entry, owner), __shfl(r.exit_, owner), s_wide + wave * WIDE_CAP,
-                                  wkey, list, lane == owner, t, x, y, z, c);
+                                  w, lane == owner, t, x, y, z, c);
                 if (lane == owner) {
                     hit = t;
                     bx = x;
@@ -685,7 +689,7 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_finish_coop(RtDevScene sc, RtDevF
                 continue;
             }
         }
-        if (coop_round<COUNT>(sc, r, stk, wkey, list, cap, postpone, hit, bx, by, bz, c)) pending = true;
+        if (coop_round<COUNT>(sc, r, stk, w, cap, postpone, hit, bx, by, bz, c)) pending = true;
     }
     if (COUNT) {
         flush_counters(c, fr.counters);

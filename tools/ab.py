@@ -1,4 +1,6 @@
 """A/B kernel variants in ONE process, interleaved rounds (guide §5.4 rule 24).
+Round r renders the same samples (seeds = mt19937 outputs [r*W*H, (r+1)*W*H))
+for every variant, so the work is identical and only the timing differs.
 
 usage: python tools/ab.py SCENE PASSES MAX_DEPTH ROUNDS VARIANT[,VARIANT...]
   VARIANT = KERNEL[:WF_TAIL[:WF_FINISH_WAVES[:DESCENT_CAP[:POSTPONE[:WIDE]]]]]; KERNEL 0 mega, 1 wavefront
@@ -32,10 +34,14 @@ def main():
     W, H = int(os.environ.get("AB_W", 1920)), int(os.environ.get("AB_H", 1080))
     run = helpers.GpuRun(scene)
     g = rt.GBuffer(W, H)
+    n = W * H
+    zf3, zf, zi = np.zeros((n, 3), np.float32), np.zeros(n, np.float32), np.zeros(n, np.int32)
     times = {v: [] for v in variants}
     profs = {v: [] for v in variants}
     for r in range(rounds):
+        seeds = rt.seeds(n, r * n)  # every variant renders the same samples in round r
         for v in variants:
+            g.upload(zf3, zf, zi, seeds)
             opt = opts(v, profile=True)
             rt.check(rt.lib().rt_synchronize())
             t = time.perf_counter()
@@ -46,6 +52,7 @@ def main():
     out = {}
     for v in variants:
         cnt = rt.DeviceCounters()
+        g.upload(zf3, zf, zi, rt.seeds(n, 0))
         opt = opts(v, counters=cnt.p)
         rt.render(run.dev, g, run.camera, 0, opt)
         c = cnt.read(finisher=True)
@@ -57,6 +64,8 @@ def main():
                   "finish_ms": [round(p["finish_ms"]) for p in profs[v]],
                   "iterations": [p["iterations"] for p in profs[v]],
                   "per_sample": {k: round(c[k] / max(c["sample"], 1), 2) for k in ("ray", "node", "tri", "cand", "plane", "rounds", "chunks", "bary")},
+                  "wide": {"calls": c["wide_calls"], "rounds_per_call": round(c["wide_rounds"] / max(c["wide_calls"], 1), 2),
+                           "clk_per_call": round(c["t_wide"] / max(c["wide_calls"], 1))},
                   "wave_time_split": {k: round(c[k] / max(c["t_descend"] + c["t_leaves"] + c["t_fetch"], 1), 3)
                                       for k in ("t_descend", "t_leaves", "t_fetch")}}
     print(json.dumps({"scene": scene, "passes": P, "max_depth": maxd, "variants": out}, indent=1))
