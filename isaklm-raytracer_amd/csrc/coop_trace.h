@@ -378,50 +378,53 @@ __device__ __forceinline__ void wide_trace(const RtDevScene &sc, Vec3D o, Vec3D 
             const int total = __builtin_amdgcn_readlane(incl, Le - 1);
             const uint32_t kbase = nd.x - (uint32_t)start; // leaf_begin - start: entry of pair p = kbase_j + p
             if (lane == 0) wkey[0] = ~0ull;
-            int list_n = 0, carry = -1;
-            for (int base = 0; base < total || list_n > 0; base += 64) {
-                if (base < total) {
-                    const int p = base + lane;
-                    const int j = chunk_owner(w.mark, start, cnt, base, carry); // owner leaf lane of pair p
-                    carry = lane63(j);
-                    const uint32_t e = (uint32_t)__shfl((int)kbase, j) + (uint32_t)p;
-                    const float ex = __shfl(it.exit_, j);
-                    bool cand = false;
-                    float num = 0.0f, dn = 0.0f;
-                    if (p < total) {
-                        const RtF4 A = ldf4(sc.isect_a + e);
-                        dn = dx * A.x + dy * A.y + dz * A.z;
-                        num = A.w - (ox * A.x + oy * A.y + oz * A.z);
-                        cand = plane_maybe(num, dn, ex);
+            // one ray: bandwidth is free, latency is not — each pair loads its
+            // plane and its barycentric record together (one memory round trip
+            // per 64 pairs), and the current winner parks its barycentrics in
+            // LDS so the result needs no reload
+            volatile float *best = reinterpret_cast<volatile float *>(list); // {bx, by, bz, tri bits}
+            int carry = -1;
+            for (int base = 0; base < total; base += 64) {
+                const int p = base + lane;
+                const int j = chunk_owner(w.mark, start, cnt, base, carry); // owner leaf lane of pair p
+                carry = lane63(j);
+                const uint32_t e = (uint32_t)__shfl((int)kbase, j) + (uint32_t)p;
+                const float ex = __shfl(it.exit_, j);
+                unsigned long long mine = ~0ull;
+                float cx = 0.0f, cy = 0.0f, cz = 0.0f;
+                int t = -1;
+                if (p < total) {
+                    const RtF4 A = ldf4(sc.isect_a + e);
+                    const RtIsectBary *rec = sc.isect_bary + e;
+                    const RtF4 B = ldf4(&rec->b), C = ldf4(&rec->c), D = ldf4(&rec->d);
+                    const uint2 R = *reinterpret_cast<const uint2 *>(&rec->rd);
+                    const float dn = dx * A.x + dy * A.y + dz * A.z;
+                    const float s = (A.w - (ox * A.x + oy * A.y + oz * A.z)) / dn; // intersect_triangle (:95-98)
+                    if (dn != 0 && s >= 0.00001f && s < ex) {
+                        const float px = ox + dx * s, py = oy + dy * s, pz = oz + dz * s; // = coop_bary
+                        const float v2x = px - B.x, v2y = py - B.y, v2z = pz - B.z;
+                        const float d20 = v2x * C.x + v2y * C.y + v2z * C.z;
+                        const float d21 = v2x * D.x + v2y * D.y + v2z * D.z;
+                        const float rd = __uint_as_float(R.x);
+                        cy = (D.w * d20 - C.w * d21) * rd;
+                        cz = (B.w * d21 - C.w * d20) * rd;
+                        cx = 1.0f - cy - cz;
+                        t = (int)R.y;
+                        if (cx >= 0.0f && cx <= 1.0f && cy >= 0.0f && cy <= 1.0f && cz >= 0.0f && cz <= 1.0f) {
+                            mine = ((unsigned long long)j << 58) | ((unsigned long long)__float_as_uint(s) << 26) |
+                                   (unsigned long long)e;
+                            atomicMin(wkey, mine);
+                        }
                     }
-                    const unsigned long long pm = __ballot(cand);
-                    if (cand)
-                        list[list_n + __popcll(pm & ((1ull << lane) - 1ull))] =
-                            CoopCand{(e << 6) | (uint32_t)j, __float_as_uint(num), __float_as_uint(dn)};
-                    list_n += __popcll(pm);
                 }
-                if (list_n >= 64 || (base + 64 >= total && list_n > 0)) {
-                    const int take = list_n < 64 ? list_n : 64;
-                    const CoopCand itm = list[lane < take ? lane : 0];
-                    const float ex = __shfl(it.exit_, (int)(itm.key & 63u));
-                    if (lane < take) {
-                        const float dn = __uint_as_float(itm.dn);
-                        const float s = __uint_as_float(itm.num) / dn;
-                        float cx, cy, cz;
-                        int t;
-                        if (dn != 0 && s >= 0.00001f && s < ex && coop_bary(sc, itm.key >> 6, o, d, s, cx, cy, cz, t))
-                            atomicMin(wkey, ((unsigned long long)(itm.key & 63u) << 58) |
-                                                ((unsigned long long)__float_as_uint(s) << 26) |
-                                                (unsigned long long)(itm.key >> 6));
-                    }
-                    const int rest = list_n - take;
-                    CoopCand mv = CoopCand{0u, 0u, 0u};
-                    if (lane < rest) mv = list[take + lane];
-                    if (lane < rest) list[lane] = mv;
-                    list_n = rest;
+                if (mine != ~0ull && *reinterpret_cast<volatile unsigned long long *>(wkey) == mine) {
+                    best[0] = cx; // keys are unique: one writer, and a later smaller key overwrites
+                    best[1] = cy;
+                    best[2] = cz;
+                    best[3] = __int_as_float(t);
                 }
             }
-            const unsigned long long key = wkey[0];
+            const unsigned long long key = *reinterpret_cast<volatile unsigned long long *>(wkey);
             const int jstar = key != ~0ull ? (int)(key >> 58) : Le - 1;
             if (COUNT) { // leaves 0..jstar are the sequential traversal's next visits
                 const unsigned long long nv = wave_sum(lane <= jstar ? it.acc + 1ull : 0ull);
@@ -432,8 +435,10 @@ __device__ __forceinline__ void wide_trace(const RtDevScene &sc, Vec3D o, Vec3D 
                 }
             }
             if (key != ~0ull) {
-                const uint32_t e = (uint32_t)(key & ((1ull << 26) - 1ull));
-                coop_bary(sc, e, o, d, __uint_as_float((uint32_t)(key >> 26)), hbx, hby, hbz, tri);
+                hbx = best[0];
+                hby = best[1];
+                hbz = best[2];
+                tri = __float_as_int(best[3]);
                 if (COUNT && counter_lane) {
                     c.v[RT_CNT_HIT]++;
                     c.v[RT_CNT_T_WIDE] += __builtin_amdgcn_s_memtime() - t0;
