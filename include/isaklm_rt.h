@@ -255,6 +255,9 @@ enum {
     RT_CNT_WIDE_CALLS = 22,
     RT_CNT_WIDE_ROUNDS = 23,
     RT_CNT_T_WIDE = 24,
+    RT_CNT_T_WIDE_LOAD = 25,   /* wide_trace phases: frontier + node load, */
+    RT_CNT_T_WIDE_LEAF = 26,   /* leaf batch, */
+    RT_CNT_T_WIDE_EXPAND = 27, /* expansion */
     RT_CNT_COUNT = 32
 };
 

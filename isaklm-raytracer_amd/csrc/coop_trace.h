@@ -355,6 +355,7 @@ __device__ __forceinline__ void wide_trace(const RtDevScene &sc, Vec3D o, Vec3D 
     if (COUNT && counter_lane) c.v[RT_CNT_WIDE_CALLS]++;
     while (n > 0) {
         if (COUNT && counter_lane) c.v[RT_CNT_WIDE_ROUNDS]++;
+        const unsigned long long tr0 = COUNT ? __builtin_amdgcn_s_memtime() : 0ull;
         int k = WIDE_CAP - WIDE_RESERVE - n; // expansions add at most one item each
         k = k < 1 ? 1 : (k > 64 ? 64 : k);
         k = k < n ? k : n;
@@ -367,6 +368,12 @@ __device__ __forceinline__ void wide_trace(const RtDevScene &sc, Vec3D o, Vec3D 
         }
         const bool leaf = have && (nd.y & 3u) == RT_LEAF_TAG;
         const unsigned long long lmask = __ballot(leaf);
+        unsigned long long tph = 0;
+        if (COUNT) {
+            __builtin_amdgcn_s_waitcnt(0);
+            tph = __builtin_amdgcn_s_memtime();
+            if (counter_lane) c.v[RT_CNT_T_WIDE_LOAD] += tph - tr0;
+        }
         const int L = ~lmask ? __ffsll((long long)~lmask) - 1 : 64; // leading run of leaves
         // consume leaves 0..Le-1: whole leaves within the entry budget (at least one)
         const int cnt_all = (lane < L) ? (int)(nd.y >> 2) : 0;
@@ -446,6 +453,11 @@ __device__ __forceinline__ void wide_trace(const RtDevScene &sc, Vec3D o, Vec3D 
                 return;
             }
         }
+        unsigned long long tex = 0;
+        if (COUNT) {
+            tex = __builtin_amdgcn_s_memtime();
+            if (counter_lane) c.v[RT_CNT_T_WIDE_LEAF] += tex - tph;
+        }
         // expand the rest of the k items (leaves behind an inner item stay as they are)
         int c_out = 0;
         WideItem a = it, b = it;
@@ -481,6 +493,7 @@ __device__ __forceinline__ void wide_trace(const RtDevScene &sc, Vec3D o, Vec3D 
         if (c_out >= 1) F[base + M - 1 - pos] = a;
         if (c_out == 2) F[base + M - 2 - pos] = b;
         n = base + M;
+        if (COUNT && counter_lane) c.v[RT_CNT_T_WIDE_EXPAND] += __builtin_amdgcn_s_memtime() - tex;
     }
     if (COUNT && counter_lane) c.v[RT_CNT_T_WIDE] += __builtin_amdgcn_s_memtime() - t0;
 }

@@ -75,7 +75,7 @@ TRIANGLE_BYTES = 152
 NODE_BYTES = 20
 COUNTER_NAMES = ["node", "tri", "hit", "texel", "nee", "sample", "skip", "ray", "watchdog", "maxdepth"]
 FINISH_COUNTER_NAMES = ["finish_node", "finish_tri", "finish_ray", "cand", "plane", "", "t_descend", "t_leaves",
-                        "t_fetch", "rounds", "chunks", "bary", "wide_calls", "wide_rounds", "t_wide"]
+                        "t_fetch", "rounds", "chunks", "bary", "wide_calls", "wide_rounds", "t_wide", "t_wide_load", "t_wide_leaf", "t_wide_expand"]
 N_COUNTERS = 32
 
 _lib = None

@@ -65,7 +65,9 @@ def main():
                   "iterations": [p["iterations"] for p in profs[v]],
                   "per_sample": {k: round(c[k] / max(c["sample"], 1), 2) for k in ("ray", "node", "tri", "cand", "plane", "rounds", "chunks", "bary")},
                   "wide": {"calls": c["wide_calls"], "rounds_per_call": round(c["wide_rounds"] / max(c["wide_calls"], 1), 2),
-                           "clk_per_call": round(c["t_wide"] / max(c["wide_calls"], 1))},
+                           "clk_per_call": round(c["t_wide"] / max(c["wide_calls"], 1)),
+                           "clk_per_round": {k: round(c[k] / max(c["wide_rounds"], 1))
+                                             for k in ("t_wide_load", "t_wide_leaf", "t_wide_expand")}},
                   "wave_time_split": {k: round(c[k] / max(c["t_descend"] + c["t_leaves"] + c["t_fetch"], 1), 3)
                                       for k in ("t_descend", "t_leaves", "t_fetch")}}
     print(json.dumps({"scene": scene, "passes": P, "max_depth": maxd, "variants": out}, indent=1))
