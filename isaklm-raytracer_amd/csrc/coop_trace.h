@@ -116,8 +116,7 @@ template <typename STK>
 __device__ __forceinline__ void coop_pop(CoopRay &r, STK &stk)
 {
     --r.sp;
-    r.node = stk.node_at(r.sp);
-    r.entry = stk.entry_at(r.sp);
+    stk.get(r.sp, r.node, r.entry);
     r.exit_ = r.sp > 0 ? stk.entry_at(r.sp - 1) : r.root_exit;
 }
 
@@ -194,7 +193,8 @@ __device__ __forceinline__ bool coop_leaves(const RtDevScene &sc, CoopRay &r, ST
     const int total = lane63(incl);
     const int start = incl - leaf_count; // exclusive prefix: lane j's pairs are [start, start + leaf_count)
     const uint32_t kbase = r.leaf_begin - (uint32_t)start; // entry of pair p = kbase_j + p
-    wkey[lane] = ~0ull;
+    lds_vu64 *vkey = (lds_vu64 *)wkey; // set and read per lane, lowered by other lanes: see chunk_owner
+    vkey[lane] = ~0ull;
     int list_n = 0, carry = -1;
     for (int base = 0; base < total || list_n > 0; base += 64) {
         if (base < total) {
@@ -248,7 +248,7 @@ __device__ __forceinline__ bool coop_leaves(const RtDevScene &sc, CoopRay &r, ST
         }
     }
     // ---- per-lane result: winner, or pop, or miss
-    const unsigned long long key = wkey[lane];
+    const unsigned long long key = vkey[lane];
     bool done = false;
     if (r.pend) {
         r.pend = false;
@@ -389,7 +389,8 @@ __device__ __forceinline__ void wide_trace(const RtDevScene &sc, Vec3D o, Vec3D 
             // plane and its barycentric record together (one memory round trip
             // per 64 pairs), and the current winner parks its barycentrics in
             // LDS so the result needs no reload
-            volatile float *best = reinterpret_cast<volatile float *>(list); // {bx, by, bz, tri bits}
+            lds_vfloat *best = (lds_vfloat *)list;      // {bx, by, bz, tri bits}: cross-lane, see chunk_owner
+            lds_vu64 *vkey = (lds_vu64 *)wkey;
             int carry = -1;
             for (int base = 0; base < total; base += 64) {
                 const int p = base + lane;
@@ -424,14 +425,14 @@ __device__ __forceinline__ void wide_trace(const RtDevScene &sc, Vec3D o, Vec3D 
                         }
                     }
                 }
-                if (mine != ~0ull && *reinterpret_cast<volatile unsigned long long *>(wkey) == mine) {
+                if (mine != ~0ull && vkey[0] == mine) {
                     best[0] = cx; // keys are unique: one writer, and a later smaller key overwrites
                     best[1] = cy;
                     best[2] = cz;
                     best[3] = __int_as_float(t);
                 }
             }
-            const unsigned long long key = *reinterpret_cast<volatile unsigned long long *>(wkey);
+            const unsigned long long key = vkey[0];
             const int jstar = key != ~0ull ? (int)(key >> 58) : Le - 1;
             if (COUNT) { // leaves 0..jstar are the sequential traversal's next visits
                 const unsigned long long nv = wave_sum(lane <= jstar ? it.acc + 1ull : 0ull);

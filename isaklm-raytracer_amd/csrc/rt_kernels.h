@@ -85,13 +85,34 @@ struct Stack {
             spill[(size_t)(k - LDS_DEPTH) * spill_stride] = make_uint2(node, __float_as_uint(t));
         }
     }
+    // (The spill read is a relaxed atomic load: otherwise the compiler merges
+    // the two branches into one generic `flat` load through a selected
+    // pointer, which makes every LDS pop pay the flat path.)
+    __device__ __forceinline__ void get(int k, uint32_t &node, float &entry) const
+    {
+        if (k < LDS_DEPTH) {
+            node = lds_node[k * stride];
+            entry = lds_entry[k * stride];
+        } else {
+            unsigned long long *p = reinterpret_cast<unsigned long long *>(spill + (size_t)(k - LDS_DEPTH) * spill_stride);
+            const unsigned long long v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+            node = (uint32_t)v;
+            entry = __uint_as_float((uint32_t)(v >> 32));
+        }
+    }
     __device__ __forceinline__ uint32_t node_at(int k) const
     {
-        return k < LDS_DEPTH ? lds_node[k * stride] : spill[(size_t)(k - LDS_DEPTH) * spill_stride].x;
+        uint32_t n;
+        float e;
+        get(k, n, e);
+        return n;
     }
     __device__ __forceinline__ float entry_at(int k) const
     {
-        return k < LDS_DEPTH ? lds_entry[k * stride] : __uint_as_float(spill[(size_t)(k - LDS_DEPTH) * spill_stride].y);
+        uint32_t n;
+        float e;
+        get(k, n, e);
+        return e;
     }
 };
 
@@ -497,9 +518,17 @@ __device__ __forceinline__ int lane63(int v) { return __builtin_amdgcn_readlane(
 // segment starts inside the chunk mark their start in `mark` (64 ints of
 // LDS per wave), a max-scan spreads the marks, and `carry` (the owner of
 // position base - 1) covers segments that began in an earlier chunk.
+// Cross-lane LDS traffic must not be optimised as single-thread code (the
+// compiler would forward a lane's own `mark[lane] = -1` to its reload on the
+// path where that lane wrote no mark, missing the other lanes' marks), so it
+// goes through volatile pointers — in the LDS address space, since a volatile
+// generic pointer becomes a system-coherent `flat` access.
+typedef __attribute__((address_space(3))) volatile int lds_vint;
+typedef __attribute__((address_space(3))) volatile float lds_vfloat;
+typedef __attribute__((address_space(3))) volatile unsigned long long lds_vu64;
 __device__ __forceinline__ int chunk_owner(int *mark_, int start, int count, int base, int carry)
 {
-    volatile int *mark = mark_; // cross-lane: keep the three LDS accesses in program order
+    lds_vint *mark = (lds_vint *)mark_;
     const int lane = __lane_id();
     mark[lane] = -1;
     if (count > 0 && start >= base && start < base + 64) mark[start - base] = lane;
