@@ -240,9 +240,12 @@ __device__ __forceinline__ Vec3D sample_texture(const RtDevMaterial &m, Vec3D bl
     float u = rt_mod(uv.x, 1.0f);
     float v = rt_mod(uv.y, 1.0f);
     int pn = (int)((float)((int)(v * (float)m.tex_height) * m.tex_width) + (u * (float)m.tex_width));
-    RtUChar4 c = m.tex[pn];
-    return rt_v3(c.x / (float)RT_MAX_COLOR_CHANNEL, c.y / (float)RT_MAX_COLOR_CHANNEL,
-                 c.z / (float)RT_MAX_COLOR_CHANNEL) *
+    // one 4-B global load (the texel array is device memory; a generic uchar4
+    // read becomes 2 flat loads)
+    typedef __attribute__((address_space(1))) const uint32_t gu32;
+    const uint32_t c = *((gu32 *)(m.tex) + pn);
+    return rt_v3((float)(c & 0xffu) / (float)RT_MAX_COLOR_CHANNEL, (float)((c >> 8) & 0xffu) / (float)RT_MAX_COLOR_CHANNEL,
+                 (float)((c >> 16) & 0xffu) / (float)RT_MAX_COLOR_CHANNEL) *
            blend;
 }
 
