@@ -79,3 +79,25 @@ def test_argument_errors_are_reported():
 
 def test_version_string():
     assert b"gfx950" in rt.lib().rt_version()
+
+
+def test_ctypes_binding_matches_header_layout(tmp_path):
+    """rt.py's RtOptions / RtProfile must mirror include/isaklm_rt.h field by
+    field: compile a probe with gcc and compare every offset and the size."""
+    structs = {"RtOptions": rt.RtOptions, "RtProfile": rt.RtProfile}
+    lines = ['#include <stddef.h>', '#include <stdio.h>', '#include "isaklm_rt.h"', "int main(void){"]
+    for cname, cls in structs.items():
+        lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')
+        for fname, _ in cls._fields_:
+            lines.append(f'printf("{cname} {fname} %zu\\n", offsetof({cname}, {fname}));')
+    lines.append("return 0;}")
+    src = tmp_path / "probe.c"
+    src.write_text("\n".join(lines) + "\n")
+    exe = tmp_path / "probe"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+    for line in filter(None, out):
+        cname, fname, val = line.split()
+        cls = structs[cname]
+        want = ctypes.sizeof(cls) if fname == "size" else getattr(cls, fname).offset
+        assert int(val) == want, (cname, fname, int(val), want)
