@@ -5,6 +5,7 @@ kernels and the C-ABI by hipcc --offload-arch=gfx950; everything with
 -ffp-contract=off so host-precomputed constants and
 GPU arithmetic round identically.  Rebuilds only what changed.
 """
+import glob
 import hashlib
 import os
 import subprocess
@@ -21,7 +22,10 @@ ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 HOST_SOURCES = ["host/mesh_loading.cpp", "host/kd_build.cpp", "host/scene_prepare.cpp", "host/misc.cpp",
                 "host/scenes.cpp"]
 HIP_SOURCES = ["path_kernel.hip", "wavefront.hip", "abi.hip", "shards.hip"]
-HEADERS = ["rt_libm.h", "rt_vecmath.h", "rt_device.h", "rt_kernels.h", "host/rt_host.h"]
+# every header under csrc/ (a header missing here would not trigger a rebuild)
+HEADERS = sorted(os.path.relpath(f, os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc"))
+                 for f in glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc", "**", "*.h"),
+                                    recursive=True))
 
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-I" + INCLUDE, "-I" + CSRC]
 HOST_FLAGS = ["-fopenmp", "-Wall", "-Wno-unused-function"]
