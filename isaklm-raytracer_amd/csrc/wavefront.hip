@@ -811,6 +811,12 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
     const int postpone = postpone_opt > 0 ? (postpone_opt > 64 ? 64 : postpone_opt) : WF_POSTPONE_DEFAULT;
     const int wide = wide_opt >= 0 ? 1 : 0; // finisher: lone rays traced by the whole wave
     static const bool trace_iters = getenv("RT_WF_TRACE_ITERS") != nullptr; // debug: per-iteration queue sizes
+    if (trace_iters) {
+        if (hipStreamSynchronize(stream) != hipSuccess) return -1;
+        timespec ts;
+        clock_gettime(CLOCK_MONOTONIC, &ts);
+        fprintf(stderr, "[wf] start live %zu t %.4f\n", slots, ts.tv_sec + ts.tv_nsec * 1e-9);
+    }
     // run the `live` paths of queue qq to the end of the call in the finisher
     auto finish = [&](int qq, uint32_t live) -> int {
         if (!mark(2)) return -1;
