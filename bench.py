@@ -249,7 +249,8 @@ def main():
         "data": "synthetic",
         "config": {
             "workload": (f"BASELINE configs[2]: README-like 2M-triangle synthetic room '{args.scene}', {W}x{H}, "
-                         f"{P} spp per step, adaptive off" if not args.adaptive and args.max_depth == 0 else
+                         f"{P} spp per step, adaptive off"
+                         if not args.adaptive and args.max_depth == 0 and args.scene == "room2m" else
                          f"scene '{args.scene}', {W}x{H}, {P} spp per step, adaptive "
                          f"{'on (min ' + str(args.min_samples) + ')' if args.adaptive else 'off'}, "
                          f"max depth {args.max_depth or 'unbounded'}"),
