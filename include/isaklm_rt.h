@@ -274,7 +274,9 @@ typedef struct RtOptions {
     int kernel;          /* RT_KERNEL_MEGA (one launch) or RT_KERNEL_WAVEFRONT (trace/shade queues) */
     void *stream;        /* hipStream_t; NULL = synchronous on the null stream */
     unsigned long long *counters_device; /* optional RT_CNT_COUNT u64 counters (adds) */
-    unsigned long long *wave_times_device; /* optional debug: 2 u64 per wave (megakernel, with counters) */
+    unsigned long long *wave_times_device; /* optional debug: megakernel (with counters): 2 u64 per wave;
+                          * wavefront: 3 u64 per trace launch (first start, first queue
+                          * exhaustion, ~last end; s_memrealtime, 100 MHz), pre-set to ~0 */
     /* wavefront tuning (0 = default): below wf_tail live paths the rest of
      * the call runs in one cooperative finisher launch on at most
      * wf_finish_waves waves; wf_tail > width*height runs the whole call in
@@ -286,7 +288,9 @@ typedef struct RtOptions {
      * round, and pending lanes (of 64) before a wave's leaf test runs */
     int wf_descent_cap;
     int wf_postpone;
-    int wf_wide;         /* finisher: a wave's lone ray is traced by all 64 lanes (0 = on, < 0 = off) */
+    int wf_wide;         /* wide single-ray traversal (all 64 lanes on one ray): < 0 off; else on for a
+                          * finisher wave's lone ray and, once a trace launch's queue is empty, for the
+                          * rays of waves with at most wf_wide (0 = default 16) left */
     /* row-interleaved sharding (the parity-exact option): with
      * num_shards > 1 only rows y % num_shards == shard_id are rendered (the
      * others are left untouched); every shard uses the single-stream seeds,

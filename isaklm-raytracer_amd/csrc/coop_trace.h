@@ -106,7 +106,7 @@ __device__ __forceinline__ bool coop_begin(const RtDevScene &sc, CoopRay &r, Vec
     r.node = 0;
     r.sp = 0;
     r.pend = false;
-    r.live = bbox_hit(sc, o, d, r.entry, r.exit_);
+    r.live = bbox_hit_recip(sc, o, d, r.yx, r.yy, r.yz, r.entry, r.exit_);
     r.root_exit = r.exit_;
     return r.live;
 }
@@ -335,28 +335,40 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v)
     return v;
 }
 
-// Trace the wave-uniform ray (o, d) whose scene-box interval is [entry, exit_]
-// with all 64 lanes.  Returns the hit (tri >= 0, barycentrics) or tri = -1.
-// Counters are added by `counter_lane` only.
+// per-wave LDS scratch of wide_trace
+struct WideLds {
+    WideItem *F;             // frontier, `cap` items
+    int cap;
+    unsigned long long *key; // 1: winner key
+    float *best;             // 4: winner barycentrics + triangle bits
+    int *mark;               // 64: chunk_owner marks
+};
+
+// an item whose node fetch (and, for a leaf, its triangle tests) the
+// sequential traversal already counted (a resumed ray's pending leaf)
+#define WIDE_COUNTED 0xFFFFFFFFu
+
+// Trace the wave-uniform ray (o, d) from a frontier of n items already in
+// W.F (F[n-1] is the next item in traversal order) with all 64 lanes.
+// Returns the hit (tri >= 0, barycentrics) or tri = -1.  Counters are added
+// by `counter_lane` only.
 template <bool COUNT>
-__device__ __forceinline__ void wide_trace(const RtDevScene &sc, Vec3D o, Vec3D d, float entry, float exit_,
-                                           WideItem *F, const CoopLds &w, bool counter_lane, int &tri, float &hbx,
-                                           float &hby, float &hbz, Cnt &c)
+__device__ __forceinline__ void wide_trace_from(const RtDevScene &sc, Vec3D o, Vec3D d, int n, const WideLds &W,
+                                                bool counter_lane, int &tri, float &hbx, float &hby, float &hbz,
+                                                Cnt &c)
 {
-    unsigned long long *wkey = w.key;
-    CoopCand *list = w.list;
+    WideItem *F = W.F;
+    unsigned long long *wkey = W.key;
     const int lane = __lane_id();
     const float ox = o.x, oy = o.y, oz = o.z, dx = d.x, dy = d.y, dz = d.z;
     const float yx = rt_recip_guard(dx), yy = rt_recip_guard(dy), yz = rt_recip_guard(dz);
-    if (lane == 0) F[0] = WideItem{0u, entry, exit_, 0u};
-    int n = 1;
     tri = -1;
     const unsigned long long t0 = COUNT ? __builtin_amdgcn_s_memtime() : 0ull;
     if (COUNT && counter_lane) c.v[RT_CNT_WIDE_CALLS]++;
     while (n > 0) {
         if (COUNT && counter_lane) c.v[RT_CNT_WIDE_ROUNDS]++;
         const unsigned long long tr0 = COUNT ? __builtin_amdgcn_s_memtime() : 0ull;
-        int k = WIDE_CAP - WIDE_RESERVE - n; // expansions add at most one item each
+        int k = W.cap - WIDE_RESERVE - n; // expansions add at most one item each
         k = k < 1 ? 1 : (k > 64 ? 64 : k);
         k = k < n ? k : n;
         WideItem it = WideItem{0u, 0.0f, 0.0f, 0u};
@@ -389,12 +401,12 @@ __device__ __forceinline__ void wide_trace(const RtDevScene &sc, Vec3D o, Vec3D 
             // plane and its barycentric record together (one memory round trip
             // per 64 pairs), and the current winner parks its barycentrics in
             // LDS so the result needs no reload
-            lds_vfloat *best = (lds_vfloat *)list;      // {bx, by, bz, tri bits}: cross-lane, see chunk_owner
+            lds_vfloat *best = (lds_vfloat *)W.best;    // {bx, by, bz, tri bits}: cross-lane, see chunk_owner
             lds_vu64 *vkey = (lds_vu64 *)wkey;
             int carry = -1;
             for (int base = 0; base < total; base += 64) {
                 const int p = base + lane;
-                const int j = chunk_owner(w.mark, start, cnt, base, carry); // owner leaf lane of pair p
+                const int j = chunk_owner(W.mark, start, cnt, base, carry); // owner leaf lane of pair p
                 carry = lane63(j);
                 const uint32_t e = (uint32_t)__shfl((int)kbase, j) + (uint32_t)p;
                 const float ex = __shfl(it.exit_, j);
@@ -435,8 +447,9 @@ __device__ __forceinline__ void wide_trace(const RtDevScene &sc, Vec3D o, Vec3D 
             const unsigned long long key = vkey[0];
             const int jstar = key != ~0ull ? (int)(key >> 58) : Le - 1;
             if (COUNT) { // leaves 0..jstar are the sequential traversal's next visits
-                const unsigned long long nv = wave_sum(lane <= jstar ? it.acc + 1ull : 0ull);
-                const unsigned long long tv = wave_sum(lane <= jstar ? (unsigned long long)cnt : 0ull);
+                const bool counted = it.acc == WIDE_COUNTED;
+                const unsigned long long nv = wave_sum(lane <= jstar && !counted ? it.acc + 1ull : 0ull);
+                const unsigned long long tv = wave_sum(lane <= jstar && !counted ? (unsigned long long)cnt : 0ull);
                 if (counter_lane) {
                     c.v[RT_CNT_NODE] += nv;
                     c.v[RT_CNT_TRI] += tv;
@@ -497,6 +510,42 @@ __device__ __forceinline__ void wide_trace(const RtDevScene &sc, Vec3D o, Vec3D 
         if (COUNT && counter_lane) c.v[RT_CNT_T_WIDE_EXPAND] += __builtin_amdgcn_s_memtime() - tex;
     }
     if (COUNT && counter_lane) c.v[RT_CNT_T_WIDE] += __builtin_amdgcn_s_memtime() - t0;
+}
+
+// a fresh ray (scene-box interval [entry, exit_]): the frontier is the root
+template <bool COUNT>
+__device__ __forceinline__ void wide_trace(const RtDevScene &sc, Vec3D o, Vec3D d, float entry, float exit_,
+                                           const WideLds &W, bool counter_lane, int &tri, float &hbx, float &hby,
+                                           float &hbz, Cnt &c)
+{
+    if (__lane_id() == 0) W.F[0] = WideItem{0u, entry, exit_, 0u};
+    wide_trace_from<COUNT>(sc, o, d, 1, W, counter_lane, tri, hbx, hby, hbz, c);
+}
+
+// Finish lane `owner`'s ray, which is in the middle of its cooperative
+// traversal, with all 64 lanes: its sequential state is already an ordered
+// frontier — stack entries 0..sp-1 (bottom = last in traversal order, each
+// with exit = the entry below it, or the root exit) under the current node
+// [entry, exit].  A pending leaf was counted when reached, so it is marked
+// WIDE_COUNTED.  `stk_owner` addresses the owner lane's stack.  Call with
+// all lanes active; results are wave-uniform.
+template <bool COUNT, int LDS_DEPTH>
+__device__ __forceinline__ void wide_resume(const RtDevScene &sc, const CoopRay &r, int owner,
+                                            const Stack<LDS_DEPTH> &stk_owner, const WideLds &W, int &tri,
+                                            float &hbx, float &hby, float &hbz, Cnt &c)
+{
+    const int lane = __lane_id();
+    const int sp = __shfl(r.sp, owner);
+    const Vec3D o = rt_v3(__shfl(r.o.x, owner), __shfl(r.o.y, owner), __shfl(r.o.z, owner));
+    const Vec3D d = rt_v3(__shfl(r.d.x, owner), __shfl(r.d.y, owner), __shfl(r.d.z, owner));
+    uint32_t node = 0;
+    float entry = 0.0f;
+    if (lane < sp) stk_owner.get(lane, node, entry);
+    const float below = __shfl_up(entry, 1); // entry of the stack entry below = this one's exit
+    const float root_exit = __shfl(r.root_exit, owner);
+    if (lane < sp) W.F[lane] = WideItem{node, entry, lane > 0 ? below : root_exit, 0u};
+    if (lane == owner) W.F[sp] = WideItem{r.node, r.entry, r.exit_, r.pend ? WIDE_COUNTED : 0u};
+    wide_trace_from<COUNT>(sc, o, d, sp + 1, W, lane == owner, tri, hbx, hby, hbz, c);
 }
 
 } // namespace rtk

@@ -54,6 +54,22 @@ __device__ __forceinline__ RtF4 ldf4(const RtF4 *p)
 }
 
 // intersect_bounding_box (rt/trace_ray.cuh:212-242)
+// the same with the ray's guarded reciprocals (rt_recip_guard): each slab
+// division by rt_div_by, bit-identical to the IEEE one
+__device__ __forceinline__ bool bbox_hit_recip(const RtDevScene &sc, Vec3D o, Vec3D d, float yx, float yy, float yz,
+                                               float &t1, float &t2)
+{
+    float tminx = rt_div_by(sc.bmin[0] - o.x, d.x, yx), tminy = rt_div_by(sc.bmin[1] - o.y, d.y, yy),
+          tminz = rt_div_by(sc.bmin[2] - o.z, d.z, yz);
+    float tmaxx = rt_div_by(sc.bmax[0] - o.x, d.x, yx), tmaxy = rt_div_by(sc.bmax[1] - o.y, d.y, yy),
+          tmaxz = rt_div_by(sc.bmax[2] - o.z, d.z, yz);
+    float s1x = fminf(tminx, tmaxx), s1y = fminf(tminy, tmaxy), s1z = fminf(tminz, tmaxz);
+    float s2x = fmaxf(tminx, tmaxx), s2y = fmaxf(tminy, tmaxy), s2z = fmaxf(tminz, tmaxz);
+    t1 = fmaxf(fmaxf(s1x, s1y), s1z);
+    t2 = fminf(fminf(s2x, s2y), s2z);
+    return t1 <= t2;
+}
+
 __device__ __forceinline__ bool bbox_hit(const RtDevScene &sc, Vec3D o, Vec3D d, float &t1, float &t2)
 {
     float tminx = (sc.bmin[0] - o.x) / d.x, tminy = (sc.bmin[1] - o.y) / d.y, tminz = (sc.bmin[2] - o.z) / d.z;

@@ -30,6 +30,8 @@ using namespace rtk;
 #define WF_FINISH_WAVES_DEFAULT 2048u // RtOptions.wf_finish_waves
 #define WF_DESCENT_CAP_DEFAULT 8      // RtOptions.wf_descent_cap
 #define WF_POSTPONE_DEFAULT 32        // RtOptions.wf_postpone
+#define WF_TIMELINE_LAUNCHES 4096     // debug timeline: 3 u64 per trace launch in RtOptions.wave_times_device
+#define WF_WIDE_TAIL_LANES 16         // RtOptions.wf_wide > 0
 
 struct WfState {
     int *passes_left;
@@ -321,8 +323,13 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_trace_dyn(RtDevScene sc, WfState 
 // `postpone` pending lanes.
 template <bool COUNT>
 __global__ void __launch_bounds__(WF_BLOCK, 6) wf_trace_coop(RtDevScene sc, WfState st, int q,
-                                                          unsigned long long *counters, int cap, int postpone)
+                                                          unsigned long long *counters, int cap, int postpone,
+                                                          int wide_lanes, unsigned long long *timeline)
 {
+    // debug timeline (RtOptions.wave_times_device): s_memrealtime of the
+    // launch's first wave start, first queue exhaustion, last wave end
+    // (stored as ~t so that all three are atomicMin)
+    if (timeline && __lane_id() == 0) atomicMin(timeline, __builtin_amdgcn_s_memrealtime());
     __shared__ uint32_t s_node[WF_LDS_STACK * WF_BLOCK];
     __shared__ float s_entry[WF_LDS_STACK * WF_BLOCK];
     __shared__ unsigned long long s_key[WF_BLOCK];
@@ -360,6 +367,7 @@ __global__ void __launch_bounds__(WF_BLOCK, 6) wf_trace_coop(RtDevScene sc, WfSt
                 e = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
                 if (e >= n) {
                     exhausted = true;
+                    if (timeline && e == n) atomicMin(timeline + 1, __builtin_amdgcn_s_memrealtime());
                 } else {
                     if (COUNT) c.v[RT_CNT_RAY]++;
                     if (!coop_begin(sc, r, ld3(ldf4(rays + 2 * (size_t)e)), ld3(ldf4(rays + 2 * (size_t)e + 1))))
@@ -374,9 +382,31 @@ __global__ void __launch_bounds__(WF_BLOCK, 6) wf_trace_coop(RtDevScene sc, WfSt
         }
         int tri = -1;
         float bx = 0.0f, by = 0.0f, bz = 0.0f;
+        // the launch's tail: the queue is empty and few rays are left in this
+        // wave — leave the loop and finish them wide (below)
+        if (wide_lanes > 0 && __any(exhausted) && __popcll(__ballot(r.live)) <= wide_lanes) break;
         if (coop_round<COUNT>(sc, r, stk, w, cap, postpone, tri, bx, by, bz, c))
             *reinterpret_cast<float4 *>(st.hits + e) = make_float4(__int_as_float(tri), bx, by, bz);
     }
+    // finish the wave's remaining rays one at a time with all 64 lanes
+    // (wide_resume) instead of letting the longest run alone at one lane's pace
+    const unsigned long long lm = __ballot(r.live);
+    if (lm) {
+        const WideLds W{reinterpret_cast<WideItem *>(list),
+                        WF_COOP_LIST * (int)sizeof(CoopCand) / (int)sizeof(WideItem), wkey,
+                        reinterpret_cast<float *>(wkey + 1), w.mark};
+        for (unsigned long long mm = lm; mm; mm &= mm - 1) {
+            const int owner = __ffsll((long long)mm) - 1;
+            const int ot = wave * 64 + owner;
+            const Stack<WF_LDS_STACK> so{s_node + ot, s_entry + ot, WF_BLOCK, st.spill + blockIdx.x * WF_BLOCK + ot,
+                                         st.spill_threads};
+            int tri = -1;
+            float bx = 0.0f, by = 0.0f, bz = 0.0f;
+            wide_resume<COUNT>(sc, r, owner, so, W, tri, bx, by, bz, c);
+            if (lane == owner) *reinterpret_cast<float4 *>(st.hits + e) = make_float4(__int_as_float(tri), bx, by, bz);
+        }
+    }
+    if (timeline && lane == 0) atomicMin(timeline + 2, ~__builtin_amdgcn_s_memrealtime());
     if (COUNT) flush_counters(c, counters);
 }
 
@@ -676,8 +706,9 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_finish_coop(RtDevScene sc, RtDevF
                 const Vec3D d = rt_v3(__shfl(r.d.x, owner), __shfl(r.d.y, owner), __shfl(r.d.z, owner));
                 int t;
                 float x, y, z;
-                wide_trace<COUNT>(sc, o, d, __shfl(r.entry, owner), __shfl(r.exit_, owner), s_wide + wave * WIDE_CAP,
-                                  w, lane == owner, t, x, y, z, c);
+                const WideLds W{s_wide + wave * WIDE_CAP, WIDE_CAP, wkey, reinterpret_cast<float *>(wkey + 1), w.mark};
+                wide_trace<COUNT>(sc, o, d, __shfl(r.entry, owner), __shfl(r.exit_, owner), W, lane == owner, t, x, y,
+                                  z, c);
                 if (lane == owner) {
                     hit = t;
                     bx = x;
@@ -810,6 +841,8 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
     const int cap = cap_opt > 0 ? cap_opt : WF_DESCENT_CAP_DEFAULT;
     const int postpone = postpone_opt > 0 ? (postpone_opt > 64 ? 64 : postpone_opt) : WF_POSTPONE_DEFAULT;
     const int wide = wide_opt >= 0 ? 1 : 0; // finisher: lone rays traced by the whole wave
+    // trace launches: once the queue is empty, a wave with at most this many rays left finishes them wide
+    const int wide_lanes = wide_opt < 0 ? 0 : (wide_opt > 0 ? (wide_opt > 64 ? 64 : wide_opt) : WF_WIDE_TAIL_LANES);
     static const bool trace_iters = getenv("RT_WF_TRACE_ITERS") != nullptr; // debug: per-iteration queue sizes
     if (trace_iters) {
         if (hipStreamSynchronize(stream) != hipSuccess) return -1;
@@ -856,8 +889,13 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
             if (hipMemsetAsync(w.st.counts + 2 + q, 0, 4, stream) != hipSuccess) return -1; // fetch cursor
             if (!mark(4)) return -1;
             if (trace_kind == 1) {
-                if (count) hipLaunchKernelGGL(wf_trace_coop<true>, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, w.st, q, fr.counters, cap, postpone);
-                else hipLaunchKernelGGL(wf_trace_coop<false>, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, w.st, q, fr.counters, cap, postpone);
+                unsigned long long *tl = fr.wave_times && it < WF_TIMELINE_LAUNCHES ? fr.wave_times + 3 * it : nullptr;
+                if (count)
+                    hipLaunchKernelGGL(wf_trace_coop<true>, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, w.st, q,
+                                       fr.counters, cap, postpone, wide_lanes, tl);
+                else
+                    hipLaunchKernelGGL(wf_trace_coop<false>, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, w.st, q,
+                                       fr.counters, cap, postpone, wide_lanes, tl);
             } else if (trace_kind == 3) {
                 if (count) hipLaunchKernelGGL(wf_trace_dyn<true>, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, w.st, q, fr.counters);
                 else hipLaunchKernelGGL(wf_trace_dyn<false>, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, w.st, q, fr.counters);

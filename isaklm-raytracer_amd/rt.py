@@ -289,7 +289,7 @@ KERNEL_WAVEFRONT = 1
 
 def options(width, height, passes=1, adaptive=True, min_samples=100, tolerance=0.05, max_depth=0, stream=None,
             counters=None, kernel=KERNEL_MEGA, wf_tail=0, wf_finish_waves=0, profile=False, wf_descent_cap=0,
-            wf_postpone=0, wf_wide=0, shard_id=0, num_shards=1):
+            wf_postpone=0, wf_wide=0, shard_id=0, num_shards=1, wave_times=None):
     o = RtOptions()
     lib().rt_default_options(ctypes.byref(o))
     o.width, o.height, o.passes = width, height, passes
@@ -300,6 +300,7 @@ def options(width, height, passes=1, adaptive=True, min_samples=100, tolerance=0
     o.wf_tail, o.wf_finish_waves, o.profile = wf_tail, wf_finish_waves, int(profile)
     o.wf_descent_cap, o.wf_postpone, o.wf_wide = wf_descent_cap, wf_postpone, wf_wide
     o.shard_id, o.num_shards = shard_id, num_shards
+    o.wave_times_device = wave_times
     return o
 
 
