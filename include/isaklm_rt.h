@@ -301,6 +301,10 @@ typedef struct RtOptions {
      * [g*W*H, (g+1)*W*H) (rt_gbuffer_seeds skip). */
     int shard_id;
     int num_shards;
+    /* wavefront: concurrent pipelines over disjoint pixel tiles, each with
+     * its own queues and stream, so one pipeline's latency-bound launch
+     * tails and finisher overlap the others' bulk work (0 = default 2, max 4) */
+    int wf_pipelines;
 } RtOptions;
 
 /* Per-call kernel timing of the last rt_render on this device with

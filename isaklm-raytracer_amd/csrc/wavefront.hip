@@ -19,6 +19,7 @@
 #include <time.h>
 
 #include <map>
+#include <thread>
 
 #include "rt_kernels.h"
 
@@ -32,6 +33,8 @@ using namespace rtk;
 #define WF_POSTPONE_DEFAULT 32        // RtOptions.wf_postpone
 #define WF_TIMELINE_LAUNCHES 4096     // debug timeline: 3 u64 per trace launch in RtOptions.wave_times_device
 #define WF_WIDE_TAIL_LANES 16         // RtOptions.wf_wide > 0
+#define WF_MAX_PIPES 4                // concurrent pipelines (RtOptions.wf_pipelines)
+#define WF_PIPES_DEFAULT 2
 
 struct WfState {
     int *passes_left;
@@ -92,12 +95,14 @@ __device__ __forceinline__ bool start_sample(const RtDevFrame &fr, const RtDevCa
 } // namespace
 
 template <bool COUNT>
-__global__ void __launch_bounds__(WF_BLOCK) wf_start(RtDevFrame fr, RtDevCamera cam, WfState st)
+__global__ void __launch_bounds__(WF_BLOCK) wf_start(RtDevFrame fr, RtDevCamera cam, WfState st, int pipe,
+                                                     int npipes)
 {
     Cnt c;
     if (COUNT) c.zero();
     const int n = fr.width * fr.height;
     const int tile = xcd_tile(blockIdx.x, gridDim.x);
+    if (tile % npipes != pipe) return; // another pipeline's 16x16 tile (block-uniform)
     const int tiles_x = (fr.width + 15) / 16;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int x = (tile % tiles_x) * 16 + (wave & 1) * 8 + (lane & 7);
@@ -731,14 +736,27 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_finish_coop(RtDevScene sc, RtDevF
 // ---------------------------------------------------------------- launcher
 namespace {
 
+// One pipeline = its own ray queues, hits, counters, stack spill area and
+// HIP stream over a disjoint set of 16x16 pixel tiles (tile % npipes).  The
+// pipelines run concurrently (one host thread each), so the latency-bound
+// tail of one pipeline's trace launches and its finisher overlap the other
+// pipelines' bulk work.  Per-pixel path state is shared (pixels are disjoint).
+struct Pipe {
+    WfState st{};
+    hipStream_t stream = nullptr;
+    uint32_t *host_count = nullptr;
+    hipEvent_t ev[6] = {};   // RtOptions.profile
+    hipEvent_t join = nullptr;
+    RtProfile prof{};
+};
+
 struct Workspace {
     size_t slots = 0;
     int grid = 0;
-    WfState st{};
     void *blob = nullptr;
-    uint32_t *host_count = nullptr;
-    hipEvent_t ev[6] = {};   // RtOptions.profile
-    bool ev_ok = false;
+    Pipe pipe[WF_MAX_PIPES];
+    bool streams_ok = false;
+    hipEvent_t fork = nullptr, ev0 = nullptr, ev1 = nullptr;
     RtProfile prof{};        // last profiled call
 };
 
@@ -746,9 +764,21 @@ std::map<int, Workspace> g_ws; // per device
 
 int ensure(Workspace &w, size_t slots, int grid)
 {
+    if (!w.streams_ok) {
+        if (hipEventCreateWithFlags(&w.fork, hipEventDisableTiming) != hipSuccess) return -1;
+        if (hipEventCreate(&w.ev0) != hipSuccess || hipEventCreate(&w.ev1) != hipSuccess) return -1;
+        for (Pipe &p : w.pipe) {
+            if (hipStreamCreateWithFlags(&p.stream, hipStreamNonBlocking) != hipSuccess) return -1;
+            if (hipHostMalloc((void **)&p.host_count, 64) != hipSuccess) return -1;
+            if (hipEventCreateWithFlags(&p.join, hipEventDisableTiming) != hipSuccess) return -1;
+            for (auto &e : p.ev)
+                if (hipEventCreate(&e) != hipSuccess) return -1;
+        }
+        w.streams_ok = true;
+    }
     if (w.slots >= slots && w.grid >= grid) return 0;
     if (w.blob) (void)hipFree(w.blob);
-    if (!w.host_count && hipHostMalloc((void **)&w.host_count, 64) != hipSuccess) return -1;
+    w.blob = nullptr;
     const size_t spill_threads = (size_t)grid * WF_BLOCK;
     size_t off = 0;
     auto take = [&](size_t bytes) {
@@ -756,32 +786,45 @@ int ensure(Workspace &w, size_t slots, int grid)
         off += (bytes + 255) & ~(size_t)255;
         return o;
     };
+    // per pixel
     const size_t o_pl = take(slots * 4), o_fl = take(slots * 4), o_T = take(slots * 12), o_L = take(slots * 12),
-                 o_c = take(slots * 12), o_n = take(slots * 12), o_rp = take(slots * 12), o_li = take(slots * 4),
-                 o_qs0 = take(slots * 4), o_qs1 = take(slots * 4), o_qr0 = take(slots * 32),
-                 o_qr1 = take(slots * 32), o_h = take(slots * 16), o_cnt = take(64),
-                 o_sp = take(spill_threads * 8 * (RT_STACK_DEPTH - WF_LDS_STACK));
+                 o_c = take(slots * 12), o_n = take(slots * 12), o_rp = take(slots * 12), o_li = take(slots * 4);
+    // per pipeline (queues sized for every pixel: a pipeline never holds more)
+    size_t o_qs0[WF_MAX_PIPES], o_qs1[WF_MAX_PIPES], o_qr0[WF_MAX_PIPES], o_qr1[WF_MAX_PIPES], o_h[WF_MAX_PIPES],
+        o_cnt[WF_MAX_PIPES], o_sp[WF_MAX_PIPES];
+    for (int i = 0; i < WF_MAX_PIPES; ++i) {
+        o_qs0[i] = take(slots * 4);
+        o_qs1[i] = take(slots * 4);
+        o_qr0[i] = take(slots * 32);
+        o_qr1[i] = take(slots * 32);
+        o_h[i] = take(slots * 16);
+        o_cnt[i] = take(256);
+        o_sp[i] = take(spill_threads * 8 * (RT_STACK_DEPTH - WF_LDS_STACK));
+    }
     if (hipMalloc(&w.blob, off) != hipSuccess) {
         w.blob = nullptr;
         return -1;
     }
     char *b = (char *)w.blob;
-    w.st.passes_left = (int *)(b + o_pl);
-    w.st.flags = (uint32_t *)(b + o_fl);
-    w.st.T = (Vec3D *)(b + o_T);
-    w.st.L = (Vec3D *)(b + o_L);
-    w.st.cont = (Vec3D *)(b + o_c);
-    w.st.snorm = (Vec3D *)(b + o_n);
-    w.st.rp = (Vec3D *)(b + o_rp);
-    w.st.light = (int *)(b + o_li);
-    w.st.q_slot[0] = (uint32_t *)(b + o_qs0);
-    w.st.q_slot[1] = (uint32_t *)(b + o_qs1);
-    w.st.q_ray[0] = (RtF4 *)(b + o_qr0);
-    w.st.q_ray[1] = (RtF4 *)(b + o_qr1);
-    w.st.hits = (RtF4 *)(b + o_h);
-    w.st.counts = (uint32_t *)(b + o_cnt);
-    w.st.spill = (uint2 *)(b + o_sp);
-    w.st.spill_threads = (int)spill_threads;
+    for (int i = 0; i < WF_MAX_PIPES; ++i) {
+        WfState &st = w.pipe[i].st;
+        st.passes_left = (int *)(b + o_pl);
+        st.flags = (uint32_t *)(b + o_fl);
+        st.T = (Vec3D *)(b + o_T);
+        st.L = (Vec3D *)(b + o_L);
+        st.cont = (Vec3D *)(b + o_c);
+        st.snorm = (Vec3D *)(b + o_n);
+        st.rp = (Vec3D *)(b + o_rp);
+        st.light = (int *)(b + o_li);
+        st.q_slot[0] = (uint32_t *)(b + o_qs0[i]);
+        st.q_slot[1] = (uint32_t *)(b + o_qs1[i]);
+        st.q_ray[0] = (RtF4 *)(b + o_qr0[i]);
+        st.q_ray[1] = (RtF4 *)(b + o_qr1[i]);
+        st.hits = (RtF4 *)(b + o_h[i]);
+        st.counts = (uint32_t *)(b + o_cnt[i]);
+        st.spill = (uint2 *)(b + o_sp[i]);
+        st.spill_threads = (int)spill_threads;
+    }
     w.slots = slots;
     w.grid = grid;
     return 0;
@@ -807,7 +850,7 @@ extern "C" int rt_last_profile(RtProfile *out)
 
 int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevCamera &cam, hipStream_t stream,
                         int variant, int tail_opt, int finish_waves_opt, int profile, int cap_opt, int postpone_opt,
-                        int wide_opt)
+                        int wide_opt, int pipes_opt)
 {
     // 1: wave-cooperative leaves (entries packed as k << 6 | lane: needs < 2^26 entries), 2: static, 3: per-lane fetch
     int trace_kind = variant;
@@ -820,19 +863,10 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
     if (ensure(w, slots, grid) != 0) return -1;
     const bool count = fr.counters != nullptr;
     const bool prof = profile != 0;
-    if (prof && !w.ev_ok) {
-        for (auto &e : w.ev)
-            if (hipEventCreate(&e) != hipSuccess) return -1;
-        w.ev_ok = true;
-    }
-    RtProfile P{};
-    auto mark = [&](int i) { return !prof || hipEventRecord(w.ev[i], stream) == hipSuccess; };
-    if (!mark(0)) return -1;
-    if (hipMemsetAsync(w.st.counts, 0, 64, stream) != hipSuccess) return -1;
     const int tiles = ((fr.width + 15) / 16) * ((fr.height + 15) / 16);
-    if (count) hipLaunchKernelGGL(wf_start<true>, dim3(tiles), dim3(WF_BLOCK), 0, stream, fr, cam, w.st);
-    else hipLaunchKernelGGL(wf_start<false>, dim3(tiles), dim3(WF_BLOCK), 0, stream, fr, cam, w.st);
-    if (!mark(1)) return -1;
+    int npipes = pipes_opt > 0 ? pipes_opt : WF_PIPES_DEFAULT;
+    npipes = npipes > WF_MAX_PIPES ? WF_MAX_PIPES : npipes;
+    npipes = npipes > tiles ? tiles : npipes;
     // below this many live paths the rest of the call runs in one finisher launch
     const uint32_t tail = tail_opt > 0 ? (uint32_t)tail_opt : WF_TAIL_DEFAULT;
     // the cooperative finisher runs on at most this many waves (up to 64 paths in flight each)
@@ -844,98 +878,142 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
     // trace launches: once the queue is empty, a wave with at most this many rays left finishes them wide
     const int wide_lanes = wide_opt < 0 ? 0 : (wide_opt > 0 ? (wide_opt > 64 ? 64 : wide_opt) : WF_WIDE_TAIL_LANES);
     static const bool trace_iters = getenv("RT_WF_TRACE_ITERS") != nullptr; // debug: per-iteration queue sizes
-    if (trace_iters) {
-        if (hipStreamSynchronize(stream) != hipSuccess) return -1;
-        timespec ts;
-        clock_gettime(CLOCK_MONOTONIC, &ts);
-        fprintf(stderr, "[wf] start live %zu t %.4f\n", slots, ts.tv_sec + ts.tv_nsec * 1e-9);
-    }
-    // run the `live` paths of queue qq to the end of the call in the finisher
-    auto finish = [&](int qq, uint32_t live) -> int {
-        if (!mark(2)) return -1;
-        if (trace_kind == 1) {
-            // paths per wave: spread over up to finish_waves waves, within the spill area (grid * WF_BLOCK threads)
-            const uint32_t max_waves = (uint32_t)grid * (WF_BLOCK / 64);
-            uint32_t ppw = (live + finish_waves - 1) / finish_waves;
-            ppw = ppw < 1 ? 1 : (ppw > 64 ? 64 : ppw);
-            uint32_t waves = (live + ppw - 1) / ppw;
-            if (waves > finish_waves) waves = finish_waves;
-            if (waves > max_waves) waves = max_waves; // persistent: lanes fetch paths until the queue is empty
-            if (hipMemsetAsync(w.st.counts + 4, 0, 4, stream) != hipSuccess) return -1;
-            const int fgrid = (int)((waves + WF_BLOCK / 64 - 1) / (WF_BLOCK / 64));
-            if (count)
-                hipLaunchKernelGGL(wf_finish_coop<true>, dim3(fgrid), dim3(WF_BLOCK), 0, stream, sc, fr, cam, w.st,
-                                   qq, (int)ppw, cap, postpone, wide);
-            else
-                hipLaunchKernelGGL(wf_finish_coop<false>, dim3(fgrid), dim3(WF_BLOCK), 0, stream, sc, fr, cam, w.st,
-                                   qq, (int)ppw, cap, postpone, wide);
+
+    // fork: every pipeline stream starts after the caller's stream
+    if (hipEventRecord(w.fork, stream) != hipSuccess) return -1;
+    if (prof && hipEventRecord(w.ev0, stream) != hipSuccess) return -1;
+
+    auto run_pipe = [&](int pi) -> int {
+        if (hipSetDevice(dev) != hipSuccess) return -1;
+        Pipe &pp = w.pipe[pi];
+        WfState &st = pp.st;
+        hipStream_t s = pp.stream;
+        if (hipStreamWaitEvent(s, w.fork, 0) != hipSuccess) return -1;
+        RtProfile P{};
+        auto mark = [&](int i) { return !prof || hipEventRecord(pp.ev[i], s) == hipSuccess; };
+        if (!mark(0)) return -1;
+        if (hipMemsetAsync(st.counts, 0, 256, s) != hipSuccess) return -1;
+        if (count) hipLaunchKernelGGL(wf_start<true>, dim3(tiles), dim3(WF_BLOCK), 0, s, fr, cam, st, pi, npipes);
+        else hipLaunchKernelGGL(wf_start<false>, dim3(tiles), dim3(WF_BLOCK), 0, s, fr, cam, st, pi, npipes);
+        if (!mark(1)) return -1;
+        // run the `live` paths of queue qq to the end of the call in the finisher
+        auto finish = [&](int qq, uint32_t live) -> int {
+            if (!mark(2)) return -1;
+            if (trace_kind == 1) {
+                // paths per wave: spread over up to finish_waves waves, within the spill area (grid * WF_BLOCK threads)
+                const uint32_t max_waves = (uint32_t)grid * (WF_BLOCK / 64);
+                uint32_t ppw = (live + finish_waves - 1) / finish_waves;
+                ppw = ppw < 1 ? 1 : (ppw > 64 ? 64 : ppw);
+                uint32_t waves = (live + ppw - 1) / ppw;
+                if (waves > finish_waves) waves = finish_waves;
+                if (waves > max_waves) waves = max_waves; // persistent: lanes fetch paths until the queue is empty
+                if (hipMemsetAsync(st.counts + 4, 0, 4, s) != hipSuccess) return -1;
+                const int fgrid = (int)((waves + WF_BLOCK / 64 - 1) / (WF_BLOCK / 64));
+                if (count)
+                    hipLaunchKernelGGL(wf_finish_coop<true>, dim3(fgrid), dim3(WF_BLOCK), 0, s, sc, fr, cam, st, qq,
+                                       (int)ppw, cap, postpone, wide);
+                else
+                    hipLaunchKernelGGL(wf_finish_coop<false>, dim3(fgrid), dim3(WF_BLOCK), 0, s, sc, fr, cam, st, qq,
+                                       (int)ppw, cap, postpone, wide);
+            } else {
+                const int fgrid = (int)((live + WF_BLOCK - 1) / WF_BLOCK);
+                if (count) hipLaunchKernelGGL(wf_finish<true>, dim3(fgrid), dim3(WF_BLOCK), 0, s, sc, fr, cam, st, qq);
+                else hipLaunchKernelGGL(wf_finish<false>, dim3(fgrid), dim3(WF_BLOCK), 0, s, sc, fr, cam, st, qq);
+            }
+            if (hipGetLastError() != hipSuccess || !mark(3)) return -1;
+            P.finish_launches = 1;
+            return 0;
+        };
+        int rc = 0;
+        if (trace_kind == 1 && tail > slots) {
+            // wf_tail above the frame size: the whole call runs in the finisher (no queue iterations)
+            rc = finish(0, (uint32_t)slots);
         } else {
-            const int fgrid = (int)((live + WF_BLOCK - 1) / WF_BLOCK);
-            if (count) hipLaunchKernelGGL(wf_finish<true>, dim3(fgrid), dim3(WF_BLOCK), 0, stream, sc, fr, cam, w.st, qq);
-            else hipLaunchKernelGGL(wf_finish<false>, dim3(fgrid), dim3(WF_BLOCK), 0, stream, sc, fr, cam, w.st, qq);
+            for (int it = 0;; ++it) {
+                const int q = it & 1;
+                if (hipMemsetAsync(st.counts + (q ^ 1), 0, 4, s) != hipSuccess) return -1;
+                if (hipMemsetAsync(st.counts + 2 + q, 0, 4, s) != hipSuccess) return -1; // fetch cursor
+                if (!mark(4)) return -1;
+                if (trace_kind == 1) {
+                    const int li = it * npipes + pi;
+                    unsigned long long *tl = fr.wave_times && li < WF_TIMELINE_LAUNCHES ? fr.wave_times + 3 * li : nullptr;
+                    if (count)
+                        hipLaunchKernelGGL(wf_trace_coop<true>, dim3(grid), dim3(WF_BLOCK), 0, s, sc, st, q,
+                                           fr.counters, cap, postpone, wide_lanes, tl);
+                    else
+                        hipLaunchKernelGGL(wf_trace_coop<false>, dim3(grid), dim3(WF_BLOCK), 0, s, sc, st, q,
+                                           fr.counters, cap, postpone, wide_lanes, tl);
+                } else if (trace_kind == 3) {
+                    if (count) hipLaunchKernelGGL(wf_trace_dyn<true>, dim3(grid), dim3(WF_BLOCK), 0, s, sc, st, q, fr.counters);
+                    else hipLaunchKernelGGL(wf_trace_dyn<false>, dim3(grid), dim3(WF_BLOCK), 0, s, sc, st, q, fr.counters);
+                } else {
+                    if (count) hipLaunchKernelGGL(wf_trace<true>, dim3(grid), dim3(WF_BLOCK), 0, s, sc, st, q, fr.counters);
+                    else hipLaunchKernelGGL(wf_trace<false>, dim3(grid), dim3(WF_BLOCK), 0, s, sc, st, q, fr.counters);
+                }
+                if (!mark(5)) return -1;
+                if (count) hipLaunchKernelGGL(wf_shade<true>, dim3(grid), dim3(WF_BLOCK), 0, s, sc, fr, cam, st, q);
+                else hipLaunchKernelGGL(wf_shade<false>, dim3(grid), dim3(WF_BLOCK), 0, s, sc, fr, cam, st, q);
+                if (hipGetLastError() != hipSuccess) return -1;
+                if (!mark(2)) return -1;
+                if (hipMemcpyAsync(pp.host_count, st.counts + (q ^ 1), 4, hipMemcpyDeviceToHost, s) != hipSuccess)
+                    return -1;
+                if (hipStreamSynchronize(s) != hipSuccess) return -1;
+                const uint32_t live = *pp.host_count;
+                P.iterations = it + 1;
+                if (prof) {
+                    P.trace_ms += elapsed_ms(pp.ev[4], pp.ev[5]);
+                    P.shade_ms += elapsed_ms(pp.ev[5], pp.ev[2]);
+                }
+                if (trace_iters) {
+                    timespec ts;
+                    clock_gettime(CLOCK_MONOTONIC, &ts);
+                    fprintf(stderr, "[wf] pipe %d it %d live %u t %.4f\n", pi, it, live, ts.tv_sec + ts.tv_nsec * 1e-9);
+                }
+                if (live == 0) break;
+                if (live < tail) {
+                    rc = finish(q ^ 1, live);
+                    break;
+                }
+            }
         }
-        if (hipGetLastError() != hipSuccess || !mark(3)) return -1;
-        P.finish_launches = 1;
+        if (rc != 0) return rc;
+        if (hipEventRecord(pp.join, s) != hipSuccess) return -1;
+        if (prof) {
+            if (!mark(4) || hipEventSynchronize(pp.ev[4]) != hipSuccess) return -1;
+            P.trace_launches = P.shade_launches = P.iterations;
+            P.start_ms = elapsed_ms(pp.ev[0], pp.ev[1]);
+            if (P.finish_launches) P.finish_ms = elapsed_ms(pp.ev[2], pp.ev[3]);
+            P.call_ms = elapsed_ms(pp.ev[0], pp.ev[4]);
+        }
+        pp.prof = P;
         return 0;
     };
-    int rc = 0;
-    if (trace_kind == 1 && tail > slots) {
-        // wf_tail above the frame size: the whole call runs in the finisher (no queue iterations)
-        rc = finish(0, (uint32_t)slots);
-    } else {
-        for (int it = 0;; ++it) {
-            const int q = it & 1;
-            if (hipMemsetAsync(w.st.counts + (q ^ 1), 0, 4, stream) != hipSuccess) return -1;
-            if (hipMemsetAsync(w.st.counts + 2 + q, 0, 4, stream) != hipSuccess) return -1; // fetch cursor
-            if (!mark(4)) return -1;
-            if (trace_kind == 1) {
-                unsigned long long *tl = fr.wave_times && it < WF_TIMELINE_LAUNCHES ? fr.wave_times + 3 * it : nullptr;
-                if (count)
-                    hipLaunchKernelGGL(wf_trace_coop<true>, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, w.st, q,
-                                       fr.counters, cap, postpone, wide_lanes, tl);
-                else
-                    hipLaunchKernelGGL(wf_trace_coop<false>, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, w.st, q,
-                                       fr.counters, cap, postpone, wide_lanes, tl);
-            } else if (trace_kind == 3) {
-                if (count) hipLaunchKernelGGL(wf_trace_dyn<true>, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, w.st, q, fr.counters);
-                else hipLaunchKernelGGL(wf_trace_dyn<false>, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, w.st, q, fr.counters);
-            } else {
-                if (count) hipLaunchKernelGGL(wf_trace<true>, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, w.st, q, fr.counters);
-                else hipLaunchKernelGGL(wf_trace<false>, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, w.st, q, fr.counters);
-            }
-            if (!mark(5)) return -1;
-            if (count) hipLaunchKernelGGL(wf_shade<true>, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, fr, cam, w.st, q);
-            else hipLaunchKernelGGL(wf_shade<false>, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, fr, cam, w.st, q);
-            if (hipGetLastError() != hipSuccess) return -1;
-            if (!mark(2)) return -1;
-            if (hipMemcpyAsync(w.host_count, w.st.counts + (q ^ 1), 4, hipMemcpyDeviceToHost, stream) != hipSuccess)
-                return -1;
-            if (hipStreamSynchronize(stream) != hipSuccess) return -1;
-            const uint32_t live = *w.host_count;
-            P.iterations = it + 1;
-            if (prof) {
-                P.trace_ms += elapsed_ms(w.ev[4], w.ev[5]);
-                P.shade_ms += elapsed_ms(w.ev[5], w.ev[2]);
-            }
-            if (trace_iters) {
-                timespec ts;
-                clock_gettime(CLOCK_MONOTONIC, &ts);
-                fprintf(stderr, "[wf] it %d live %u t %.4f\n", it, live, ts.tv_sec + ts.tv_nsec * 1e-9);
-            }
-            if (live == 0) break;
-            if (live < tail) {
-                rc = finish(q ^ 1, live);
-                break;
-            }
-        }
-    }
-    if (rc != 0) return rc;
+
+    int rcs[WF_MAX_PIPES] = {};
+    std::thread threads[WF_MAX_PIPES];
+    for (int pi = 1; pi < npipes; ++pi) threads[pi] = std::thread([&, pi] { rcs[pi] = run_pipe(pi); });
+    rcs[0] = run_pipe(0);
+    for (int pi = 1; pi < npipes; ++pi) threads[pi].join();
+    for (int pi = 0; pi < npipes; ++pi)
+        if (rcs[pi] != 0) return rcs[pi];
+    // join: the caller's stream continues after every pipeline
+    for (int pi = 0; pi < npipes; ++pi)
+        if (hipStreamWaitEvent(stream, w.pipe[pi].join, 0) != hipSuccess) return -1;
     if (prof) {
-        if (!mark(4) || hipEventSynchronize(w.ev[4]) != hipSuccess) return -1;
-        P.trace_launches = P.shade_launches = P.iterations;
-        P.start_ms = elapsed_ms(w.ev[0], w.ev[1]);
-        if (P.finish_launches) P.finish_ms = elapsed_ms(w.ev[2], w.ev[3]);
-        P.call_ms = elapsed_ms(w.ev[0], w.ev[4]);
+        RtProfile P{};
+        for (int pi = 0; pi < npipes; ++pi) { // kernel times summed over the (concurrent) pipelines
+            const RtProfile &q = w.pipe[pi].prof;
+            P.iterations += q.iterations;
+            P.trace_launches += q.trace_launches;
+            P.shade_launches += q.shade_launches;
+            P.finish_launches += q.finish_launches;
+            P.start_ms += q.start_ms;
+            P.trace_ms += q.trace_ms;
+            P.shade_ms += q.shade_ms;
+            P.finish_ms += q.finish_ms;
+        }
+        if (hipEventRecord(w.ev1, stream) != hipSuccess || hipEventSynchronize(w.ev1) != hipSuccess) return -1;
+        P.call_ms = elapsed_ms(w.ev0, w.ev1); // wall time of the call
         w.prof = P;
     }
     return 0;

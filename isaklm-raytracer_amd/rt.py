@@ -55,7 +55,7 @@ class RtOptions(ctypes.Structure):
                 ("counters_device", ctypes.c_void_p), ("wave_times_device", ctypes.c_void_p),
                 ("wf_tail", ctypes.c_int), ("wf_finish_waves", ctypes.c_int), ("profile", ctypes.c_int),
                 ("wf_descent_cap", ctypes.c_int), ("wf_postpone", ctypes.c_int), ("wf_wide", ctypes.c_int),
-                ("shard_id", ctypes.c_int), ("num_shards", ctypes.c_int)]
+                ("shard_id", ctypes.c_int), ("num_shards", ctypes.c_int), ("wf_pipelines", ctypes.c_int)]
 
 
 class RtProfile(ctypes.Structure):
@@ -289,7 +289,7 @@ KERNEL_WAVEFRONT = 1
 
 def options(width, height, passes=1, adaptive=True, min_samples=100, tolerance=0.05, max_depth=0, stream=None,
             counters=None, kernel=KERNEL_MEGA, wf_tail=0, wf_finish_waves=0, profile=False, wf_descent_cap=0,
-            wf_postpone=0, wf_wide=0, shard_id=0, num_shards=1, wave_times=None):
+            wf_postpone=0, wf_wide=0, shard_id=0, num_shards=1, wave_times=None, wf_pipelines=0):
     o = RtOptions()
     lib().rt_default_options(ctypes.byref(o))
     o.width, o.height, o.passes = width, height, passes
@@ -301,6 +301,7 @@ def options(width, height, passes=1, adaptive=True, min_samples=100, tolerance=0
     o.wf_descent_cap, o.wf_postpone, o.wf_wide = wf_descent_cap, wf_postpone, wf_wide
     o.shard_id, o.num_shards = shard_id, num_shards
     o.wave_times_device = wave_times
+    o.wf_pipelines = wf_pipelines
     return o
 
 
