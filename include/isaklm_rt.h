@@ -290,7 +290,7 @@ typedef struct RtOptions {
     int wf_postpone;
     int wf_wide;         /* wide single-ray traversal (all 64 lanes on one ray): < 0 off; else on for a
                           * finisher wave's lone ray and, once a trace launch's queue is empty, for the
-                          * rays of waves with at most wf_wide (0 = default 16) left */
+                          * rays of waves with at most wf_wide (0 = default 32) left */
     /* row-interleaved sharding (the parity-exact option): with
      * num_shards > 1 only rows y % num_shards == shard_id are rendered (the
      * others are left untouched); every shard uses the single-stream seeds,
@@ -303,7 +303,8 @@ typedef struct RtOptions {
     int num_shards;
     /* wavefront: concurrent pipelines over disjoint pixel tiles, each with
      * its own queues and stream, so one pipeline's latency-bound launch
-     * tails and finisher overlap the others' bulk work (0 = default 2, max 4) */
+     * tails and finisher overlap the others' bulk work (0 = default 3, max 3:
+     * with the caller's stream that is the 4 hardware queues of a process) */
     int wf_pipelines;
 } RtOptions;
 
@@ -316,8 +317,11 @@ typedef struct RtProfile {
     float start_ms;      /* wf_start */
     float trace_ms;      /* sum over the call's trace launches */
     float shade_ms;      /* sum over the call's shade launches */
-    float finish_ms;     /* the finisher launch (0 or 1 per call) */
+    float finish_ms;     /* the finisher launches (0 or 1 per pipeline) */
     float call_ms;       /* first to last event of the call */
+    float trace_union_ms; /* wall time with at least one trace launch running (launches of
+                          * concurrent pipelines overlap: trace_ms sums their durations) */
+    int pipelines;
 } RtProfile;
 int rt_last_profile(RtProfile *out);
 

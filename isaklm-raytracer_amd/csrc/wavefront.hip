@@ -18,8 +18,10 @@
 #include <stdio.h>
 #include <time.h>
 
+#include <algorithm>
 #include <map>
 #include <thread>
+#include <vector>
 
 #include "rt_kernels.h"
 
@@ -32,9 +34,9 @@ using namespace rtk;
 #define WF_DESCENT_CAP_DEFAULT 8      // RtOptions.wf_descent_cap
 #define WF_POSTPONE_DEFAULT 32        // RtOptions.wf_postpone
 #define WF_TIMELINE_LAUNCHES 4096     // debug timeline: 3 u64 per trace launch in RtOptions.wave_times_device
-#define WF_WIDE_TAIL_LANES 16         // RtOptions.wf_wide > 0
-#define WF_MAX_PIPES 4                // concurrent pipelines (RtOptions.wf_pipelines)
-#define WF_PIPES_DEFAULT 2
+#define WF_WIDE_TAIL_LANES 32         // RtOptions.wf_wide > 0
+#define WF_MAX_PIPES 3                // concurrent pipelines (RtOptions.wf_pipelines); + the caller's stream = the 4 HW queues
+#define WF_PIPES_DEFAULT 3
 
 struct WfState {
     int *passes_left;
@@ -742,6 +744,7 @@ namespace {
 // tail of one pipeline's trace launches and its finisher overlap the other
 // pipelines' bulk work.  Per-pixel path state is shared (pixels are disjoint).
 struct Pipe {
+    std::vector<std::pair<float, float>> trace_iv; // profiled trace launches: [start, end] ms after the call's start
     WfState st{};
     hipStream_t stream = nullptr;
     uint32_t *host_count = nullptr;
@@ -886,6 +889,7 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
     auto run_pipe = [&](int pi) -> int {
         if (hipSetDevice(dev) != hipSuccess) return -1;
         Pipe &pp = w.pipe[pi];
+        pp.trace_iv.clear();
         WfState &st = pp.st;
         hipStream_t s = pp.stream;
         if (hipStreamWaitEvent(s, w.fork, 0) != hipSuccess) return -1;
@@ -963,6 +967,7 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
                 if (prof) {
                     P.trace_ms += elapsed_ms(pp.ev[4], pp.ev[5]);
                     P.shade_ms += elapsed_ms(pp.ev[5], pp.ev[2]);
+                    pp.trace_iv.emplace_back(elapsed_ms(w.ev0, pp.ev[4]), elapsed_ms(w.ev0, pp.ev[5]));
                 }
                 if (trace_iters) {
                     timespec ts;
@@ -1014,6 +1019,21 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
         }
         if (hipEventRecord(w.ev1, stream) != hipSuccess || hipEventSynchronize(w.ev1) != hipSuccess) return -1;
         P.call_ms = elapsed_ms(w.ev0, w.ev1); // wall time of the call
+        std::vector<std::pair<float, float>> iv; // union of the pipelines' trace launch intervals
+        for (int pi = 0; pi < npipes; ++pi) iv.insert(iv.end(), w.pipe[pi].trace_iv.begin(), w.pipe[pi].trace_iv.end());
+        std::sort(iv.begin(), iv.end());
+        float lo = 0.0f, hi = -1.0f;
+        for (const auto &x : iv) {
+            if (x.first > hi) {
+                if (hi > lo) P.trace_union_ms += hi - lo;
+                lo = x.first;
+                hi = x.second;
+            } else if (x.second > hi) {
+                hi = x.second;
+            }
+        }
+        if (hi > lo) P.trace_union_ms += hi - lo;
+        P.pipelines = npipes;
         w.prof = P;
     }
     return 0;

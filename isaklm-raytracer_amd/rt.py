@@ -61,7 +61,8 @@ class RtOptions(ctypes.Structure):
 class RtProfile(ctypes.Structure):
     _fields_ = [("iterations", ctypes.c_int), ("trace_launches", ctypes.c_int), ("shade_launches", ctypes.c_int),
                 ("finish_launches", ctypes.c_int), ("start_ms", ctypes.c_float), ("trace_ms", ctypes.c_float),
-                ("shade_ms", ctypes.c_float), ("finish_ms", ctypes.c_float), ("call_ms", ctypes.c_float)]
+                ("shade_ms", ctypes.c_float), ("finish_ms", ctypes.c_float), ("call_ms", ctypes.c_float),
+                ("trace_union_ms", ctypes.c_float), ("pipelines", ctypes.c_int)]
 
 
 def last_profile():
