@@ -306,6 +306,11 @@ typedef struct RtOptions {
      * tails and finisher overlap the others' bulk work (0 = default 3, max 3:
      * with the caller's stream that is the 4 hardware queues of a process) */
     int wf_pipelines;
+    /* wavefront: a path deeper than this many bounces (total internal
+     * reflection loops in glass reach 10^4 and more) is handed to a kernel
+     * running beside the pipelines, which finishes it one ray per wave with
+     * all 64 lanes (0 = default 64, < 0 = off) */
+    int wf_long_depth;
 } RtOptions;
 
 /* Per-call kernel timing of the last rt_render on this device with

@@ -19,6 +19,7 @@
 #include <time.h>
 
 #include <algorithm>
+#include <atomic>
 #include <map>
 #include <thread>
 #include <vector>
@@ -35,8 +36,11 @@ using namespace rtk;
 #define WF_POSTPONE_DEFAULT 32        // RtOptions.wf_postpone
 #define WF_TIMELINE_LAUNCHES 4096     // debug timeline: 3 u64 per trace launch in RtOptions.wave_times_device
 #define WF_WIDE_TAIL_LANES 32         // RtOptions.wf_wide > 0
-#define WF_MAX_PIPES 3                // concurrent pipelines (RtOptions.wf_pipelines); + the caller's stream = the 4 HW queues
+#define WF_MAX_PIPES 6                // concurrent pipelines (RtOptions.wf_pipelines); more than 3 need GPU_MAX_HW_QUEUES > 4
 #define WF_PIPES_DEFAULT 3
+#define WF_LONG_DEPTH_DEFAULT 64      // RtOptions.wf_long_depth: paths deeper than this go to wf_long
+#define WF_LONG_BLOCKS 64             // wf_long grid (4 waves each, one path per wave at a time)
+#define WF_LONG_TIMEOUT 60000000000ull // s_memrealtime ticks (100 MHz): 600 s safety net
 
 struct WfState {
     int *passes_left;
@@ -49,6 +53,12 @@ struct WfState {
     uint32_t *counts;  // [0], [1]: queue sizes
     uint2 *spill;      // traversal stack spill
     int spill_threads;
+    // long-path hand-off (wf_long): a path deeper than long_depth leaves its
+    // pipeline for the concurrently running wf_long kernel
+    uint32_t *long_flag;  // per entry: slot + 1 once published (agent-scope store after a release fence)
+    RtF4 *long_ray;       // 2 per entry
+    uint32_t *long_ctr;   // [0] entries reserved, [1] entries claimed, [2] producers done
+    int long_depth;       // 0 = off
 };
 
 namespace {
@@ -71,6 +81,26 @@ __device__ __forceinline__ void enqueue(const WfState &st, int q, bool want, uin
         st.q_slot[q][e] = slot;
         st.q_ray[q][2 * (size_t)e] = RtF4{o.x, o.y, o.z, 0.0f};
         st.q_ray[q][2 * (size_t)e + 1] = RtF4{d.x, d.y, d.z, 0.0f};
+    }
+}
+
+// hand `to_long` lanes' paths (state already stored) to wf_long: reserve an
+// entry, store the ray, drain this wave's stores, release (write back the
+// XCD's L2: MI355X_MICROARCH.md hand-off rules), then publish the entry with
+// an agent-scope store that wf_long polls for
+__device__ __forceinline__ void publish_long(const WfState &st, bool to_long, uint32_t slot, Vec3D o, Vec3D d)
+{
+    uint32_t e = 0;
+    if (to_long) {
+        e = __hip_atomic_fetch_add(st.long_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        st.long_ray[2 * (size_t)e] = RtF4{o.x, o.y, o.z, 0.0f};
+        st.long_ray[2 * (size_t)e + 1] = RtF4{d.x, d.y, d.z, 0.0f};
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (to_long) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(st.long_flag + e, slot + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -578,7 +608,9 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_shade(RtDevScene sc, RtDevFrame f
             want = shade_step<COUNT>(sc, fr, cam, p, __float_as_int(h.x), h.y, h.z, h.w, limit, c);
             store_regs(st, fr, p);
         }
-        enqueue(st, qn, want, p.slot, p.ro, p.rd);
+        const bool to_long = want && st.long_depth > 0 && p.depth > st.long_depth;
+        enqueue(st, qn, want && !to_long, p.slot, p.ro, p.rd);
+        if (__any(to_long)) publish_long(st, to_long, p.slot, p.ro, p.rd);
     }
     if (COUNT) flush_counters(c, fr.counters);
 }
@@ -735,6 +767,94 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_finish_coop(RtDevScene sc, RtDevF
     }
 }
 
+// Long paths (total internal reflection in glass runs to 10^4 bounces and
+// more) would otherwise advance one bounce per queue iteration and then hold
+// up the end of the call in the finisher.  wf_shade hands every path deeper
+// than st.long_depth to this kernel, which runs concurrently with the
+// pipelines for the whole call: each wave claims one published path and runs
+// it to the end of its pixel's passes, every ray traced by all 64 lanes
+// (wide_trace), lane 0 shading.  It exits once the producers are done and
+// every reserved entry has been claimed (or, as a safety net, after
+// WF_LONG_TIMEOUT ticks of s_memrealtime without that).
+template <bool COUNT>
+__global__ void __launch_bounds__(WF_BLOCK) wf_long(RtDevScene sc, RtDevFrame fr, RtDevCamera cam, WfState st)
+{
+    __shared__ WideItem s_wide[(WF_BLOCK / 64) * WIDE_CAP];
+    __shared__ unsigned long long s_key[(WF_BLOCK / 64) * 4];
+    __shared__ int s_mark[WF_BLOCK];
+    const int lane = __lane_id();
+    const int wave = threadIdx.x >> 6;
+    const WideLds W{s_wide + wave * WIDE_CAP, WIDE_CAP, s_key + wave * 4,
+                    reinterpret_cast<float *>(s_key + wave * 4 + 1), s_mark + wave * 64};
+    Cnt c;
+    if (COUNT) c.zero();
+    const int limit = fr.max_depth > 0 ? fr.max_depth : RT_WATCHDOG_BOUNCES;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (true) {
+        // ---- claim the next entry; wait until it is published (or there is none)
+        uint32_t e = 0, flag = 0;
+        int quit = 0;
+        if (lane == 0) {
+            e = __hip_atomic_fetch_add(st.long_ctr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            while (true) {
+                flag = __hip_atomic_load(st.long_flag + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (flag) break;
+                if (__hip_atomic_load(st.long_ctr + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) &&
+                    e >= __hip_atomic_load(st.long_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                    quit = 1; // producers done and this claim is past the last entry
+                    break;
+                }
+                if (__builtin_amdgcn_s_memrealtime() - t0 > WF_LONG_TIMEOUT) {
+                    quit = 1;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(16);
+            }
+            if (!quit) { // acquire: this lane's loads below see the producer's stores
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+        }
+        if (__shfl(quit, 0)) break;
+        e = (uint32_t)__shfl((int)e, 0);
+        flag = (uint32_t)__shfl((int)flag, 0);
+        // ---- run the path (state in lane 0) to the end of its pixel's passes
+        PathRegs p;
+        p.slot = 0;
+        p.ro = p.rd = rt_v3(0, 0, 0);
+        if (lane == 0) {
+            load_regs(st, fr, flag - 1u, p);
+            p.ro = ld3(ldf4(st.long_ray + 2 * (size_t)e));
+            p.rd = ld3(ldf4(st.long_ray + 2 * (size_t)e + 1));
+        }
+        while (true) {
+            CoopRay r;
+            coop_idle(r);
+            if (lane == 0) {
+                if (COUNT) c.v[RT_CNT_RAY]++;
+                coop_begin(sc, r, p.ro, p.rd);
+            }
+            int hit = -1;
+            float bx = 0.0f, by = 0.0f, bz = 0.0f;
+            if (__shfl((int)r.live, 0)) {
+                const Vec3D o = rt_v3(__shfl(r.o.x, 0), __shfl(r.o.y, 0), __shfl(r.o.z, 0));
+                const Vec3D d = rt_v3(__shfl(r.d.x, 0), __shfl(r.d.y, 0), __shfl(r.d.z, 0));
+                wide_trace<COUNT>(sc, o, d, __shfl(r.entry, 0), __shfl(r.exit_, 0), W, lane == 0, hit, bx, by, bz, c);
+            }
+            int want = 0;
+            if (lane == 0) want = shade_step<COUNT>(sc, fr, cam, p, hit, bx, by, bz, limit, c) ? 1 : 0;
+            if (!__shfl(want, 0)) break;
+        }
+        if (lane == 0) store_regs(st, fr, p);
+    }
+    if (COUNT) flush_counters(c, fr.counters);
+}
+
+__global__ void wf_long_done(uint32_t *ctr)
+{
+    if (threadIdx.x == 0) __hip_atomic_store(ctr + 2, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // ---------------------------------------------------------------- launcher
 namespace {
 
@@ -792,6 +912,8 @@ int ensure(Workspace &w, size_t slots, int grid)
     // per pixel
     const size_t o_pl = take(slots * 4), o_fl = take(slots * 4), o_T = take(slots * 12), o_L = take(slots * 12),
                  o_c = take(slots * 12), o_n = take(slots * 12), o_rp = take(slots * 12), o_li = take(slots * 4);
+    // long-path hand-off (shared by the pipelines), wf_long's stack-free wide traversal needs no spill
+    const size_t o_lf = take(slots * 4), o_lr = take(slots * 32), o_lc = take(256);
     // per pipeline (queues sized for every pixel: a pipeline never holds more)
     size_t o_qs0[WF_MAX_PIPES], o_qs1[WF_MAX_PIPES], o_qr0[WF_MAX_PIPES], o_qr1[WF_MAX_PIPES], o_h[WF_MAX_PIPES],
         o_cnt[WF_MAX_PIPES], o_sp[WF_MAX_PIPES];
@@ -827,6 +949,10 @@ int ensure(Workspace &w, size_t slots, int grid)
         st.counts = (uint32_t *)(b + o_cnt[i]);
         st.spill = (uint2 *)(b + o_sp[i]);
         st.spill_threads = (int)spill_threads;
+        st.long_flag = (uint32_t *)(b + o_lf);
+        st.long_ray = (RtF4 *)(b + o_lr);
+        st.long_ctr = (uint32_t *)(b + o_lc);
+        st.long_depth = 0;
     }
     w.slots = slots;
     w.grid = grid;
@@ -853,7 +979,7 @@ extern "C" int rt_last_profile(RtProfile *out)
 
 int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevCamera &cam, hipStream_t stream,
                         int variant, int tail_opt, int finish_waves_opt, int profile, int cap_opt, int postpone_opt,
-                        int wide_opt, int pipes_opt)
+                        int wide_opt, int pipes_opt, int long_opt)
 {
     // 1: wave-cooperative leaves (entries packed as k << 6 | lane: needs < 2^26 entries), 2: static, 3: per-lane fetch
     int trace_kind = variant;
@@ -881,10 +1007,34 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
     // trace launches: once the queue is empty, a wave with at most this many rays left finishes them wide
     const int wide_lanes = wide_opt < 0 ? 0 : (wide_opt > 0 ? (wide_opt > 64 ? 64 : wide_opt) : WF_WIDE_TAIL_LANES);
     static const bool trace_iters = getenv("RT_WF_TRACE_ITERS") != nullptr; // debug: per-iteration queue sizes
+    // paths deeper than this leave their pipeline for wf_long (cooperative trace only)
+    const int long_depth = trace_kind == 1 && long_opt >= 0 ? (long_opt > 0 ? long_opt : WF_LONG_DEPTH_DEFAULT) : 0;
+    for (int pi = 0; pi < WF_MAX_PIPES; ++pi) w.pipe[pi].st.long_depth = long_depth;
+    const WfState &lst = w.pipe[0].st;
 
+    if (long_depth > 0) {
+        if (hipMemsetAsync(lst.long_flag, 0, slots * 4, stream) != hipSuccess) return -1;
+        if (hipMemsetAsync(lst.long_ctr, 0, 256, stream) != hipSuccess) return -1;
+    }
     // fork: every pipeline stream starts after the caller's stream
     if (hipEventRecord(w.fork, stream) != hipSuccess) return -1;
     if (prof && hipEventRecord(w.ev0, stream) != hipSuccess) return -1;
+    if (long_depth > 0) { // runs beside the pipelines until they are done producing
+        if (count) hipLaunchKernelGGL(wf_long<true>, dim3(WF_LONG_BLOCKS), dim3(WF_BLOCK), 0, stream, sc, fr, cam, lst);
+        else hipLaunchKernelGGL(wf_long<false>, dim3(WF_LONG_BLOCKS), dim3(WF_BLOCK), 0, stream, sc, fr, cam, lst);
+        if (hipGetLastError() != hipSuccess) return -1;
+    }
+    std::atomic<int> producing(npipes);
+    bool produced_done[WF_MAX_PIPES] = {};
+    // a pipeline's queue iterations are over: the last one tells wf_long no more paths will come
+    // (called exactly once per pipeline, on error paths too, so that wf_long always ends)
+    auto producer_done = [&](int pi, hipStream_t s) -> int {
+        if (produced_done[pi]) return 0;
+        produced_done[pi] = true;
+        if (producing.fetch_sub(1) != 1 || long_depth <= 0) return 0;
+        hipLaunchKernelGGL(wf_long_done, dim3(1), dim3(64), 0, s, lst.long_ctr);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    };
 
     auto run_pipe = [&](int pi) -> int {
         if (hipSetDevice(dev) != hipSuccess) return -1;
@@ -931,6 +1081,7 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
         int rc = 0;
         if (trace_kind == 1 && tail > slots) {
             // wf_tail above the frame size: the whole call runs in the finisher (no queue iterations)
+            if (producer_done(pi, s) != 0) return -1;
             rc = finish(0, (uint32_t)slots);
         } else {
             for (int it = 0;; ++it) {
@@ -974,9 +1125,9 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
                     clock_gettime(CLOCK_MONOTONIC, &ts);
                     fprintf(stderr, "[wf] pipe %d it %d live %u t %.4f\n", pi, it, live, ts.tv_sec + ts.tv_nsec * 1e-9);
                 }
-                if (live == 0) break;
-                if (live < tail) {
-                    rc = finish(q ^ 1, live);
+                if (live == 0 || live < tail) {
+                    if (producer_done(pi, s) != 0) return -1;
+                    if (live != 0) rc = finish(q ^ 1, live);
                     break;
                 }
             }
@@ -999,6 +1150,8 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
     for (int pi = 1; pi < npipes; ++pi) threads[pi] = std::thread([&, pi] { rcs[pi] = run_pipe(pi); });
     rcs[0] = run_pipe(0);
     for (int pi = 1; pi < npipes; ++pi) threads[pi].join();
+    for (int pi = 0; pi < npipes; ++pi) // a pipeline that failed early must still release wf_long
+        if (!produced_done[pi]) (void)producer_done(pi, w.pipe[pi].stream);
     for (int pi = 0; pi < npipes; ++pi)
         if (rcs[pi] != 0) return rcs[pi];
     // join: the caller's stream continues after every pipeline

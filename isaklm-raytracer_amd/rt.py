@@ -55,7 +55,8 @@ class RtOptions(ctypes.Structure):
                 ("counters_device", ctypes.c_void_p), ("wave_times_device", ctypes.c_void_p),
                 ("wf_tail", ctypes.c_int), ("wf_finish_waves", ctypes.c_int), ("profile", ctypes.c_int),
                 ("wf_descent_cap", ctypes.c_int), ("wf_postpone", ctypes.c_int), ("wf_wide", ctypes.c_int),
-                ("shard_id", ctypes.c_int), ("num_shards", ctypes.c_int), ("wf_pipelines", ctypes.c_int)]
+                ("shard_id", ctypes.c_int), ("num_shards", ctypes.c_int), ("wf_pipelines", ctypes.c_int),
+                ("wf_long_depth", ctypes.c_int)]
 
 
 class RtProfile(ctypes.Structure):
@@ -290,7 +291,7 @@ KERNEL_WAVEFRONT = 1
 
 def options(width, height, passes=1, adaptive=True, min_samples=100, tolerance=0.05, max_depth=0, stream=None,
             counters=None, kernel=KERNEL_MEGA, wf_tail=0, wf_finish_waves=0, profile=False, wf_descent_cap=0,
-            wf_postpone=0, wf_wide=0, shard_id=0, num_shards=1, wave_times=None, wf_pipelines=0):
+            wf_postpone=0, wf_wide=0, shard_id=0, num_shards=1, wave_times=None, wf_pipelines=0, wf_long_depth=0):
     o = RtOptions()
     lib().rt_default_options(ctypes.byref(o))
     o.width, o.height, o.passes = width, height, passes
@@ -303,6 +304,7 @@ def options(width, height, passes=1, adaptive=True, min_samples=100, tolerance=0
     o.shard_id, o.num_shards = shard_id, num_shards
     o.wave_times_device = wave_times
     o.wf_pipelines = wf_pipelines
+    o.wf_long_depth = wf_long_depth
     return o
 
 

@@ -89,6 +89,23 @@ def test_wavefront_finisher_modes(scene, tail, waves, wide):
     assert gcnt == rcnt
 
 
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("scene", ["room_small", "cornell_blob"])
+@pytest.mark.parametrize("long_depth,pipes", [(1, 3), (3, 1), (-1, 2)],
+                         ids=["long-handoff-all", "long-handoff-deep-1-pipe", "no-handoff-2-pipes"])
+def test_wavefront_long_paths_and_pipelines(scene, long_depth, pipes):
+    """Paths handed to wf_long (every path deeper than 1 or 3 bounces, so the
+    cross-kernel hand-off is exercised thousands of times) and the pipeline
+    split leave every accumulator and counter bit-identical."""
+    run = helpers.GpuRun(scene)
+    W, H, P = 48, 27, 3
+    gpu, gcnt, _ = run.render(W, H, P, calls=2, count=True, kernel=rt.KERNEL_WAVEFRONT, wf_long_depth=long_depth,
+                              wf_pipelines=pipes)
+    ref, rcnt = helpers.oracle_render(run.path, W, H, P, calls=2)
+    helpers.assert_bitwise(gpu, ref, what=f"long_depth={long_depth} pipes={pipes}")
+    assert gcnt == rcnt
+
+
 def test_kernels_agree_multi_call(cornell):
     """Megakernel and wavefront give the same bits across calls with reset."""
     W, H = 33, 31

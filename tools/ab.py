@@ -3,7 +3,8 @@ Round r renders the same samples (seeds = mt19937 outputs [r*W*H, (r+1)*W*H))
 for every variant, so the work is identical and only the timing differs.
 
 usage: python tools/ab.py SCENE PASSES MAX_DEPTH ROUNDS VARIANT[,VARIANT...]
-  VARIANT = KERNEL[:WF_TAIL[:WF_FINISH_WAVES[:DESCENT_CAP[:POSTPONE[:WIDE[:PIPES]]]]]]; KERNEL 0 mega, 1 wavefront
+  VARIANT = KERNEL[:WF_TAIL[:WF_FINISH_WAVES[:DESCENT_CAP[:POSTPONE[:WIDE[:PIPES[:LONG_DEPTH]]]]]]]; KERNEL 0 mega,
+            1 wavefront
             (cooperative leaves), 2 wavefront static, 3 wavefront lane fetch
 Prints per-variant Msamples/s (median, min, max) at 1920x1080 and the work
 counters of one counted run.
@@ -27,9 +28,10 @@ def main():
     variants = sys.argv[5].split(",")
 
     def opts(v, **kw):
-        f = [int(x) for x in v.split(":")] + [0, 0, 0, 0, 0, 0]
+        f = [int(x) for x in v.split(":")] + [0, 0, 0, 0, 0, 0, 0]
         return rt.options(W, H, P, adaptive=False, max_depth=maxd, kernel=f[0], wf_tail=f[1], wf_finish_waves=f[2],
-                          wf_descent_cap=f[3], wf_postpone=f[4], wf_wide=f[5], wf_pipelines=f[6], **kw)
+                          wf_descent_cap=f[3], wf_postpone=f[4], wf_wide=f[5], wf_pipelines=f[6],
+                          wf_long_depth=f[7], **kw)
 
     W, H = int(os.environ.get("AB_W", 1920)), int(os.environ.get("AB_H", 1080))
     run = helpers.GpuRun(scene)
