@@ -1152,6 +1152,18 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
     for (int pi = 1; pi < npipes; ++pi) threads[pi].join();
     for (int pi = 0; pi < npipes; ++pi) // a pipeline that failed early must still release wf_long
         if (!produced_done[pi]) (void)producer_done(pi, w.pipe[pi].stream);
+    if (trace_iters) {
+        for (int pi = 0; pi < npipes; ++pi) (void)hipStreamSynchronize(w.pipe[pi].stream);
+        timespec ts;
+        clock_gettime(CLOCK_MONOTONIC, &ts);
+        fprintf(stderr, "[wf] pipelines done t %.4f\n", ts.tv_sec + ts.tv_nsec * 1e-9);
+        uint32_t lc[3] = {};
+        (void)hipStreamSynchronize(stream);
+        (void)hipMemcpy(lc, lst.long_ctr, sizeof lc, hipMemcpyDeviceToHost);
+        clock_gettime(CLOCK_MONOTONIC, &ts);
+        fprintf(stderr, "[wf] long paths %u claimed %u done %u; caller stream done t %.4f\n", lc[0], lc[1], lc[2],
+                ts.tv_sec + ts.tv_nsec * 1e-9);
+    }
     for (int pi = 0; pi < npipes; ++pi)
         if (rcs[pi] != 0) return rcs[pi];
     // join: the caller's stream continues after every pipeline
