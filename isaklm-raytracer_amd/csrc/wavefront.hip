@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <atomic>
 #include <map>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -40,7 +41,7 @@ using namespace rtk;
 #define WF_PIPES_DEFAULT 3
 #define WF_LONG_DEPTH_DEFAULT 64      // RtOptions.wf_long_depth: paths deeper than this go to wf_long
 #define WF_LONG_BLOCKS 64             // wf_long grid (4 waves each, one path per wave at a time)
-#define WF_LONG_TIMEOUT 60000000000ull // s_memrealtime ticks (100 MHz): 600 s safety net
+#define WF_LONG_IDLE 2000000000ull   // s_memrealtime ticks (100 MHz): 20 s without a claim ends a wf_long wave
 
 struct WfState {
     int *passes_left;
@@ -57,7 +58,7 @@ struct WfState {
     // pipeline for the concurrently running wf_long kernel
     uint32_t *long_flag;  // per entry: slot + 1 once published (agent-scope store after a release fence)
     RtF4 *long_ray;       // 2 per entry
-    uint32_t *long_ctr;   // [0] entries reserved, [1] entries claimed, [2] producers done
+    uint32_t *long_ctr;   // [0] entries reserved, [1] entries claimed, [3] paths running in wf_long
     int long_depth;       // 0 = off
 };
 
@@ -87,7 +88,7 @@ __device__ __forceinline__ void enqueue(const WfState &st, int q, bool want, uin
 // hand `to_long` lanes' paths (state already stored) to wf_long: reserve an
 // entry, store the ray, drain this wave's stores, release (write back the
 // XCD's L2: MI355X_MICROARCH.md hand-off rules), then publish the entry with
-// an agent-scope store that wf_long polls for
+// an agent-scope store that wf_long's claims check
 __device__ __forceinline__ void publish_long(const WfState &st, bool to_long, uint32_t slot, Vec3D o, Vec3D d)
 {
     uint32_t e = 0;
@@ -770,14 +771,21 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_finish_coop(RtDevScene sc, RtDevF
 // Long paths (total internal reflection in glass runs to 10^4 bounces and
 // more) would otherwise advance one bounce per queue iteration and then hold
 // up the end of the call in the finisher.  wf_shade hands every path deeper
-// than st.long_depth to this kernel, which runs concurrently with the
-// pipelines for the whole call: each wave claims one published path and runs
-// it to the end of its pixel's passes, every ray traced by all 64 lanes
-// (wide_trace), lane 0 shading.  It exits once the producers are done and
-// every reserved entry has been claimed (or, as a safety net, after
-// WF_LONG_TIMEOUT ticks of s_memrealtime without that).
+// than st.long_depth to this kernel, launched on the caller's stream (idle
+// during the call) in slices beside the pipelines: each wave claims the next
+// PUBLISHED entry in order (compare-and-swap on the claim counter, never an
+// entry whose publication is still in flight) and runs that path to the end
+// of its pixel's passes, every ray traced by all 64 lanes (wide_trace), lane 0
+// shading.  A wave with nothing to claim keeps polling only while another
+// wave of this slice still runs a path (new paths keep arriving meanwhile),
+// then leaves; the host launches the next slice when this one is over.  The
+// slice never waits on work another queue must do, so it cannot deadlock
+// when the runtime maps the caller's stream and a pipeline stream to one
+// hardware queue.  The final slice (every producer done, all entries
+// published) drains what is left.
 template <bool COUNT>
-__global__ void __launch_bounds__(WF_BLOCK) wf_long(RtDevScene sc, RtDevFrame fr, RtDevCamera cam, WfState st)
+__global__ void __launch_bounds__(WF_BLOCK) wf_long(RtDevScene sc, RtDevFrame fr, RtDevCamera cam, WfState st,
+                                                    int final_slice)
 {
     __shared__ WideItem s_wide[(WF_BLOCK / 64) * WIDE_CAP];
     __shared__ unsigned long long s_key[(WF_BLOCK / 64) * 4];
@@ -789,22 +797,31 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_long(RtDevScene sc, RtDevFrame fr
     Cnt c;
     if (COUNT) c.zero();
     const int limit = fr.max_depth > 0 ? fr.max_depth : RT_WATCHDOG_BOUNCES;
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t *const reserved = st.long_ctr, *const claimed = st.long_ctr + 1, *const running = st.long_ctr + 3;
+    unsigned long long t_idle = __builtin_amdgcn_s_memrealtime();
     while (true) {
-        // ---- claim the next entry; wait until it is published (or there is none)
+        // ---- claim the next published entry (lane 0)
         uint32_t e = 0, flag = 0;
         int quit = 0;
         if (lane == 0) {
-            e = __hip_atomic_fetch_add(st.long_ctr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             while (true) {
-                flag = __hip_atomic_load(st.long_flag + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (flag) break;
-                if (__hip_atomic_load(st.long_ctr + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) &&
-                    e >= __hip_atomic_load(st.long_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                    quit = 1; // producers done and this claim is past the last entry
-                    break;
+                e = __hip_atomic_load(claimed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t r = __hip_atomic_load(reserved, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                flag = e < r ? __hip_atomic_load(st.long_flag + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+                if (flag) {
+                    uint32_t expect = e;
+                    if (__hip_atomic_compare_exchange_strong(claimed, &expect, e + 1u, __ATOMIC_RELAXED,
+                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                        __hip_atomic_fetch_add(running, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        break;
+                    }
+                    continue; // another wave took it: try the next one
                 }
-                if (__builtin_amdgcn_s_memrealtime() - t0 > WF_LONG_TIMEOUT) {
+                // nothing claimable now.  Final slice: done once every entry is claimed.  Otherwise wait
+                // only while a path of this slice is still running.  Safety net: WF_LONG_IDLE ticks idle.
+                const bool others = __hip_atomic_load(running, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+                if ((final_slice ? e >= r : !others) ||
+                    __builtin_amdgcn_s_memrealtime() - t_idle > WF_LONG_IDLE) {
                     quit = 1;
                     break;
                 }
@@ -845,14 +862,13 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_long(RtDevScene sc, RtDevFrame fr
             if (lane == 0) want = shade_step<COUNT>(sc, fr, cam, p, hit, bx, by, bz, limit, c) ? 1 : 0;
             if (!__shfl(want, 0)) break;
         }
-        if (lane == 0) store_regs(st, fr, p);
+        if (lane == 0) {
+            store_regs(st, fr, p);
+            __hip_atomic_fetch_sub(running, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        t_idle = __builtin_amdgcn_s_memrealtime();
     }
     if (COUNT) flush_counters(c, fr.counters);
-}
-
-__global__ void wf_long_done(uint32_t *ctr)
-{
-    if (threadIdx.x == 0) __hip_atomic_store(ctr + 2, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ---------------------------------------------------------------- launcher
@@ -880,6 +896,7 @@ struct Workspace {
     Pipe pipe[WF_MAX_PIPES];
     bool streams_ok = false;
     hipEvent_t fork = nullptr, ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t long_ev = nullptr; // after the last wf_long slice on the caller's stream
     RtProfile prof{};        // last profiled call
 };
 
@@ -889,6 +906,7 @@ int ensure(Workspace &w, size_t slots, int grid)
 {
     if (!w.streams_ok) {
         if (hipEventCreateWithFlags(&w.fork, hipEventDisableTiming) != hipSuccess) return -1;
+        if (hipEventCreateWithFlags(&w.long_ev, hipEventDisableTiming) != hipSuccess) return -1;
         if (hipEventCreate(&w.ev0) != hipSuccess || hipEventCreate(&w.ev1) != hipSuccess) return -1;
         for (Pipe &p : w.pipe) {
             if (hipStreamCreateWithFlags(&p.stream, hipStreamNonBlocking) != hipSuccess) return -1;
@@ -1019,21 +1037,38 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
     // fork: every pipeline stream starts after the caller's stream
     if (hipEventRecord(w.fork, stream) != hipSuccess) return -1;
     if (prof && hipEventRecord(w.ev0, stream) != hipSuccess) return -1;
-    if (long_depth > 0) { // runs beside the pipelines until they are done producing
-        if (count) hipLaunchKernelGGL(wf_long<true>, dim3(WF_LONG_BLOCKS), dim3(WF_BLOCK), 0, stream, sc, fr, cam, lst);
-        else hipLaunchKernelGGL(wf_long<false>, dim3(WF_LONG_BLOCKS), dim3(WF_BLOCK), 0, stream, sc, fr, cam, lst);
+    std::mutex long_mu;
+    bool long_final = false;
+    // launches a wf_long slice on the caller's stream unless the previous one
+    // is still running; the final slice (every producer done) is queued after it
+    auto kick_long = [&](bool final) -> int {
+        if (long_depth <= 0) return 0;
+        std::lock_guard<std::mutex> g(long_mu);
+        if (long_final) return 0;
+        if (!final) {
+            const hipError_t q = hipEventQuery(w.long_ev);
+            if (q == hipErrorNotReady) return 0;
+            if (q != hipSuccess) return -1;
+        }
+        const int fin = final ? 1 : 0;
+        if (count)
+            hipLaunchKernelGGL(wf_long<true>, dim3(WF_LONG_BLOCKS), dim3(WF_BLOCK), 0, stream, sc, fr, cam, lst, fin);
+        else
+            hipLaunchKernelGGL(wf_long<false>, dim3(WF_LONG_BLOCKS), dim3(WF_BLOCK), 0, stream, sc, fr, cam, lst, fin);
         if (hipGetLastError() != hipSuccess) return -1;
-    }
+        long_final = final;
+        return hipEventRecord(w.long_ev, stream) == hipSuccess ? 0 : -1;
+    };
     std::atomic<int> producing(npipes);
     bool produced_done[WF_MAX_PIPES] = {};
-    // a pipeline's queue iterations are over: the last one tells wf_long no more paths will come
-    // (called exactly once per pipeline, on error paths too, so that wf_long always ends)
-    auto producer_done = [&](int pi, hipStream_t s) -> int {
+    // a pipeline's queue iterations are over (every shade launch that could
+    // publish has completed: the host read its queue size): the last one
+    // queues the final wf_long slice
+    auto producer_done = [&](int pi) -> int {
         if (produced_done[pi]) return 0;
         produced_done[pi] = true;
-        if (producing.fetch_sub(1) != 1 || long_depth <= 0) return 0;
-        hipLaunchKernelGGL(wf_long_done, dim3(1), dim3(64), 0, s, lst.long_ctr);
-        return hipGetLastError() == hipSuccess ? 0 : -1;
+        if (producing.fetch_sub(1) != 1) return 0;
+        return kick_long(true);
     };
 
     auto run_pipe = [&](int pi) -> int {
@@ -1081,7 +1116,7 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
         int rc = 0;
         if (trace_kind == 1 && tail > slots) {
             // wf_tail above the frame size: the whole call runs in the finisher (no queue iterations)
-            if (producer_done(pi, s) != 0) return -1;
+            if (producer_done(pi) != 0) return -1;
             rc = finish(0, (uint32_t)slots);
         } else {
             for (int it = 0;; ++it) {
@@ -1125,8 +1160,9 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
                     clock_gettime(CLOCK_MONOTONIC, &ts);
                     fprintf(stderr, "[wf] pipe %d it %d live %u t %.4f\n", pi, it, live, ts.tv_sec + ts.tv_nsec * 1e-9);
                 }
+                if (kick_long(false) != 0) return -1; // paths published by this shade launch
                 if (live == 0 || live < tail) {
-                    if (producer_done(pi, s) != 0) return -1;
+                    if (producer_done(pi) != 0) return -1;
                     if (live != 0) rc = finish(q ^ 1, live);
                     break;
                 }
@@ -1150,18 +1186,17 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
     for (int pi = 1; pi < npipes; ++pi) threads[pi] = std::thread([&, pi] { rcs[pi] = run_pipe(pi); });
     rcs[0] = run_pipe(0);
     for (int pi = 1; pi < npipes; ++pi) threads[pi].join();
-    for (int pi = 0; pi < npipes; ++pi) // a pipeline that failed early must still release wf_long
-        if (!produced_done[pi]) (void)producer_done(pi, w.pipe[pi].stream);
+    if (!long_final) (void)kick_long(true); // a pipeline failed early: drain the published paths anyway
     if (trace_iters) {
         for (int pi = 0; pi < npipes; ++pi) (void)hipStreamSynchronize(w.pipe[pi].stream);
         timespec ts;
         clock_gettime(CLOCK_MONOTONIC, &ts);
         fprintf(stderr, "[wf] pipelines done t %.4f\n", ts.tv_sec + ts.tv_nsec * 1e-9);
-        uint32_t lc[3] = {};
+        uint32_t lc[4] = {};
         (void)hipStreamSynchronize(stream);
         (void)hipMemcpy(lc, lst.long_ctr, sizeof lc, hipMemcpyDeviceToHost);
         clock_gettime(CLOCK_MONOTONIC, &ts);
-        fprintf(stderr, "[wf] long paths %u claimed %u done %u; caller stream done t %.4f\n", lc[0], lc[1], lc[2],
+        fprintf(stderr, "[wf] long paths %u claimed %u running %u; caller stream done t %.4f\n", lc[0], lc[1], lc[3],
                 ts.tv_sec + ts.tv_nsec * 1e-9);
     }
     for (int pi = 0; pi < npipes; ++pi)

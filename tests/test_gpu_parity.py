@@ -3,6 +3,8 @@ same seeds, for both kernel variants (megakernel, wavefront).  The bar is
 bit-exact accumulators (fb, sq, count, RNG state) and equal work counters;
 north_star's 1e-4 relative L-infinity is asserted too.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -104,6 +106,21 @@ def test_wavefront_long_paths_and_pipelines(scene, long_depth, pipes):
     ref, rcnt = helpers.oracle_render(run.path, W, H, P, calls=2)
     helpers.assert_bitwise(gpu, ref, what=f"long_depth={long_depth} pipes={pipes}")
     assert gcnt == rcnt
+
+
+@pytest.mark.timeout(180)
+def test_long_handoff_with_shared_hw_queues():
+    """The wf_long slices run on the caller's stream beside the pipeline
+    streams.  With the process's hardware queues taken by other streams first
+    (RCCL's, in a multi-GPU bench) the runtime maps several streams onto one
+    queue: the slices must not wait on work queued behind them.  Runs in a
+    child process (fresh stream-to-queue mapping), bounded by a timeout."""
+    import subprocess
+    import sys
+
+    child = os.path.join(os.path.dirname(os.path.abspath(__file__)), "queue_sharing_child.py")
+    r = subprocess.run([sys.executable, child, "8"], capture_output=True, text=True, timeout=150)
+    assert r.returncode == 0 and "OK" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
 
 
 def test_kernels_agree_multi_call(cornell):
