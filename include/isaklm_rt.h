@@ -152,6 +152,20 @@ static_assert(sizeof(Camera) == 28 && offsetof(Camera, FOV) == 20, "Camera");
 const char *rt_last_error(void);
 const char *rt_version(void);
 
+/* ---------------- texture decoding ----------------
+ * stbi_load(path, &w, &h, &n, 4) as make_texture (rt/scene.cuh:25-63) calls
+ * it: RGBA8 rows in file order (no flip).  PNG (all colour types / depths,
+ * Adam7, tRNS) and baseline / extended-sequential JPEG, bit-identical to
+ * stb_image v2.28; other formats and progressive JPEG -> RT_E_UNSUPPORTED.
+ * The pixels are a host array (rt_host_free).  rt_host_scene_load_mesh decodes
+ * a material's `texture` with it, and rt_create_scene uploads each texture
+ * with width + 1 zero texels after the image: mod(uv, 1) can return 1.0, so
+ * sample_texture's index reaches width*height + width.  Callers
+ * of rt_scene_prepare_host that supply their own device texels should pad
+ * them the same way. */
+int rt_decode_image(const char *path, uint8_t **rgba_out, int *width, int *height);
+int rt_decode_image_memory(const void *data, size_t size, uint8_t **rgba_out, int *width, int *height);
+
 /* ---------------- device memory (hipMalloc/hipMemcpy stand-ins) ---------------- */
 int rt_device_alloc(void **ptr_device, size_t bytes);
 int rt_free(void *ptr_device);
@@ -159,6 +173,9 @@ int rt_upload(void *dst_device, const void *src_host, size_t bytes);
 int rt_download(void *dst_host, const void *src_device, size_t bytes);
 int rt_memset(void *dst_device, int value, size_t bytes);
 int rt_device_count(int *count);
+/* selects the device for the calling thread and creates the wavefront
+ * pipelines' streams there (call it before other GPU users of the process,
+ * e.g. RCCL, take the hardware queues) */
 int rt_set_device(int device);
 int rt_synchronize(void);
 void rt_host_free(void *ptr_host);  /* frees host arrays returned by this library */

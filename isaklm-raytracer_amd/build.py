@@ -19,7 +19,7 @@ ROOT = os.path.dirname(HERE)
 INCLUDE = os.path.join(ROOT, "include")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
-HOST_SOURCES = ["host/mesh_loading.cpp", "host/kd_build.cpp", "host/scene_prepare.cpp", "host/misc.cpp",
+HOST_SOURCES = ["host/mesh_loading.cpp", "host/kd_build.cpp", "host/scene_prepare.cpp", "host/misc.cpp", "host/image_decode.cpp",
                 "host/scenes.cpp"]
 HIP_SOURCES = ["path_kernel.hip", "wavefront.hip", "abi.hip", "shards.hip"]
 # every header under csrc/ (a header missing here would not trigger a rebuild)

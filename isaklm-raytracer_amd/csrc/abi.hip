@@ -10,6 +10,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -21,6 +23,8 @@ int rt_launch_tonemap(const Vec3D *fb, const int *count, RtUChar4 *out, int n, h
 int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevCamera &cam, hipStream_t stream,
                         int variant, int tail, int finish_waves, int profile, int cap, int postpone, int wide,
                         int pipes, int long_depth);
+
+int rt_wavefront_device_init();
 
 static thread_local std::string g_error;
 
@@ -155,6 +159,10 @@ int rt_device_count(int *count)
 int rt_set_device(int device)
 {
     HIPCHK(hipSetDevice(device));
+    if (rt_wavefront_device_init() != 0) { // the pipelines' streams take their hardware queues first
+        rt_set_error("rt_set_device: wavefront streams: %s", hipGetErrorString(hipGetLastError()));
+        return RT_E_HIP;
+    }
     return RT_OK;
 }
 int rt_synchronize(void)
@@ -163,6 +171,46 @@ int rt_synchronize(void)
     return RT_OK;
 }
 void rt_host_free(void *p) { free(p); }
+
+// ---------------- texture decoding (make_texture's stbi_load, rt/scene.cuh:33) ----------------
+static int decode_out(int rc, const std::vector<uint8_t> &rgba, const std::string &err, int w, int h,
+                      uint8_t **rgba_out, int *width, int *height)
+{
+    if (rc != RT_OK) {
+        rt_set_error("rt_decode_image: %s", err.c_str());
+        return rc;
+    }
+    uint8_t *p = (uint8_t *)malloc(rgba.size() ? rgba.size() : 1);
+    if (!p) { rt_set_error("rt_decode_image: out of host memory"); return RT_E_NOMEM; }
+    memcpy(p, rgba.data(), rgba.size());
+    *rgba_out = p;
+    *width = w;
+    *height = h;
+    return RT_OK;
+}
+
+int rt_decode_image(const char *path, uint8_t **rgba_out, int *width, int *height)
+{
+    if (!path || !rgba_out || !width || !height) { rt_set_error("rt_decode_image: null argument"); return RT_E_INVALID; }
+    std::vector<uint8_t> rgba;
+    std::string err;
+    int w = 0, h = 0;
+    const int rc = rt_host::decode_image_file(path, rgba, w, h, err);
+    return decode_out(rc, rgba, err, w, h, rgba_out, width, height);
+}
+
+int rt_decode_image_memory(const void *data, size_t size, uint8_t **rgba_out, int *width, int *height)
+{
+    if (!data || !rgba_out || !width || !height) {
+        rt_set_error("rt_decode_image_memory: null argument");
+        return RT_E_INVALID;
+    }
+    std::vector<uint8_t> rgba;
+    std::string err;
+    int w = 0, h = 0;
+    const int rc = rt_host::decode_image_memory((const uint8_t *)data, size, rgba, w, h, err);
+    return decode_out(rc, rgba, err, w, h, rgba_out, width, height);
+}
 
 // ---------------- G_Buffer ----------------
 int rt_gbuffer_seeds(uint32_t *out, size_t count, uint64_t skip)
@@ -254,6 +302,10 @@ int rt_build_kd_tree(const Triangle *tris, int n, KD_Tree_Node **nodes_out, int 
 }
 
 // create_scene (rt/create_scene.cuh:18-73)
+// device textures uploaded by rt_create_scene, per device triangle array (freed by rt_destroy_scene)
+static std::mutex g_tex_mu;
+static std::map<const void *, std::vector<void *>> g_scene_textures;
+
 int rt_create_scene(const RtHostScene *s, Scene *out, int *node_count, int *index_count)
 {
     if (!s || !out || s->tris.empty()) { rt_set_error("rt_create_scene: bad arguments"); return RT_E_INVALID; }
@@ -266,7 +318,36 @@ int rt_create_scene(const RtHostScene *s, Scene *out, int *node_count, int *inde
     if (rc) return rc;
     std::vector<int> lights = rt_host::light_list(s->tris.data(), n);
     HIPCHK(hipMalloc((void **)&out->triangles, (size_t)n * sizeof(Triangle)));
-    HIPCHK(hipMemcpy(out->triangles, s->tris.data(), (size_t)n * sizeof(Triangle), hipMemcpyHostToDevice));
+    if (s->textures.empty()) {
+        HIPCHK(hipMemcpy(out->triangles, s->tris.data(), (size_t)n * sizeof(Triangle), hipMemcpyHostToDevice));
+    } else {
+        // make_texture's cudaMalloc/cudaMemcpy (rt/scene.cuh:58-59): one device
+        // copy per decoded texture (with its zero pad), triangles re-pointed to it
+        std::map<const void *, RtUChar4 *> dev;
+        std::vector<void *> owned;
+        for (const auto &t : s->textures) {
+            RtUChar4 *d = nullptr;
+            const size_t bytes = t->texels.size() * sizeof(RtUChar4);
+            HIPCHK(hipMalloc((void **)&d, bytes));
+            owned.push_back(d);
+            HIPCHK(hipMemcpy(d, t->texels.data(), bytes, hipMemcpyHostToDevice));
+            dev[t->texels.data()] = d;
+        }
+        std::vector<Triangle> tris(s->tris);
+        for (Triangle &t : tris)
+            if (t.material.texture.buffer) {
+                auto it = dev.find(t.material.texture.buffer);
+                if (it == dev.end()) {
+                    rt_set_error("rt_create_scene: triangle texture not owned by the host scene");
+                    for (void *d : owned) (void)hipFree(d);
+                    return RT_E_INVALID;
+                }
+                t.material.texture.buffer = it->second;
+            }
+        HIPCHK(hipMemcpy(out->triangles, tris.data(), (size_t)n * sizeof(Triangle), hipMemcpyHostToDevice));
+        std::lock_guard<std::mutex> g(g_tex_mu);
+        g_scene_textures[out->triangles] = owned;
+    }
     out->triangle_count = n;
     HIPCHK(hipMalloc((void **)&out->light_indicies, (lights.size() + 1) * sizeof(int)));
     if (!lights.empty())
@@ -286,6 +367,14 @@ int rt_create_scene(const RtHostScene *s, Scene *out, int *node_count, int *inde
 int rt_destroy_scene(Scene *s)
 {
     if (!s) return RT_E_INVALID;
+    {
+        std::lock_guard<std::mutex> g(g_tex_mu);
+        auto it = g_scene_textures.find(s->triangles);
+        if (it != g_scene_textures.end()) {
+            for (void *d : it->second) (void)hipFree(d);
+            g_scene_textures.erase(it);
+        }
+    }
     (void)hipFree(s->triangles);
     (void)hipFree(s->light_indicies);
     (void)hipFree(s->kd_tree.nodes);

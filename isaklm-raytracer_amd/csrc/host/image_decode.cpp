@@ -1,0 +1,1187 @@
+// image_decode.cpp — texture decoding for make_texture (rt/scene.cuh:25-63).
+//
+// The reference decodes its textures with stb_image v2.28
+// (rt/stb_image/stb_image.h, third-party, vendored in the reference) through
+// stbi_load(path, &w, &h, &n, 4): RGBA8, row 0 = the file's first row (no
+// vertical flip: stbi_set_flip_vertically_on_load is commented out at
+// rt/scene.cuh:27).  This file restates the two formats the reference's
+// textures use, with stb's output semantics:
+//
+//  * PNG (every colour type and bit depth, Adam7, tRNS, PLTE): lossless, so
+//    any correct decoder agrees; stb's channel conversions are kept (grey ->
+//    g,g,g,255; low bit depth grey scaled by 0xff/0x55/0x11; 16 -> 8 bit by
+//    v >> 8; tRNS colour key -> alpha 0).  Inflate is written here (RFC 1951);
+//    like stb, the zlib Adler-32 and the chunk CRCs are not verified.
+//  * JPEG, baseline and extended-sequential Huffman (SOF0/SOF1): the
+//    arithmetic follows stb's pipeline, because a JPEG decoder's output is
+//    defined by its IDCT, upsampler and colour conversion: dequantise into
+//    16-bit coefficients, the jidctint-derived integer IDCT with 12-bit
+//    constants (stb_image.h:2439-2540; its SSE2 twin is bit-identical),
+//    "fancy" upsampling for h2v1 / h1v2 / h2v2 (:3487-3550) and nearest for
+//    other ratios (:3668), the reduced-precision fixed-point YCbCr->RGB
+//    (:3679-3705), Adobe/JFIF/'RGB' colour-space rules and CMYK/YCCK via the
+//    8x8 "blinn" product (:3881-4040).  Progressive JPEG (SOF2) is reported
+//    as unsupported.
+//
+// Pinned against stb_image itself: tests/test_textures.py compares every
+// texture the reference ships plus synthetic PNG/JPEG variants with
+// oracle/_ref/libstb_ref.so (stb_image.cpp compiled from the reference's own
+// source by oracle/Makefile.ref), and the committed digests in
+// tests/golden/textures/ carry that to machines without the reference.
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "rt_host.h"
+
+namespace {
+
+// ============================================================== inflate
+struct BitIn {
+    const uint8_t *p;
+    size_t n, pos = 0;
+    uint32_t buf = 0;
+    int cnt = 0;
+    bool bad = false;
+    int bits(int need)
+    {
+        while (cnt < need) {
+            if (pos >= n) {
+                bad = true;
+                return 0;
+            }
+            buf |= (uint32_t)p[pos++] << cnt;
+            cnt += 8;
+        }
+        const int v = (int)(buf & ((1u << need) - 1u));
+        buf >>= need;
+        cnt -= need;
+        return v;
+    }
+};
+
+// canonical Huffman code: counts per length, symbols ordered by code, and a
+// 9-bit first-level table (bit-reversed code -> symbol | length << 9)
+struct Huff {
+    uint16_t count[16];
+    uint16_t symbol[320];
+    uint16_t fast[512];
+};
+
+// returns false for an over-subscribed code (incomplete codes are allowed, as
+// zlib allows a single distance code)
+bool huff_build(Huff &h, const uint8_t *len, int n)
+{
+    memset(h.count, 0, sizeof h.count);
+    for (int s = 0; s < n; ++s) h.count[len[s]]++;
+    if (h.count[0] == n) { // no codes
+        memset(h.fast, 0, sizeof h.fast);
+        return true;
+    }
+    int left = 1;
+    for (int l = 1; l < 16; ++l) {
+        left <<= 1;
+        left -= h.count[l];
+        if (left < 0) return false;
+    }
+    uint16_t offs[16];
+    offs[1] = 0;
+    for (int l = 1; l < 15; ++l) offs[l + 1] = offs[l] + h.count[l];
+    for (int s = 0; s < n; ++s)
+        if (len[s]) h.symbol[offs[len[s]]++] = (uint16_t)s;
+    // first-level table
+    memset(h.fast, 0, sizeof h.fast);
+    int code = 0, first = 0, index = 0;
+    for (int l = 1; l <= 9; ++l) {
+        for (int k = 0; k < h.count[l]; ++k) {
+            const int c = code + k; // canonical code of length l, MSB first
+            int rev = 0;
+            for (int b = 0; b < l; ++b) rev |= ((c >> b) & 1) << (l - 1 - b);
+            for (int fill = rev; fill < 512; fill += 1 << l)
+                h.fast[fill] = (uint16_t)(h.symbol[index + k] | (l << 9));
+        }
+        index += h.count[l];
+        first += h.count[l];
+        code = (code + h.count[l]) << 1;
+    }
+    (void)first;
+    return true;
+}
+
+int huff_decode(BitIn &in, const Huff &h)
+{
+    // fast path: 9 bits available without running past the input
+    while (in.cnt < 9 && in.pos < in.n) {
+        in.buf |= (uint32_t)in.p[in.pos++] << in.cnt;
+        in.cnt += 8;
+    }
+    if (in.cnt >= 9) {
+        const uint16_t e = h.fast[in.buf & 511u];
+        if (e) {
+            const int l = e >> 9;
+            in.buf >>= l;
+            in.cnt -= l;
+            return e & 511;
+        }
+    }
+    // slow path (puff): one bit at a time, MSB-first code
+    int code = 0, first = 0, index = 0;
+    for (int l = 1; l < 16; ++l) {
+        code |= in.bits(1);
+        if (in.bad) return -1;
+        const int count = h.count[l];
+        if (code - count < first) return h.symbol[index + (code - first)];
+        index += count;
+        first += count;
+        first <<= 1;
+        code <<= 1;
+    }
+    return -1;
+}
+
+const uint16_t kLenBase[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
+                               31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
+const uint8_t kLenExtra[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
+const uint16_t kDistBase[30] = {1,   2,   3,   4,   5,   7,    9,    13,   17,   25,   33,   49,   65,    97,    129,
+                                193, 257, 385, 513, 769, 1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
+const uint8_t kDistExtra[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
+
+bool inflate_codes(BitIn &in, std::vector<uint8_t> &out, const Huff &lit, const Huff &dist)
+{
+    while (true) {
+        int s = huff_decode(in, lit);
+        if (s < 0) return false;
+        if (s < 256) {
+            out.push_back((uint8_t)s);
+        } else if (s == 256) {
+            return true;
+        } else {
+            s -= 257;
+            if (s >= 29) return false;
+            const int len = kLenBase[s] + in.bits(kLenExtra[s]);
+            const int d = huff_decode(in, dist);
+            if (d < 0 || d >= 30) return false;
+            const size_t back = (size_t)kDistBase[d] + (size_t)in.bits(kDistExtra[d]);
+            if (in.bad || back > out.size()) return false;
+            const size_t from = out.size() - back;
+            for (int k = 0; k < len; ++k) out.push_back(out[from + k]);
+        }
+    }
+}
+
+// zlib stream (RFC 1950 header, RFC 1951 data) -> bytes; false on a malformed stream
+bool zlib_inflate(const uint8_t *p, size_t n, std::vector<uint8_t> &out, std::string &err)
+{
+    if (n < 2) { err = "zlib stream too short"; return false; }
+    const int cmf = p[0], flg = p[1];
+    if ((cmf * 256 + flg) % 31 != 0) { err = "bad zlib header"; return false; }
+    if (flg & 32) { err = "zlib preset dictionary"; return false; }
+    if ((cmf & 15) != 8) { err = "bad zlib compression method"; return false; }
+    BitIn in{p, n, 2};
+    Huff lit, dist;
+    struct Fixed {
+        Huff lit, dist;
+        Fixed()
+        {
+            uint8_t l[288];
+            for (int i = 0; i < 144; ++i) l[i] = 8;
+            for (int i = 144; i < 256; ++i) l[i] = 9;
+            for (int i = 256; i < 280; ++i) l[i] = 7;
+            for (int i = 280; i < 288; ++i) l[i] = 8;
+            huff_build(lit, l, 288);
+            for (int i = 0; i < 30; ++i) l[i] = 5;
+            huff_build(dist, l, 30);
+        }
+    };
+    static const Fixed fixed; // thread-safe static initialisation
+    const Huff &fixed_lit = fixed.lit, &fixed_dist = fixed.dist;
+    int last = 0;
+    do {
+        last = in.bits(1);
+        const int type = in.bits(2);
+        if (in.bad) { err = "truncated zlib stream"; return false; }
+        if (type == 0) { // stored
+            // byte align: drop the partial byte, give back whole bytes the decoder read ahead
+            in.pos -= (size_t)(in.cnt >> 3);
+            in.buf = 0;
+            in.cnt = 0;
+            if (in.pos + 4 > n) { err = "truncated stored block"; return false; }
+            const unsigned len = p[in.pos] | (p[in.pos + 1] << 8), nlen = p[in.pos + 2] | (p[in.pos + 3] << 8);
+            in.pos += 4;
+            if ((len ^ 0xffffu) != nlen) { err = "corrupt stored block"; return false; }
+            if (in.pos + len > n) { err = "truncated stored block"; return false; }
+            out.insert(out.end(), p + in.pos, p + in.pos + len);
+            in.pos += len;
+        } else if (type == 1) {
+            if (!inflate_codes(in, out, fixed_lit, fixed_dist)) { err = "corrupt zlib data"; return false; }
+        } else if (type == 2) {
+            const int nlen = in.bits(5) + 257, ndist = in.bits(5) + 1, ncode = in.bits(4) + 4;
+            if (in.bad || nlen > 286 || ndist > 30) { err = "bad dynamic block"; return false; }
+            static const uint8_t order[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+            uint8_t lengths[320] = {};
+            for (int i = 0; i < ncode; ++i) lengths[order[i]] = (uint8_t)in.bits(3);
+            Huff lencode;
+            if (in.bad || !huff_build(lencode, lengths, 19)) { err = "bad code lengths"; return false; }
+            uint8_t ll[320] = {};
+            int k = 0;
+            while (k < nlen + ndist) {
+                int s = huff_decode(in, lencode);
+                if (s < 0) { err = "bad code lengths"; return false; }
+                if (s < 16) {
+                    ll[k++] = (uint8_t)s;
+                } else {
+                    int rep = 0;
+                    uint8_t v = 0;
+                    if (s == 16) {
+                        if (k == 0) { err = "bad code lengths"; return false; }
+                        v = ll[k - 1];
+                        rep = 3 + in.bits(2);
+                    } else if (s == 17) {
+                        rep = 3 + in.bits(3);
+                    } else {
+                        rep = 11 + in.bits(7);
+                    }
+                    if (in.bad || k + rep > nlen + ndist) { err = "bad code lengths"; return false; }
+                    while (rep--) ll[k++] = v;
+                }
+            }
+            if (ll[256] == 0) { err = "no end-of-block code"; return false; }
+            if (!huff_build(lit, ll, nlen) || !huff_build(dist, ll + nlen, ndist)) {
+                err = "bad huffman lengths";
+                return false;
+            }
+            if (!inflate_codes(in, out, lit, dist)) { err = "corrupt zlib data"; return false; }
+        } else {
+            err = "bad zlib block type";
+            return false;
+        }
+    } while (!last);
+    return true;
+}
+
+// ================================================================ PNG
+uint32_t be32(const uint8_t *p) { return (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3]; }
+
+int paeth(int a, int b, int c)
+{
+    const int p = a + b - c, pa = p > a ? p - a : a - p, pb = p > b ? p - b : b - p, pc = p > c ? p - c : c - p;
+    if (pa <= pb && pa <= pc) return a;
+    if (pb <= pc) return b;
+    return c;
+}
+
+// unfilter one (sub)image: raw -> samples as bytes per row (stride = row bytes)
+bool png_unfilter(const uint8_t *raw, size_t raw_n, size_t &used, int w, int h, int channels, int depth,
+                  std::vector<uint8_t> &rows, size_t &stride)
+{
+    const size_t bits_per_px = (size_t)channels * depth;
+    stride = ((size_t)w * bits_per_px + 7) / 8;
+    const int bpp = (int)((bits_per_px + 7) / 8); // filter byte distance (>= 1)
+    rows.assign(stride * h, 0);
+    if (w == 0 || h == 0) {
+        used = 0;
+        return true;
+    }
+    if (raw_n < (stride + 1) * h) return false;
+    const uint8_t *prior = nullptr;
+    for (int y = 0; y < h; ++y) {
+        const uint8_t *in = raw + (stride + 1) * y;
+        const int f = in[0];
+        ++in;
+        uint8_t *cur = &rows[stride * y];
+        for (size_t i = 0; i < stride; ++i) {
+            const int a = i >= (size_t)bpp ? cur[i - bpp] : 0;
+            const int b = prior ? prior[i] : 0;
+            const int c = prior && i >= (size_t)bpp ? prior[i - bpp] : 0;
+            int v = in[i];
+            switch (f) {
+            case 0: break;
+            case 1: v += a; break;
+            case 2: v += b; break;
+            case 3: v += (a + b) >> 1; break;
+            case 4: v += paeth(a, b, c); break;
+            default: return false;
+            }
+            cur[i] = (uint8_t)v;
+        }
+        prior = cur;
+    }
+    used = (stride + 1) * h;
+    return true;
+}
+
+// sample k of a packed row (depth 1, 2, 4, 8 or 16)
+inline int sample_at(const uint8_t *row, size_t k, int depth)
+{
+    switch (depth) {
+    case 16: return row[2 * k] << 8 | row[2 * k + 1];
+    case 8: return row[k];
+    default: {
+        const size_t bit = k * depth;
+        return (row[bit >> 3] >> (8 - depth - (int)(bit & 7))) & ((1 << depth) - 1);
+    }
+    }
+}
+
+int png_decode(const uint8_t *p, size_t n, std::vector<uint8_t> &rgba, int &w, int &h, std::string &err)
+{
+    static const uint8_t sig[8] = {137, 80, 78, 71, 13, 10, 26, 10};
+    if (n < 8 || memcmp(p, sig, 8) != 0) { err = "not a PNG"; return RT_E_PARSE; }
+    size_t pos = 8;
+    bool have_hdr = false, have_plte = false, have_trns = false;
+    int depth = 0, color = 0, interlace = 0;
+    uint8_t pal[256][4];
+    int pal_n = 0;
+    int tc[3] = {0, 0, 0}; // tRNS colour key (grey or RGB), in sample units
+    std::vector<uint8_t> idat;
+    bool ended = false;
+    while (!ended) {
+        if (pos + 8 > n) { err = "truncated PNG"; return RT_E_PARSE; }
+        const uint32_t len = be32(p + pos), type = be32(p + pos + 4);
+        const uint8_t *d = p + pos + 8;
+        if (len > n || pos + 12 + (size_t)len > n) { err = "truncated PNG chunk"; return RT_E_PARSE; }
+        pos += 12 + (size_t)len;
+        switch (type) {
+        case 0x49484452: // IHDR
+            if (have_hdr || len != 13) { err = "bad IHDR"; return RT_E_PARSE; }
+            have_hdr = true;
+            w = (int)be32(d);
+            h = (int)be32(d + 4);
+            depth = d[8];
+            color = d[9];
+            interlace = d[12];
+            if (be32(d) > (1u << 24) || be32(d + 4) > (1u << 24) || w <= 0 || h <= 0) {
+                err = "bad PNG dimensions";
+                return RT_E_PARSE;
+            }
+            if (d[10] != 0 || d[11] != 0 || interlace > 1) { err = "bad IHDR methods"; return RT_E_PARSE; }
+            if (!(depth == 1 || depth == 2 || depth == 4 || depth == 8 || depth == 16) ||
+                !(color == 0 || color == 2 || color == 3 || color == 4 || color == 6) ||
+                (color == 3 && depth == 16) || (color != 0 && color != 3 && depth < 8)) {
+                err = "bad PNG colour type / bit depth";
+                return RT_E_PARSE;
+            }
+            break;
+        case 0x504C5445: // PLTE
+            if (!have_hdr || len > 768 || len % 3) { err = "bad PLTE"; return RT_E_PARSE; }
+            pal_n = (int)(len / 3);
+            for (int i = 0; i < pal_n; ++i) {
+                pal[i][0] = d[3 * i];
+                pal[i][1] = d[3 * i + 1];
+                pal[i][2] = d[3 * i + 2];
+                pal[i][3] = 255;
+            }
+            have_plte = true;
+            break;
+        case 0x74524E53: // tRNS
+            if (!have_hdr || !idat.empty()) { err = "tRNS after IDAT"; return RT_E_PARSE; }
+            if (color == 3) {
+                if (!have_plte || (int)len > pal_n || len == 0) { err = "bad tRNS"; return RT_E_PARSE; }
+                for (uint32_t i = 0; i < len; ++i) pal[i][3] = d[i];
+            } else if (color == 0 || color == 2) {
+                const uint32_t k = color == 0 ? 1 : 3;
+                if (len != 2 * k) { err = "bad tRNS length"; return RT_E_PARSE; }
+                for (uint32_t i = 0; i < k; ++i) tc[i] = depth == 16 ? (d[2 * i] << 8 | d[2 * i + 1]) : d[2 * i + 1];
+            } else {
+                err = "tRNS with alpha";
+                return RT_E_PARSE;
+            }
+            have_trns = true;
+            break;
+        case 0x49444154: // IDAT
+            if (!have_hdr || (color == 3 && !have_plte)) { err = "IDAT before IHDR/PLTE"; return RT_E_PARSE; }
+            idat.insert(idat.end(), d, d + len);
+            break;
+        case 0x49454E44: // IEND
+            ended = true;
+            break;
+        case 0x43674249: // CgBI (Apple's non-standard PNG)
+            err = "CgBI PNG not supported";
+            return RT_E_UNSUPPORTED;
+        default:
+            if (!(type & (1u << 29))) { // unknown critical chunk
+                err = "unknown critical PNG chunk";
+                return RT_E_PARSE;
+            }
+            break;
+        }
+    }
+    if (!have_hdr || idat.empty()) { err = "PNG without image data"; return RT_E_PARSE; }
+    std::vector<uint8_t> raw;
+    if (!zlib_inflate(idat.data(), idat.size(), raw, err)) return RT_E_PARSE;
+    const int channels = color == 0 ? 1 : color == 2 ? 3 : color == 3 ? 1 : color == 4 ? 2 : 4;
+    rgba.assign((size_t)w * h * 4, 0);
+    // pass geometry (Adam7 or one pass)
+    static const int ax[7] = {0, 4, 0, 2, 0, 1, 0}, ay[7] = {0, 0, 4, 0, 2, 0, 1};
+    static const int sx[7] = {8, 8, 4, 4, 2, 2, 1}, sy[7] = {8, 8, 8, 4, 4, 2, 2};
+    const int passes = interlace ? 7 : 1;
+    // grey scale-up of low bit depths (stbi__depth_scale_table)
+    const int scale = depth == 1 ? 0xff : depth == 2 ? 0x55 : depth == 4 ? 0x11 : 1;
+    size_t off = 0;
+    std::vector<uint8_t> rows;
+    for (int ps = 0; ps < passes; ++ps) {
+        const int pw = interlace ? (w - ax[ps] + sx[ps] - 1) / sx[ps] : w;
+        const int ph = interlace ? (h - ay[ps] + sy[ps] - 1) / sy[ps] : h;
+        if (pw <= 0 || ph <= 0) continue;
+        size_t used = 0, stride = 0;
+        if (!png_unfilter(raw.data() + off, raw.size() - off, used, pw, ph, channels, depth, rows, stride)) {
+            err = "corrupt PNG image data";
+            return RT_E_PARSE;
+        }
+        off += used;
+        for (int y = 0; y < ph; ++y) {
+            const uint8_t *row = &rows[stride * y];
+            const int oy = interlace ? ay[ps] + y * sy[ps] : y;
+            for (int x = 0; x < pw; ++x) {
+                const int ox = interlace ? ax[ps] + x * sx[ps] : x;
+                uint8_t *o = &rgba[((size_t)oy * w + ox) * 4];
+                int s[4] = {0, 0, 0, 0};
+                for (int c = 0; c < channels; ++c) s[c] = sample_at(row, (size_t)x * channels + c, depth);
+                // 16 -> 8 bits: v >> 8 (stbi__convert_16_to_8); the colour key compares full samples
+                auto to8 = [&](int v) { return depth == 16 ? v >> 8 : depth < 8 ? v * scale : v; };
+                switch (color) {
+                case 0: { // grey
+                    const uint8_t g = (uint8_t)to8(s[0]);
+                    o[0] = o[1] = o[2] = g;
+                    o[3] = have_trns && s[0] == tc[0] ? 0 : 255;
+                    break;
+                }
+                case 2: // RGB
+                    o[0] = (uint8_t)to8(s[0]);
+                    o[1] = (uint8_t)to8(s[1]);
+                    o[2] = (uint8_t)to8(s[2]);
+                    o[3] = have_trns && s[0] == tc[0] && s[1] == tc[1] && s[2] == tc[2] ? 0 : 255;
+                    break;
+                case 3: { // palette (indices are not scaled); out-of-range index -> error like stb
+                    if (s[0] >= pal_n) { err = "PNG palette index out of range"; return RT_E_PARSE; }
+                    memcpy(o, pal[s[0]], 4);
+                    break;
+                }
+                case 4: // grey + alpha
+                    o[0] = o[1] = o[2] = (uint8_t)to8(s[0]);
+                    o[3] = (uint8_t)to8(s[1]);
+                    break;
+                default: // RGBA
+                    for (int c = 0; c < 4; ++c) o[c] = (uint8_t)to8(s[c]);
+                    break;
+                }
+            }
+        }
+    }
+    return RT_OK;
+}
+
+// =============================================================== JPEG
+const uint8_t kDezigzag[64 + 15] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,  12, 19, 26, 33,
+                                    40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36,
+                                    29, 22, 15, 23, 30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54,
+                                    47, 55, 62, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63};
+
+struct JHuff { // JPEG F.2.2.3 decoding tables
+    uint8_t size[257];
+    uint16_t code[256];
+    uint8_t values[256];
+    uint32_t maxcode[18];
+    int delta[17];
+    bool ok = false;
+};
+
+bool jhuff_build(JHuff &h, const int *count)
+{
+    int k = 0;
+    for (int i = 0; i < 16; ++i)
+        for (int j = 0; j < count[i]; ++j) {
+            h.size[k++] = (uint8_t)(i + 1);
+            if (k >= 257) return false;
+        }
+    h.size[k] = 0;
+    unsigned code = 0;
+    k = 0;
+    int j;
+    for (j = 1; j <= 16; ++j) {
+        h.delta[j] = k - (int)code;
+        if (h.size[k] == j) {
+            while (h.size[k] == j) h.code[k++] = (uint16_t)(code++);
+            if (code - 1 >= (1u << j)) return false;
+        }
+        h.maxcode[j] = code << (16 - j);
+        code <<= 1;
+    }
+    h.maxcode[j] = 0xffffffffu;
+    h.ok = true;
+    return true;
+}
+
+struct JComp {
+    int id, h, v, tq, hd, ha, dc_pred;
+    int x, y, w2, h2;
+    std::vector<uint8_t> data;
+};
+
+struct Jpeg {
+    const uint8_t *p;
+    size_t n, pos = 0;
+    bool eof() const { return pos >= n; }
+    int get8() { return pos < n ? p[pos++] : 0; }
+    int get16() { const int a = get8(); return a << 8 | get8(); }
+    void skip(int k) { pos = k < 0 ? n : (pos + (size_t)k > n ? n : pos + k); }
+
+    JHuff hdc[4], hac[4];
+    uint16_t dequant[4][64];
+    JComp comp[4];
+    int img_x = 0, img_y = 0, img_n = 0, h_max = 1, v_max = 1, mcu_x = 0, mcu_y = 0;
+    int scan_n = 0, order[4] = {0, 0, 0, 0};
+    int restart_interval = 0, todo = 0;
+    int jfif = 0, app14 = -1, rgb = 0, progressive = 0;
+    uint32_t code_buffer = 0;
+    int code_bits = 0;
+    int marker = 0xff; // none
+    bool nomore = false;
+    std::string err;
+
+    // entropy-coded bytes: 0xFF00 stuffing; a marker ends the data (zeros after it)
+    void grow()
+    {
+        do {
+            unsigned b = nomore ? 0 : (unsigned)get8();
+            if (b == 0xff) {
+                int c = get8();
+                while (c == 0xff) c = get8();
+                if (c != 0) {
+                    marker = c;
+                    nomore = true;
+                    return;
+                }
+            }
+            code_buffer |= b << (24 - code_bits);
+            code_bits += 8;
+        } while (code_bits <= 24);
+    }
+    int huff_decode(const JHuff &h)
+    {
+        if (code_bits < 16) grow();
+        // the code length is the shortest k whose (preshifted) limit exceeds the next 16 bits
+        const uint32_t temp = code_buffer >> 16;
+        int k;
+        for (k = 1; k <= 16; ++k)
+            if (temp < h.maxcode[k]) break;
+        if (k == 17) {
+            code_bits -= 16;
+            return -1;
+        }
+        if (k > code_bits) return -1;
+        const int c = (int)((code_buffer >> (32 - k)) & ((1u << k) - 1u)) + h.delta[k];
+        if (c < 0 || c >= 256) return -1;
+        code_bits -= k;
+        code_buffer <<= k;
+        return h.values[c];
+    }
+    int extend_receive(int nb)
+    {
+        if (code_bits < nb) grow();
+        if (code_bits < nb) return 0;
+        const int sgn = (int)(code_buffer >> 31);
+        uint32_t k = (code_buffer << nb) | (code_buffer >> ((32 - nb) & 31));
+        const uint32_t mask = (1u << nb) - 1u;
+        code_buffer = k & ~mask;
+        k &= mask;
+        code_bits -= nb;
+        static const int bias[16] = {0,    -1,   -3,    -7,    -15,   -31,    -63,    -127,
+                                     -255, -511, -1023, -2047, -4095, -8191, -16383, -32767};
+        return (int)k + (bias[nb] & (sgn - 1));
+    }
+    void reset()
+    {
+        code_bits = 0;
+        code_buffer = 0;
+        nomore = false;
+        for (auto &c : comp) c.dc_pred = 0;
+        marker = 0xff;
+        todo = restart_interval ? restart_interval : 0x7fffffff;
+    }
+    int get_marker()
+    {
+        if (marker != 0xff) {
+            const int x = marker;
+            marker = 0xff;
+            return x;
+        }
+        int x = get8();
+        if (x != 0xff) return 0xff;
+        while (x == 0xff) x = get8();
+        return x;
+    }
+    bool fail(const char *m)
+    {
+        err = m;
+        return false;
+    }
+    bool decode_block(short *data, int b);
+    bool process_marker(int m);
+    bool frame_header();
+    bool scan_header();
+    bool entropy_data();
+};
+
+inline bool add_ok(int a, int b) { return (b < 0) ? a >= INT32_MIN - b : a <= INT32_MAX - b; }
+inline bool mul_short_ok(int a, int b)
+{
+    if (b == 0 || a == 0) return true;
+    const long long v = (long long)a * b;
+    return v >= -32768 && v <= 32767;
+}
+
+bool Jpeg::decode_block(short *data, int b)
+{
+    JComp &c = comp[b];
+    const JHuff &hd = hdc[c.hd], &ha = hac[c.ha];
+    const uint16_t *dq = dequant[c.tq];
+    if (!hd.ok || !ha.ok) return fail("missing Huffman table");
+    if (code_bits < 16) grow();
+    const int t = huff_decode(hd);
+    if (t < 0 || t > 15) return fail("bad huffman code");
+    memset(data, 0, 64 * sizeof(short));
+    const int diff = t ? extend_receive(t) : 0;
+    if (!add_ok(c.dc_pred, diff)) return fail("bad delta");
+    const int dc = c.dc_pred + diff;
+    c.dc_pred = dc;
+    if (!mul_short_ok(dc, dq[0])) return fail("can't merge dc and ac");
+    data[0] = (short)(dc * dq[0]);
+    int k = 1;
+    do {
+        const int rs = huff_decode(ha);
+        if (rs < 0) return fail("bad huffman code");
+        const int s = rs & 15, r = rs >> 4;
+        if (s == 0) {
+            if (rs != 0xf0) break; // end of block
+            k += 16;
+        } else {
+            k += r;
+            const int zig = kDezigzag[k++];
+            data[zig] = (short)(extend_receive(s) * dq[zig]);
+        }
+    } while (k < 64);
+    return true;
+}
+
+// stb's IDCT (jidctint-derived, 12-bit fixed-point constants)
+inline int f2f(double x) { return (int)(x * 4096 + 0.5); }
+inline uint8_t clamp255(int x) { return (unsigned)x > 255 ? (x < 0 ? 0 : 255) : (uint8_t)x; }
+
+struct Idct1 {
+    int t0, t1, t2, t3, x0, x1, x2, x3;
+    Idct1(int s0, int s1, int s2, int s3, int s4, int s5, int s6, int s7)
+    {
+        int p1, p2, p3, p4, p5;
+        p2 = s2;
+        p3 = s6;
+        p1 = (p2 + p3) * f2f(0.5411961f);
+        t2 = p1 + p3 * f2f(-1.847759065f);
+        t3 = p1 + p2 * f2f(0.765366865f);
+        p2 = s0;
+        p3 = s4;
+        t0 = (p2 + p3) * 4096;
+        t1 = (p2 - p3) * 4096;
+        x0 = t0 + t3;
+        x3 = t0 - t3;
+        x1 = t1 + t2;
+        x2 = t1 - t2;
+        t0 = s7;
+        t1 = s5;
+        t2 = s3;
+        t3 = s1;
+        p3 = t0 + t2;
+        p4 = t1 + t3;
+        p1 = t0 + t3;
+        p2 = t1 + t2;
+        p5 = (p3 + p4) * f2f(1.175875602f);
+        t0 = t0 * f2f(0.298631336f);
+        t1 = t1 * f2f(2.053119869f);
+        t2 = t2 * f2f(3.072711026f);
+        t3 = t3 * f2f(1.501321110f);
+        p1 = p5 + p1 * f2f(-0.899976223f);
+        p2 = p5 + p2 * f2f(-2.562915447f);
+        p3 = p3 * f2f(-1.961570560f);
+        p4 = p4 * f2f(-0.390180644f);
+        t3 += p1 + p4;
+        t2 += p2 + p3;
+        t1 += p2 + p4;
+        t0 += p1 + p3;
+    }
+};
+
+void idct_block(uint8_t *out, int stride, const short *d)
+{
+    int val[64];
+    for (int i = 0; i < 8; ++i) {
+        const short *c = d + i;
+        int *v = val + i;
+        if (c[8] == 0 && c[16] == 0 && c[24] == 0 && c[32] == 0 && c[40] == 0 && c[48] == 0 && c[56] == 0) {
+            const int dc = c[0] * 4;
+            for (int r = 0; r < 8; ++r) v[8 * r] = dc;
+        } else {
+            Idct1 k(c[0], c[8], c[16], c[24], c[32], c[40], c[48], c[56]);
+            k.x0 += 512;
+            k.x1 += 512;
+            k.x2 += 512;
+            k.x3 += 512;
+            v[0] = (k.x0 + k.t3) >> 10;
+            v[56] = (k.x0 - k.t3) >> 10;
+            v[8] = (k.x1 + k.t2) >> 10;
+            v[48] = (k.x1 - k.t2) >> 10;
+            v[16] = (k.x2 + k.t1) >> 10;
+            v[40] = (k.x2 - k.t1) >> 10;
+            v[24] = (k.x3 + k.t0) >> 10;
+            v[32] = (k.x3 - k.t0) >> 10;
+        }
+    }
+    for (int i = 0; i < 8; ++i) {
+        const int *v = val + 8 * i;
+        uint8_t *o = out + stride * i;
+        Idct1 k(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]);
+        const int bias = 65536 + (128 << 17);
+        k.x0 += bias;
+        k.x1 += bias;
+        k.x2 += bias;
+        k.x3 += bias;
+        o[0] = clamp255((k.x0 + k.t3) >> 17);
+        o[7] = clamp255((k.x0 - k.t3) >> 17);
+        o[1] = clamp255((k.x1 + k.t2) >> 17);
+        o[6] = clamp255((k.x1 - k.t2) >> 17);
+        o[2] = clamp255((k.x2 + k.t1) >> 17);
+        o[5] = clamp255((k.x2 - k.t1) >> 17);
+        o[3] = clamp255((k.x3 + k.t0) >> 17);
+        o[4] = clamp255((k.x3 - k.t0) >> 17);
+    }
+}
+
+bool Jpeg::process_marker(int m)
+{
+    int L;
+    switch (m) {
+    case 0xff: return fail("expected marker");
+    case 0xDD:
+        if (get16() != 4) return fail("bad DRI len");
+        restart_interval = get16();
+        return true;
+    case 0xDB:
+        L = get16() - 2;
+        while (L > 0) {
+            const int q = get8(), pr = q >> 4, t = q & 15;
+            if (pr != 0 && pr != 1) return fail("bad DQT type");
+            if (t > 3) return fail("bad DQT table");
+            for (int i = 0; i < 64; ++i) dequant[t][kDezigzag[i]] = (uint16_t)(pr ? get16() : get8());
+            L -= pr ? 129 : 65;
+        }
+        return L == 0 ? true : fail("bad DQT len");
+    case 0xC4:
+        L = get16() - 2;
+        while (L > 0) {
+            int sizes[16], cnt = 0;
+            const int q = get8(), tc = q >> 4, th = q & 15;
+            if (tc > 1 || th > 3) return fail("bad DHT header");
+            for (int i = 0; i < 16; ++i) {
+                sizes[i] = get8();
+                cnt += sizes[i];
+            }
+            if (cnt > 256) return fail("bad DHT header");
+            L -= 17;
+            JHuff &h = tc == 0 ? hdc[th] : hac[th];
+            if (!jhuff_build(h, sizes)) return fail("bad code lengths");
+            for (int i = 0; i < cnt; ++i) h.values[i] = (uint8_t)get8();
+            L -= cnt;
+        }
+        return L == 0 ? true : fail("bad DHT len");
+    }
+    if ((m >= 0xE0 && m <= 0xEF) || m == 0xFE) {
+        L = get16();
+        if (L < 2) return fail(m == 0xFE ? "bad COM len" : "bad APP len");
+        L -= 2;
+        if (m == 0xE0 && L >= 5) {
+            static const uint8_t tag[5] = {'J', 'F', 'I', 'F', 0};
+            bool ok = true;
+            for (int i = 0; i < 5; ++i)
+                if (get8() != tag[i]) ok = false;
+            L -= 5;
+            if (ok) jfif = 1;
+        } else if (m == 0xEE && L >= 12) {
+            static const uint8_t tag[6] = {'A', 'd', 'o', 'b', 'e', 0};
+            bool ok = true;
+            for (int i = 0; i < 6; ++i)
+                if (get8() != tag[i]) ok = false;
+            L -= 6;
+            if (ok) {
+                get8();
+                get16();
+                get16();
+                app14 = get8();
+                L -= 6;
+            }
+        }
+        skip(L);
+        return true;
+    }
+    return fail("unknown marker");
+}
+
+bool Jpeg::frame_header()
+{
+    const int Lf = get16();
+    if (Lf < 11) return fail("bad SOF len");
+    if (get8() != 8) return fail("only 8-bit JPEG supported");
+    img_y = get16();
+    if (img_y == 0) return fail("JPEG without height");
+    img_x = get16();
+    if (img_x == 0) return fail("0 width");
+    if (img_x > (1 << 24) || img_y > (1 << 24)) return fail("too large");
+    const int c = get8();
+    if (c != 3 && c != 1 && c != 4) return fail("bad component count");
+    img_n = c;
+    if (Lf != 8 + 3 * img_n) return fail("bad SOF len");
+    rgb = 0;
+    static const uint8_t rgbid[3] = {'R', 'G', 'B'};
+    for (int i = 0; i < img_n; ++i) {
+        comp[i].id = get8();
+        if (img_n == 3 && comp[i].id == rgbid[i]) ++rgb;
+        const int q = get8();
+        comp[i].h = q >> 4;
+        if (!comp[i].h || comp[i].h > 4) return fail("bad H");
+        comp[i].v = q & 15;
+        if (!comp[i].v || comp[i].v > 4) return fail("bad V");
+        comp[i].tq = get8();
+        if (comp[i].tq > 3) return fail("bad TQ");
+    }
+    h_max = v_max = 1;
+    for (int i = 0; i < img_n; ++i) {
+        if (comp[i].h > h_max) h_max = comp[i].h;
+        if (comp[i].v > v_max) v_max = comp[i].v;
+    }
+    for (int i = 0; i < img_n; ++i)
+        if (h_max % comp[i].h || v_max % comp[i].v) return fail("bad H/V");
+    mcu_x = (img_x + h_max * 8 - 1) / (h_max * 8);
+    mcu_y = (img_y + v_max * 8 - 1) / (v_max * 8);
+    for (int i = 0; i < img_n; ++i) {
+        JComp &k = comp[i];
+        k.x = (img_x * k.h + h_max - 1) / h_max;
+        k.y = (img_y * k.v + v_max - 1) / v_max;
+        k.w2 = mcu_x * k.h * 8;
+        k.h2 = mcu_y * k.v * 8;
+        k.data.assign((size_t)k.w2 * k.h2, 0);
+    }
+    return true;
+}
+
+bool Jpeg::scan_header()
+{
+    const int Ls = get16();
+    scan_n = get8();
+    if (scan_n < 1 || scan_n > 4 || scan_n > img_n) return fail("bad SOS component count");
+    if (Ls != 6 + 2 * scan_n) return fail("bad SOS len");
+    for (int i = 0; i < scan_n; ++i) {
+        const int id = get8(), q = get8();
+        int which;
+        for (which = 0; which < img_n; ++which)
+            if (comp[which].id == id) break;
+        if (which == img_n) return fail("SOS component not in frame");
+        comp[which].hd = q >> 4;
+        if (comp[which].hd > 3) return fail("bad DC huff");
+        comp[which].ha = q & 15;
+        if (comp[which].ha > 3) return fail("bad AC huff");
+        order[i] = which;
+    }
+    const int ss = get8();
+    get8(); // spectral end (63 for sequential)
+    const int aa = get8();
+    if (ss != 0 || aa != 0) return fail("bad SOS");
+    return true;
+}
+
+bool Jpeg::entropy_data()
+{
+    reset();
+    short data[64];
+    if (scan_n == 1) {
+        const int nn = order[0];
+        JComp &c = comp[nn];
+        const int w = (c.x + 7) >> 3, h = (c.y + 7) >> 3;
+        for (int j = 0; j < h; ++j)
+            for (int i = 0; i < w; ++i) {
+                if (!decode_block(data, nn)) return false;
+                idct_block(c.data.data() + (size_t)c.w2 * j * 8 + i * 8, c.w2, data);
+                if (--todo <= 0) {
+                    if (code_bits < 24) grow();
+                    if (!(marker >= 0xd0 && marker <= 0xd7)) return true;
+                    reset();
+                }
+            }
+        return true;
+    }
+    for (int j = 0; j < mcu_y; ++j)
+        for (int i = 0; i < mcu_x; ++i) {
+            for (int k = 0; k < scan_n; ++k) {
+                const int nn = order[k];
+                JComp &c = comp[nn];
+                for (int y = 0; y < c.v; ++y)
+                    for (int x = 0; x < c.h; ++x) {
+                        const int x2 = (i * c.h + x) * 8, y2 = (j * c.v + y) * 8;
+                        if (!decode_block(data, nn)) return false;
+                        idct_block(c.data.data() + (size_t)c.w2 * y2 + x2, c.w2, data);
+                    }
+            }
+            if (--todo <= 0) {
+                if (code_bits < 24) grow();
+                if (!(marker >= 0xd0 && marker <= 0xd7)) return true;
+                reset();
+            }
+        }
+    return true;
+}
+
+// ---- upsampling (one output row from the component's near/far rows)
+inline uint8_t div4(int x) { return (uint8_t)(x >> 2); }
+inline uint8_t div16(int x) { return (uint8_t)(x >> 4); }
+
+const uint8_t *resample(int hs, int vs, uint8_t *out, const uint8_t *in_near, const uint8_t *in_far, int w)
+{
+    if (hs == 1 && vs == 1) return in_near;
+    if (hs == 1 && vs == 2) {
+        for (int i = 0; i < w; ++i) out[i] = div4(3 * in_near[i] + in_far[i] + 2);
+        return out;
+    }
+    if (hs == 2 && vs == 1) {
+        const uint8_t *in = in_near;
+        if (w == 1) {
+            out[0] = out[1] = in[0];
+            return out;
+        }
+        out[0] = in[0];
+        out[1] = div4(in[0] * 3 + in[1] + 2);
+        int i;
+        for (i = 1; i < w - 1; ++i) {
+            const int n = 3 * in[i] + 2;
+            out[i * 2] = div4(n + in[i - 1]);
+            out[i * 2 + 1] = div4(n + in[i + 1]);
+        }
+        out[i * 2] = div4(in[w - 2] * 3 + in[w - 1] + 2);
+        out[i * 2 + 1] = in[w - 1];
+        return out;
+    }
+    if (hs == 2 && vs == 2) {
+        if (w == 1) {
+            out[0] = out[1] = div4(3 * in_near[0] + in_far[0] + 2);
+            return out;
+        }
+        int t1 = 3 * in_near[0] + in_far[0];
+        out[0] = div4(t1 + 2);
+        for (int i = 1; i < w; ++i) {
+            const int t0 = t1;
+            t1 = 3 * in_near[i] + in_far[i];
+            out[i * 2 - 1] = div16(3 * t0 + t1 + 8);
+            out[i * 2] = div16(3 * t1 + t0 + 8);
+        }
+        out[w * 2 - 1] = div4(t1 + 2);
+        return out;
+    }
+    for (int i = 0; i < w; ++i) // nearest neighbour for other ratios
+        for (int j = 0; j < hs; ++j) out[i * hs + j] = in_near[i];
+    return out;
+}
+
+inline int float2fixed(float x) { return ((int)(x * 4096.0f + 0.5f)) << 8; }
+
+void ycbcr_to_rgba(uint8_t *out, const uint8_t *y, const uint8_t *pcb, const uint8_t *pcr, int count)
+{
+    for (int i = 0; i < count; ++i, out += 4) {
+        const int y_fixed = (y[i] << 20) + (1 << 19);
+        const int cr = pcr[i] - 128, cb = pcb[i] - 128;
+        int r = y_fixed + cr * float2fixed(1.40200f);
+        int g = y_fixed + (cr * -float2fixed(0.71414f)) + ((cb * -float2fixed(0.34414f)) & (int)0xffff0000);
+        int b = y_fixed + cb * float2fixed(1.77200f);
+        r >>= 20;
+        g >>= 20;
+        b >>= 20;
+        out[0] = clamp255(r);
+        out[1] = clamp255(g);
+        out[2] = clamp255(b);
+        out[3] = 255;
+    }
+}
+
+inline uint8_t blinn8(uint8_t x, uint8_t y)
+{
+    const unsigned t = (unsigned)x * y + 128;
+    return (uint8_t)((t + (t >> 8)) >> 8);
+}
+
+int jpeg_decode(const uint8_t *p, size_t n, std::vector<uint8_t> &rgba, int &w, int &h, std::string &err)
+{
+    Jpeg j;
+    j.p = p;
+    j.n = n;
+    memset(j.dequant, 0, sizeof j.dequant);
+    for (auto &c : j.comp) c = JComp{};
+    auto bad = [&](const std::string &m) {
+        err = m.empty() ? "corrupt JPEG" : m;
+        return RT_E_PARSE;
+    };
+    if (j.get_marker() != 0xD8) return bad("no SOI");
+    int m = j.get_marker();
+    while (!(m == 0xC0 || m == 0xC1 || m == 0xC2)) {
+        if (!j.process_marker(m)) return bad(j.err);
+        m = j.get_marker();
+        while (m == 0xff) {
+            if (j.eof()) return bad("no SOF");
+            m = j.get_marker();
+        }
+    }
+    if (m == 0xC2) {
+        err = "progressive JPEG not supported";
+        return RT_E_UNSUPPORTED;
+    }
+    if (!j.frame_header()) return bad(j.err);
+    m = j.get_marker();
+    while (m != 0xD9) {
+        if (m == 0xDA) {
+            if (!j.scan_header() || !j.entropy_data()) return bad(j.err);
+            if (j.marker == 0xff) { // skip junk up to the next marker
+                int found = 0xff;
+                while (!j.eof()) {
+                    int x = j.get8();
+                    bool done = false;
+                    while (x == 255) {
+                        if (j.eof()) { done = true; break; }
+                        x = j.get8();
+                        if (x != 0x00 && x != 0xff) {
+                            found = x;
+                            done = true;
+                            break;
+                        }
+                    }
+                    if (done) break;
+                }
+                j.marker = found;
+            }
+            m = j.get_marker();
+            if (m >= 0xd0 && m <= 0xd7) m = j.get_marker();
+        } else if (m == 0xDC) {
+            const int Ld = j.get16();
+            const int NL = j.get16();
+            if (Ld != 4) return bad("bad DNL len");
+            if (NL != j.img_y) return bad("bad DNL height");
+            m = j.get_marker();
+        } else {
+            if (!j.process_marker(m)) break; // stb stops here and keeps what it decoded
+            m = j.get_marker();
+        }
+    }
+    // ---- resample + colour convert to RGBA (load_jpeg_image, n = 4)
+    const int is_rgb = j.img_n == 3 && (j.rgb == 3 || (j.app14 == 0 && !j.jfif));
+    const int decode_n = j.img_n;
+    struct Res { int hs, vs, ystep, w_lores, ypos; const uint8_t *line0, *line1; std::vector<uint8_t> buf; } res[4];
+    for (int k = 0; k < decode_n; ++k) {
+        Res &r = res[k];
+        r.buf.assign((size_t)j.img_x + 3, 0);
+        r.hs = j.h_max / j.comp[k].h;
+        r.vs = j.v_max / j.comp[k].v;
+        r.ystep = r.vs >> 1;
+        r.w_lores = (j.img_x + r.hs - 1) / r.hs;
+        r.ypos = 0;
+        r.line0 = r.line1 = j.comp[k].data.data();
+    }
+    w = j.img_x;
+    h = j.img_y;
+    rgba.assign((size_t)w * h * 4, 0);
+    const uint8_t *co[4] = {nullptr, nullptr, nullptr, nullptr};
+    for (int y = 0; y < h; ++y) {
+        uint8_t *out = &rgba[(size_t)w * 4 * y];
+        for (int k = 0; k < decode_n; ++k) {
+            Res &r = res[k];
+            const bool y_bot = r.ystep >= (r.vs >> 1);
+            co[k] = resample(r.hs, r.vs, r.buf.data(), y_bot ? r.line1 : r.line0, y_bot ? r.line0 : r.line1,
+                             r.w_lores);
+            if (++r.ystep >= r.vs) {
+                r.ystep = 0;
+                r.line0 = r.line1;
+                if (++r.ypos < j.comp[k].y) r.line1 += j.comp[k].w2;
+            }
+        }
+        if (j.img_n == 3) {
+            if (is_rgb) {
+                for (int i = 0; i < w; ++i, out += 4) {
+                    out[0] = co[0][i];
+                    out[1] = co[1][i];
+                    out[2] = co[2][i];
+                    out[3] = 255;
+                }
+            } else {
+                ycbcr_to_rgba(out, co[0], co[1], co[2], w);
+            }
+        } else if (j.img_n == 4) {
+            if (j.app14 == 0) { // CMYK
+                for (int i = 0; i < w; ++i, out += 4) {
+                    const uint8_t mm = co[3][i];
+                    out[0] = blinn8(co[0][i], mm);
+                    out[1] = blinn8(co[1][i], mm);
+                    out[2] = blinn8(co[2][i], mm);
+                    out[3] = 255;
+                }
+            } else if (j.app14 == 2) { // YCCK
+                ycbcr_to_rgba(out, co[0], co[1], co[2], w);
+                for (int i = 0; i < w; ++i, out += 4) {
+                    const uint8_t mm = co[3][i];
+                    out[0] = blinn8(255 - out[0], mm);
+                    out[1] = blinn8(255 - out[1], mm);
+                    out[2] = blinn8(255 - out[2], mm);
+                }
+            } else {
+                ycbcr_to_rgba(out, co[0], co[1], co[2], w);
+            }
+        } else {
+            for (int i = 0; i < w; ++i, out += 4) {
+                out[0] = out[1] = out[2] = co[0][i];
+                out[3] = 255;
+            }
+        }
+    }
+    return RT_OK;
+}
+
+} // namespace
+
+namespace rt_host {
+
+int decode_image_memory(const uint8_t *data, size_t size, std::vector<uint8_t> &rgba, int &width, int &height,
+                        std::string &err)
+{
+    width = height = 0;
+    if (!data || size < 4) {
+        err = "empty image";
+        return RT_E_PARSE;
+    }
+    if (data[0] == 137 && data[1] == 'P' && data[2] == 'N' && data[3] == 'G')
+        return png_decode(data, size, rgba, width, height, err);
+    if (data[0] == 0xFF && data[1] == 0xD8) return jpeg_decode(data, size, rgba, width, height, err);
+    err = "unsupported image format (PNG and JPEG are decoded)";
+    return RT_E_UNSUPPORTED;
+}
+
+int decode_image_file(const std::string &path, std::vector<uint8_t> &rgba, int &width, int &height,
+                      std::string &err)
+{
+    FILE *f = fopen(path.c_str(), "rb");
+    if (!f) {
+        err = "cannot open " + path;
+        return RT_E_IO;
+    }
+    std::vector<uint8_t> buf;
+    uint8_t chunk[1 << 16];
+    size_t got;
+    while ((got = fread(chunk, 1, sizeof chunk, f)) > 0) buf.insert(buf.end(), chunk, chunk + got);
+    fclose(f);
+    return decode_image_memory(buf.data(), buf.size(), rgba, width, height, err);
+}
+
+} // namespace rt_host

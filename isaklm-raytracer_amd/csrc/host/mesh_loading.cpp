@@ -114,8 +114,71 @@ bool create_vertex(const char *tok, int npos, int ntex, int nnor, ObjVertex &v)
 
 } // namespace
 
+static std::string dir_of(const std::string &p)
+{
+    const size_t k = p.find_last_of('/');
+    return k == std::string::npos ? std::string() : p.substr(0, k + 1);
+}
+
+static bool file_exists(const std::string &p)
+{
+    FILE *f = fopen(p.c_str(), "rb");
+    if (f) fclose(f);
+    return f != nullptr;
+}
+
+// make_texture (rt/scene.cuh:25-63): stbi_load(path, ..., 4) -> RGBA8 texels.
+// The reference opens `file` relative to the working directory; a path that
+// does not exist there is also looked up next to the .mat file and in its
+// parent directory (the reference's layout: materials/x.mat, textures/y.png).
+// A texture file that exists nowhere leaves the material untextured, as in the
+// reference (stbi_load fails, a 0x0 texture whose cudaMalloc(0) buffer is
+// NULL).  A file that exists but does not decode is an error.
+static int make_texture(RtHostScene &scene, const std::string &mat_path, const std::string &file, Texture &tex)
+{
+    memset(&tex, 0, sizeof tex);
+    std::string found;
+    const std::string d = dir_of(mat_path);
+    const std::string up = d.empty() ? std::string("../") : dir_of(d.substr(0, d.size() - 1));
+    for (const std::string &c : {file, d + file, up + file})
+        if (!c.empty() && file_exists(c)) {
+            found = c;
+            break;
+        }
+    if (found.empty()) return RT_OK;
+    for (const auto &t : scene.textures) // one decode per file per scene
+        if (t->path == found) {
+            tex.buffer = t->texels.data();
+            tex.width = t->width;
+            tex.height = t->height;
+            return RT_OK;
+        }
+    std::vector<uint8_t> rgba;
+    int w = 0, h = 0;
+    std::string err;
+    const int rc = decode_image_file(found, rgba, w, h, err);
+    if (rc != RT_OK) {
+        rt_set_error("%s: texture %s: %s", mat_path.c_str(), found.c_str(), err.c_str());
+        return rc;
+    }
+    std::unique_ptr<RtHostTexture> t(new RtHostTexture);
+    t->path = found;
+    t->width = w;
+    t->height = h;
+    // + (width + 1) zero texels: mod(uv, 1) can return 1.0, so sample_texture's
+    // index reaches width * height + width (the reference reads past
+    // its buffer there)
+    t->texels.assign((size_t)w * h + (size_t)w + 1, RtUChar4{0, 0, 0, 0});
+    memcpy(t->texels.data(), rgba.data(), (size_t)w * h * 4);
+    tex.buffer = t->texels.data();
+    tex.width = w;
+    tex.height = h;
+    scene.textures.push_back(std::move(t));
+    return RT_OK;
+}
+
 // load_material (rt/mesh_loading.cuh:152-219)
-static int load_material(const std::string &path, const std::string &name, Material &m)
+static int load_material(RtHostScene &scene, const std::string &path, const std::string &name, Material &m)
 {
     memset(&m, 0, sizeof m); // { ZERO_VEC3D, ZERO_VEC3D, 0, 0, 0, false, NO_TEXTURE }
     std::string text;
@@ -160,13 +223,9 @@ static int load_material(const std::string &path, const std::string &name, Mater
                 ok = parse_float(tk.t[1], m.extinction);
             } else if (key == "transparent") {
                 m.transparent = true;
-            } else if (key == "texture") {
-                // make_texture (rt/scene.cuh:25-63) decodes PNG/JPG with stb_image;
-                // image decoding is not part of this build.
-                rt_set_error("%s: material %s uses a texture (%s); texture decoding is not supported by the "
-                             "host loader — pass decoded RGBA8 device texels through rt_scene_prepare_host",
-                             path.c_str(), name.c_str(), tk.t.size() > 1 ? tk.t[1] : "?");
-                return RT_E_UNSUPPORTED;
+            } else if (key == "texture" && tk.t.size() >= 2) {
+                const int rc = make_texture(scene, path, tk.t[1], m.texture);
+                if (rc != RT_OK) return rc;
             }
             if (!ok) {
                 rt_set_error("%s: bad number in material %s", path.c_str(), name.c_str());
@@ -239,7 +298,7 @@ int load_mesh(RtHostScene &scene, const std::string &obj_path, const std::string
                 auto it = material_ids.find(name);
                 if (it == material_ids.end()) {
                     Material m;
-                    int rc = load_material(mat_path, name, m);
+                    int rc = load_material(scene, mat_path, name, m);
                     if (rc != RT_OK) return rc;
                     int id = (int)materials.size();
                     materials.push_back(m);
@@ -334,11 +393,6 @@ int load_mesh(RtHostScene &scene, const std::string &obj_path, const std::string
     return RT_OK;
 }
 
-static std::string dir_of(const std::string &p)
-{
-    size_t s = p.rfind('/');
-    return s == std::string::npos ? std::string() : p.substr(0, s + 1);
-}
 static std::string resolve(const std::string &dir, const std::string &p)
 {
     return (!p.empty() && p[0] == '/') ? p : dir + p;

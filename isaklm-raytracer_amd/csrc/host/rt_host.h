@@ -4,6 +4,7 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -12,8 +13,19 @@
 
 void rt_set_error(const char *fmt, ...);
 
+// A decoded texture owned by a host scene.  Host triangles' material.texture
+// points at `texels` (host memory); rt_create_scene uploads every texture once
+// and points the device triangles at the device copy (make_texture,
+// rt/scene.cuh:25-63, cudaMallocs at load time instead).
+struct RtHostTexture {
+    std::string path; // as written in the .mat file
+    int width = 0, height = 0;
+    std::vector<RtUChar4> texels; // width * height + RT_TEXTURE_PAD
+};
+
 struct RtHostScene {
     std::vector<Triangle> tris;
+    std::vector<std::unique_ptr<RtHostTexture>> textures;
 };
 
 namespace rt_host {
@@ -49,5 +61,11 @@ int prepare_host(const Triangle *tris, int ntris, const KD_Tree_Node *nodes, int
                  int nindices, const int *lights, int nlights, Bounding_Box bounds, PreparedHost &out);
 
 int write_png(const char *path, const uint8_t *rgba, int width, int height);
+
+// stbi_load(path, &w, &h, &n, 4) for PNG and baseline JPEG (image_decode.cpp)
+int decode_image_memory(const uint8_t *data, size_t size, std::vector<uint8_t> &rgba, int &width, int &height,
+                        std::string &err);
+int decode_image_file(const std::string &path, std::vector<uint8_t> &rgba, int &width, int &height,
+                      std::string &err);
 
 } // namespace rt_host

@@ -902,21 +902,37 @@ struct Workspace {
 
 std::map<int, Workspace> g_ws; // per device
 
-int ensure(Workspace &w, size_t slots, int grid)
+__global__ void wf_bind_stream() {}
+
+// the pipelines' streams (created on first use, each bound to its hardware
+// queue by an empty launch: the runtime maps a stream to a queue when it is
+// first used, and streams created later share queues once the process has
+// used its GPU_MAX_HW_QUEUES)
+int ensure_streams(Workspace &w, int npipes)
 {
     if (!w.streams_ok) {
         if (hipEventCreateWithFlags(&w.fork, hipEventDisableTiming) != hipSuccess) return -1;
         if (hipEventCreateWithFlags(&w.long_ev, hipEventDisableTiming) != hipSuccess) return -1;
         if (hipEventCreate(&w.ev0) != hipSuccess || hipEventCreate(&w.ev1) != hipSuccess) return -1;
-        for (Pipe &p : w.pipe) {
-            if (hipStreamCreateWithFlags(&p.stream, hipStreamNonBlocking) != hipSuccess) return -1;
-            if (hipHostMalloc((void **)&p.host_count, 64) != hipSuccess) return -1;
-            if (hipEventCreateWithFlags(&p.join, hipEventDisableTiming) != hipSuccess) return -1;
-            for (auto &e : p.ev)
-                if (hipEventCreate(&e) != hipSuccess) return -1;
-        }
         w.streams_ok = true;
     }
+    for (int i = 0; i < npipes && i < WF_MAX_PIPES; ++i) {
+        Pipe &p = w.pipe[i];
+        if (p.stream) continue;
+        if (hipStreamCreateWithFlags(&p.stream, hipStreamNonBlocking) != hipSuccess) return -1;
+        if (hipHostMalloc((void **)&p.host_count, 64) != hipSuccess) return -1;
+        if (hipEventCreateWithFlags(&p.join, hipEventDisableTiming) != hipSuccess) return -1;
+        for (auto &e : p.ev)
+            if (hipEventCreate(&e) != hipSuccess) return -1;
+        hipLaunchKernelGGL(wf_bind_stream, dim3(1), dim3(64), 0, p.stream);
+        if (hipGetLastError() != hipSuccess || hipStreamSynchronize(p.stream) != hipSuccess) return -1;
+    }
+    return 0;
+}
+
+int ensure(Workspace &w, size_t slots, int grid, int npipes)
+{
+    if (ensure_streams(w, npipes) != 0) return -1;
     if (w.slots >= slots && w.grid >= grid) return 0;
     if (w.blob) (void)hipFree(w.blob);
     w.blob = nullptr;
@@ -985,6 +1001,15 @@ float elapsed_ms(hipEvent_t a, hipEvent_t b)
 
 } // namespace
 
+// rt_set_device: the default pipelines' streams take their hardware queues
+// before anything else in the process (RCCL's streams in a multi-GPU run)
+int rt_wavefront_device_init()
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return -1;
+    return ensure_streams(g_ws[dev], WF_PIPES_DEFAULT);
+}
+
 extern "C" int rt_last_profile(RtProfile *out)
 {
     if (!out) return RT_E_INVALID;
@@ -1007,13 +1032,13 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
     Workspace &w = g_ws[dev];
     const int grid = 2048; // persistent-ish grid for trace/shade (grid-stride over the queue)
     const size_t slots = (size_t)fr.width * fr.height;
-    if (ensure(w, slots, grid) != 0) return -1;
     const bool count = fr.counters != nullptr;
     const bool prof = profile != 0;
     const int tiles = ((fr.width + 15) / 16) * ((fr.height + 15) / 16);
     int npipes = pipes_opt > 0 ? pipes_opt : WF_PIPES_DEFAULT;
     npipes = npipes > WF_MAX_PIPES ? WF_MAX_PIPES : npipes;
     npipes = npipes > tiles ? tiles : npipes;
+    if (ensure(w, slots, grid, npipes) != 0) return -1;
     // below this many live paths the rest of the call runs in one finisher launch
     const uint32_t tail = tail_opt > 0 ? (uint32_t)tail_opt : WF_TAIL_DEFAULT;
     // the cooperative finisher runs on at most this many waves (up to 64 paths in flight each)

@@ -105,6 +105,8 @@ def lib():
         L.rt_set_device.argtypes = [i]
         L.rt_host_free.argtypes = [vp]
         L.rt_host_free.restype = None
+        L.rt_decode_image.argtypes = [ctypes.c_char_p, ctypes.POINTER(vp), ctypes.POINTER(i), ctypes.POINTER(i)]
+        L.rt_decode_image_memory.argtypes = [vp, sz, ctypes.POINTER(vp), ctypes.POINTER(i), ctypes.POINTER(i)]
         L.rt_gbuffer_seeds.argtypes = [vp, sz, ctypes.c_uint64]
         L.rt_gbuffer_create.argtypes = [i, i, ctypes.c_uint64, ctypes.POINTER(G_Buffer)]
         L.rt_gbuffer_destroy.argtypes = [ctypes.POINTER(G_Buffer)]
@@ -187,6 +189,22 @@ class HostScene:
                 self.h = None
         except Exception:
             pass
+
+
+def decode_image(path=None, data=None):
+    """stbi_load(path, &w, &h, &n, 4) as make_texture calls it (rt/scene.cuh:33):
+    RGBA8 (H, W, 4) uint8, rows in file order.  PNG and baseline JPEG."""
+    p, w, h = ctypes.c_void_p(), ctypes.c_int(), ctypes.c_int()
+    if data is not None:
+        buf = np.frombuffer(bytes(data), dtype=np.uint8)
+        check(lib().rt_decode_image_memory(_ptr(buf), buf.nbytes, ctypes.byref(p), ctypes.byref(w), ctypes.byref(h)))
+    else:
+        check(lib().rt_decode_image(path.encode(), ctypes.byref(p), ctypes.byref(w), ctypes.byref(h)))
+    try:
+        n = w.value * h.value * 4
+        return np.frombuffer(ctypes.string_at(p, n), dtype=np.uint8).reshape(h.value, w.value, 4).copy()
+    finally:
+        lib().rt_host_free(p)
 
 
 def build_kd_tree(tri_ptr, n):

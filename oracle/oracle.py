@@ -52,6 +52,7 @@ def lib():
         L.or_scene_copy.argtypes = [vp, vp, vp, vp, vp, vp]
         L.or_scene_copy.restype = None
         L.or_load_material.argtypes = [ctypes.c_char_p, ctypes.c_char_p, vp]
+        L.or_register_texture.argtypes = [ctypes.c_char_p, vp, i, i]
         L.or_trace_rays.argtypes = [vp, vp, i, vp]
         L.or_trace_rays.restype = None
         L.or_scatter.argtypes = [vp, vp, i, ctypes.c_uint32, vp, ctypes.POINTER(ctypes.c_uint32),
@@ -156,6 +157,13 @@ def correct_color(c):
     o = np.zeros(3, dtype=np.float32)
     lib().or_correct_color(_p(a), _p(o))
     return o
+
+
+def register_texture(path, rgba):
+    """texels (H, W, 4) uint8 for `texture <path>` in .mat files (the oracle decodes no images)."""
+    a = np.ascontiguousarray(rgba, dtype=np.uint8)
+    if lib().or_register_texture(path.encode(), _p(a), a.shape[1], a.shape[0]) != 0:
+        raise RuntimeError("or_register_texture failed")
 
 
 def load_material(path, name):

@@ -994,8 +994,48 @@ static char *read_line(FILE *f, char **buf, size_t *cap)
     return *buf;
 }
 
-/* load_material (:152-219); textures are not decoded by the oracle (the
- * texture field stays NO_TEXTURE; synthetic scenes carry no textures). */
+/* Textures (make_texture, rt/scene.cuh:25-63).  The oracle does not decode
+ * images: the test registers the RGBA8 texels of each `texture` path (the
+ * string as written in the .mat file) beforehand; a path with no registered
+ * texels stays NO_TEXTURE, like a file stbi_load cannot open.  Each texture is
+ * stored with width + 1 zero texels after the image (mod() can return 1.0,
+ * SURVEY H10), as the product pads its device copy. */
+typedef struct { char *path; UC4 *texels; int width, height; } OrTex;
+static OrTex *g_tex = NULL;
+static int g_ntex = 0;
+
+int or_register_texture(const char *path, const uint8_t *rgba, int width, int height)
+{
+    if (!path || !rgba || width <= 0 || height <= 0) return -1;
+    OrTex *t = realloc(g_tex, sizeof(OrTex) * (size_t)(g_ntex + 1));
+    if (!t) return -1;
+    g_tex = t;
+    const size_t n = (size_t)width * height;
+    UC4 *tx = calloc(n + (size_t)width + 1, sizeof(UC4));
+    if (!tx) return -1;
+    memcpy(tx, rgba, n * 4);
+    g_tex[g_ntex].path = strdup(path);
+    g_tex[g_ntex].texels = tx;
+    g_tex[g_ntex].width = width;
+    g_tex[g_ntex].height = height;
+    ++g_ntex;
+    return 0;
+}
+
+static Texture find_texture(const char *path)
+{
+    Texture t = {NULL, 0, 0};
+    for (int i = g_ntex - 1; i >= 0; --i)
+        if (!strcmp(g_tex[i].path, path)) {
+            t.buffer = g_tex[i].texels;
+            t.width = g_tex[i].width;
+            t.height = g_tex[i].height;
+            break;
+        }
+    return t;
+}
+
+/* load_material (:152-219) */
 static bool load_material(const char *path, const char *name, Material *m, bool *ok)
 {
     memset(m, 0, sizeof *m);
@@ -1026,6 +1066,8 @@ static bool load_material(const char *path, const char *name, Material *m, bool 
                 m->extinction = stof_(s.s[1], ok);
             } else if (!strcmp(s.s[0], "transparent")) {
                 m->transparent = true;
+            } else if (!strcmp(s.s[0], "texture") && s.n >= 2) {
+                m->texture = find_texture(s.s[1]);
             }
             sv_free(&s);
         }

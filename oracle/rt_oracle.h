@@ -63,6 +63,10 @@ void or_scene_copy(const OrScene *s, void *triangles152, void *nodes20, int *ind
  * roughness, n, k, transparent(0/1); returns 1 if found, 0 if not */
 int or_load_material(const char *mat_path, const char *name, float out[10]);
 
+/* registers the RGBA8 texels load_material uses for `texture <path>` (the
+ * string as written in the .mat file); the oracle decodes no images */
+int or_register_texture(const char *path, const uint8_t *rgba, int width, int height);
+
 /* trace_ray (rt/trace_ray.cuh:244-318) for n rays (o.xyz, d.xyz);
  * out per ray: [hit, triangle_index, position.xyz, normal.xyz, tangent.xyz] as float[12] */
 void or_trace_rays(const OrScene *s, const float *rays6, int n, float *out12);

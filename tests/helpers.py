@@ -88,3 +88,62 @@ def rel_linf(gpu_fb, gpu_cnt, ref_fb, ref_cnt):
     b = ref_fb / np.maximum(ref_cnt, 1)[:, None]
     den = np.maximum(np.abs(b), 1e-30)
     return float(np.max(np.abs(a - b) / den)) if len(a) else 0.0
+
+
+# ------------------------------------------------------------ textured scene
+TEXTURED_VARIANTS = {"floor": "jpeg_ycc420_odd", "wall": "png_pal8_trns", "lamp": "png_rgba8_adam7",
+                     "back": "jpeg_ycc_q100", "grey": "png_grey4_trns"}
+
+
+def make_textured_scene(d):
+    """A closed room whose materials use textures (sample_texture, rt/trace_ray.cuh:31-46):
+    UVs far outside [0, 1] (mod wrap), a triangle whose UVs are a tiny negative
+    number (mod(uv, 1) == 1.0: the index reaches the padded texel after the
+    image), an emissive textured lamp (emittance * texel), a
+    material whose texture file is missing (untextured, as in the reference)
+    and one untextured material.  Texture files are synthetic variants whose
+    stb_image decode is recorded in tests/golden/textures.json.
+    Returns (scene_path, {texture path as in the .mat: variant name})."""
+    import texture_fixtures
+
+    os.makedirs(os.path.join(d, "textures"), exist_ok=True)
+    files = {}
+    data = texture_fixtures.variants()
+    for mat, var in TEXTURED_VARIANTS.items():
+        ext = "jpg" if var.startswith("jpeg") else "png"
+        rel = f"textures/{mat}.{ext}"
+        with open(os.path.join(d, rel), "wb") as f:
+            f.write(data[var])
+        files[rel] = var
+    mat_txt = ""
+    for mat in ("floor", "wall", "back", "grey"):
+        rel = [k for k, v in files.items() if v == TEXTURED_VARIANTS[mat]][0]
+        mat_txt += f"material {mat}\nalbedo 0.9 0.85 0.8\nroughness 0.4\nn 1.5\ntexture {rel}\n\n"
+    lamp = [k for k, v in files.items() if v == TEXTURED_VARIANTS["lamp"]][0]
+    mat_txt += f"material lamp\nalbedo 0.7 0.7 0.7\nemittance 12.0 11.0 9.0\nroughness 0.5\nn 1.5\ntexture {lamp}\n\n"
+    mat_txt += "material plain\nalbedo 0.5 0.6 0.7\nroughness 0.3\nn 1.4\n\n"
+    mat_txt += "material lost\nalbedo 0.8 0.3 0.3\nroughness 0.3\nn 1.4\ntexture textures/does_not_exist.png\n\n"
+    mat_txt += "material metal\nalbedo 0.95 0.9 0.8\nroughness 0.05\nn 1.2\nk 3.5\ntexture textures/floor.jpg\n"
+    with open(os.path.join(d, "room.mat"), "w") as f:
+        f.write(mat_txt)
+    v = [(-1, 0, -1), (1, 0, -1), (1, 0, 1), (-1, 0, 1), (-1, 2, -1), (1, 2, -1), (1, 2, 1), (-1, 2, 1),
+         (-0.3, 1.99, -0.3), (0.3, 1.99, -0.3), (0.3, 1.99, 0.3), (-0.3, 1.99, 0.3),
+         (-0.5, 0.001, 0.2), (0.1, 0.001, 0.2), (-0.2, 0.6, 0.3)]
+    vt = [(-1.3, -0.7), (2.7, -0.7), (2.7, 3.1), (-1.3, 3.1), (0, 0), (1, 0), (1, 1), (0, 1),
+          (-1e-9, -1e-9), (0.25, 0.75)]
+    obj = ["# textured room"] + [f"v {x} {y} {z}" for x, y, z in v] + [f"vt {a} {b}" for a, b in vt]
+    obj += ["usemtl floor", "f 1/1 2/2 3/3 4/4",
+            "usemtl wall", "f 1/5 4/6 8/7 5/8",
+            "usemtl back", "f 4/1 3/2 7/3 8/4",
+            "usemtl grey", "f 2/5 6/6 7/7 3/8",
+            "usemtl plain", "f 5/5 8/6 7/7 6/8",
+            "usemtl lost", "f 1/5 5/6 6/7 2/8",
+            "usemtl lamp", "f 9/5 12/8 11/7 10/6",
+            "usemtl metal", "f 13/9 14/9 15/9",
+            "usemtl grey", "f 13/10 15/10 14/9"]
+    with open(os.path.join(d, "room.obj"), "w") as f:
+        f.write("\n".join(obj) + "\n")
+    scene = os.path.join(d, "scene.txt")
+    with open(scene, "w") as f:
+        f.write("mesh room.obj room.mat 0 0 0 0 0 1 0\ncamera 0.05 1.0 -0.93 0.07 -0.05 1.3 0.005\n")
+    return scene, files

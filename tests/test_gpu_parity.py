@@ -123,6 +123,33 @@ def test_long_handoff_with_shared_hw_queues():
     assert r.returncode == 0 and "OK" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
 
 
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_textured_scene_bitwise(kernel, tmp_path):
+    """sample_texture (rt/trace_ray.cuh:31-46) on the GPU: textures decoded by
+    the product loader (PNG palette/Adam7/grey, baseline JPEG 4:2:0 and q100;
+    digests pinned to stb_image in tests/golden/textures.json), UVs wrapping
+    far outside [0, 1], a triangle whose mod(uv, 1) is 1.0 (padded texel), a
+    textured emitter and a missing texture file.  The oracle gets the same
+    texels through its registry."""
+    import hashlib
+    import json
+
+    scene, files = helpers.make_textured_scene(str(tmp_path))
+    golden = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "textures.json")))
+    for rel, var in files.items():
+        a = rt.decode_image(os.path.join(str(tmp_path), rel))
+        d = hashlib.sha256(a.tobytes()).hexdigest() + f":{a.shape[1]}x{a.shape[0]}"
+        assert d == golden["variants"][var], rel
+        oracle.register_texture(rel, a)
+    run = helpers.GpuRun(scene)
+    W, H, P = 48, 32, 6
+    gpu, gcnt, _ = run.render(W, H, P, calls=2, count=True, kernel=kernel)
+    ref, rcnt = helpers.oracle_render(scene, W, H, P, calls=2)
+    helpers.assert_bitwise(gpu, ref, what="textured")
+    assert gcnt == rcnt, (gcnt, rcnt)
+    assert rcnt["texel"] > 0
+
+
 def test_kernels_agree_multi_call(cornell):
     """Megakernel and wavefront give the same bits across calls with reset."""
     W, H = 33, 31

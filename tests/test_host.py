@@ -91,14 +91,18 @@ def test_face_index_out_of_range_is_parse_error(tmp_path):
     _expect_error(lambda: hs.load_mesh(str(p), str(tmp_path / "m.mat"), [0, 0, 0], np.eye(3)), -4)
 
 
-def test_textured_material_is_unsupported(tmp_path):
+def test_missing_texture_leaves_material_untextured(tmp_path):
+    """room.mat names textures/wall.png; where no such file exists the
+    reference's stbi_load fails and the material stays untextured."""
     (tmp_path / "t.obj").write_text("usemtl walls\nv 0 0 0\nv 1 0 0\nv 0 1 0\nf 1 2 3\n")
     import shutil
 
     shutil.copy(os.path.join(GOLDEN, "materials", "room.mat"), tmp_path / "room.mat")
     hs = rt.HostScene()
-    _expect_error(lambda: hs.load_mesh(str(tmp_path / "t.obj"), str(tmp_path / "room.mat"), [0, 0, 0],
-                                       np.eye(3)), -5)
+    hs.load_mesh(str(tmp_path / "t.obj"), str(tmp_path / "room.mat"), [0, 0, 0], np.eye(3))
+    tb, n = hs.triangles_bytes()
+    t = np.frombuffer(tb, np.uint8).reshape(n, 152)
+    assert not t[:, 136:152].any()  # Texture {NULL, 0, 0}
 
 
 def test_load_mesh_api_matches_scene_file(tmp_path):
