@@ -63,6 +63,15 @@ __device__ __forceinline__ bool plane_maybe(float num, float dn, float ex)
     return !(sa < 0.0000099999f) && !(sa >= ex * 1.00001f);
 }
 
+// plane_maybe as one expression of compares and selects (same result)
+__device__ __forceinline__ bool plane_maybe_sel(float num, float dn, float ex)
+{
+    const float sa = num * __builtin_amdgcn_rcpf(dn);
+    const bool tiny = !(fabsf(dn) >= 0x1p-100f);
+    const bool keep = !(sa < 0.0000099999f) & !(sa >= ex * 1.00001f);
+    return (dn != 0.0f) & (tiny | keep);
+}
+
 // per-wave LDS scratch of the cooperative leaf test
 struct CoopLds {
     unsigned long long *key; // 64: per-lane winner key (atomicMin)
@@ -206,6 +215,17 @@ __device__ __forceinline__ bool coop_leaves(const RtDevScene &sc, CoopRay &r, ST
             const Vec3D oo = rt_v3(__shfl(r.o.x, j), __shfl(r.o.y, j), __shfl(r.o.z, j));
             const Vec3D dd = rt_v3(__shfl(r.d.x, j), __shfl(r.d.y, j), __shfl(r.d.z, j));
             const float ex = __shfl(r.exit_, j);
+#ifndef RT_COOP_BRANCHY
+            // every lane loads (past the last pair: entry 0, a
+            // valid address) and the prescreen is a chain of selects: no exec-mask
+            // branches in the hot loop
+            const bool valid = p < total;
+            const uint32_t kk = valid ? k : 0u;
+            const RtF4 A = ldf4(sc.isect_a + kk); // n, d
+            const float dn = dd.x * A.x + dd.y * A.y + dd.z * A.z;
+            const float num = A.w - (oo.x * A.x + oo.y * A.y + oo.z * A.z);
+            const bool cand = valid & plane_maybe_sel(num, dn, ex);
+#else
             bool cand = false;
             float num = 0.0f, dn = 0.0f;
             if (p < total) {
@@ -214,6 +234,7 @@ __device__ __forceinline__ bool coop_leaves(const RtDevScene &sc, CoopRay &r, ST
                 num = A.w - (oo.x * A.x + oo.y * A.y + oo.z * A.z);
                 cand = plane_maybe(num, dn, ex);
             }
+#endif
             const unsigned long long pm = __ballot(cand);
             if (cand)
                 list[list_n + __popcll(pm & ((1ull << lane) - 1ull))] =
