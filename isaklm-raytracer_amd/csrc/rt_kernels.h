@@ -530,6 +530,18 @@ __device__ __forceinline__ int wave_incl_max(int v) // identity -1
     v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x143, 0xc, 0xf, false));
     return v;
 }
+// inclusive max-scan of non-negative values: identity 0, so each step is one
+// v_max_u32 with a DPP operand (no separate v_mov of an identity)
+__device__ __forceinline__ uint32_t wave_incl_umax(uint32_t v)
+{
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false));
+    return v;
+}
 __device__ __forceinline__ int lane63(int v) { return __builtin_amdgcn_readlane(v, 63); }
 
 // Owner lane of every position of a 64-wide chunk [base, base + 64) of a
@@ -549,10 +561,18 @@ __device__ __forceinline__ int chunk_owner(int *mark_, int start, int count, int
 {
     lds_vint *mark = (lds_vint *)mark_;
     const int lane = __lane_id();
+#ifdef RT_OWNER_SMAX
     mark[lane] = -1;
     if (count > 0 && start >= base && start < base + 64) mark[start - base] = lane;
     const int m = wave_incl_max(mark[lane]);
     return max(m, carry);
+#else
+    // marks are lane + 1 (0 = none): the scan's identity is 0
+    mark[lane] = 0;
+    if (count > 0 && start >= base && start < base + 64) mark[start - base] = lane + 1;
+    const int m = (int)wave_incl_umax((uint32_t)mark[lane]) - 1;
+    return max(m, carry);
+#endif
 }
 
 // block -> 16x16 tile, remapped so each XCD (blocks b, b+8, ...) owns one
