@@ -206,7 +206,7 @@ __device__ __forceinline__ bool coop_leaves(const RtDevScene &sc, CoopRay &r, ST
     const int start = incl - leaf_count; // exclusive prefix: lane j's pairs are [start, start + leaf_count)
     const uint32_t kbase = r.leaf_begin - (uint32_t)start; // entry of pair p = kbase_j + p
     lds_vu64 *vkey = (lds_vu64 *)wkey; // set and read per lane, lowered by other lanes: see chunk_owner
-    vkey[lane] = ~0ull;
+    vkey[lane] = (unsigned long long)(uint32_t)vconst(-1) << 32 | (uint32_t)vconst(-1);
     int list_n = 0, carry = -1;
 #ifndef RT_COOP_NO_PREFETCH
     // software pipeline: the owner, entry and plane load of chunk c + 1 are

@@ -542,6 +542,20 @@ __device__ __forceinline__ uint32_t wave_incl_umax(uint32_t v)
     v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false));
     return v;
 }
+// a constant materialised where it is used: the compiler otherwise hoists
+// constant register tuples (the miss record, the ~0 key) out of the traversal
+// loop and, short of registers, spills and reloads them from scratch there
+__device__ __forceinline__ int vconst(int c)
+{
+    int r;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "i"(c));
+    return r;
+}
+__device__ __forceinline__ float4 miss_record() // hits[]: tri = -1, no barycentrics
+{
+    return make_float4(__int_as_float(vconst(-1)), __int_as_float(vconst(0)), __int_as_float(vconst(0)),
+                       __int_as_float(vconst(0)));
+}
 __device__ __forceinline__ int lane63(int v) { return __builtin_amdgcn_readlane(v, 63); }
 
 // Owner lane of every position of a 64-wide chunk [base, base + 64) of a
@@ -567,10 +581,16 @@ __device__ __forceinline__ int chunk_owner(int *mark_, int start, int count, int
     const int m = wave_incl_max(mark[lane]);
     return max(m, carry);
 #else
-    // marks are lane + 1 (0 = none): the scan's identity is 0
-    mark[lane] = 0;
-    if (count > 0 && start >= base && start < base + 64) mark[start - base] = lane + 1;
-    const int m = (int)wave_incl_umax((uint32_t)mark[lane]) - 1;
+    // marks are lane + 1 (0 = none): the scan's identity is 0.  Addressed
+    // relative to the lane's own slot (no second base-address register).
+    lds_vint *mine = mark + lane;
+    mine[0] = 0;
+    if (count > 0 && start >= base && start < base + 64) {
+        int rel = start - base - lane;
+        asm volatile("" : "+v"(rel)); // keep `mine + rel` (the compiler would re-derive the base)
+        mine[rel] = lane + 1;
+    }
+    const int m = (int)wave_incl_umax((uint32_t)mine[0]) - 1;
     return max(m, carry);
 #endif
 }

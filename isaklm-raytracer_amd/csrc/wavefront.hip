@@ -30,7 +30,12 @@
 using namespace rtk;
 
 #define WF_BLOCK 256
+#ifndef WF_LDS_STACK
 #define WF_LDS_STACK 8  // stack entries in LDS; deeper ones spill to HBM (rare)
+#endif
+#ifndef WF_TRACE_WAVES
+#define WF_TRACE_WAVES 6 // wf_trace_coop occupancy target (blocks of 4 waves per CU = waves per SIMD)
+#endif
 #define WF_TAIL_DEFAULT 65536u       // RtOptions.wf_tail
 #define WF_FINISH_WAVES_DEFAULT 2048u // RtOptions.wf_finish_waves
 #define WF_DESCENT_CAP_DEFAULT 8      // RtOptions.wf_descent_cap
@@ -242,7 +247,7 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_trace_dyn(RtDevScene sc, WfState 
                         sp = 0;
                         live = true;
                     } else {
-                        *reinterpret_cast<float4 *>(st.hits + e) = make_float4(__int_as_float(-1), 0.f, 0.f, 0.f);
+                        *reinterpret_cast<float4 *>(st.hits + e) = miss_record();
                     }
                 }
             }
@@ -341,7 +346,7 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_trace_dyn(RtDevScene sc, WfState 
             *reinterpret_cast<float4 *>(st.hits + e) = make_float4(__int_as_float(best), bx, by, bz);
             live = false;
         } else if (sp == 0) {
-            *reinterpret_cast<float4 *>(st.hits + e) = make_float4(__int_as_float(-1), 0.f, 0.f, 0.f);
+            *reinterpret_cast<float4 *>(st.hits + e) = miss_record();
             live = false;
         } else {
             --sp;
@@ -360,7 +365,7 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_trace_dyn(RtDevScene sc, WfState 
 // capped at `cap` node fetches per round and the leaf test waits for
 // `postpone` pending lanes.
 template <bool COUNT>
-__global__ void __launch_bounds__(WF_BLOCK, 6) wf_trace_coop(RtDevScene sc, WfState st, int q,
+__global__ void __launch_bounds__(WF_BLOCK, WF_TRACE_WAVES) wf_trace_coop(RtDevScene sc, WfState st, int q,
                                                           unsigned long long *counters, int cap, int postpone,
                                                           int wide_lanes, unsigned long long *timeline)
 {
@@ -409,7 +414,7 @@ __global__ void __launch_bounds__(WF_BLOCK, 6) wf_trace_coop(RtDevScene sc, WfSt
                 } else {
                     if (COUNT) c.v[RT_CNT_RAY]++;
                     if (!coop_begin(sc, r, ld3(ldf4(rays + 2 * (size_t)e)), ld3(ldf4(rays + 2 * (size_t)e + 1))))
-                        *reinterpret_cast<float4 *>(st.hits + e) = make_float4(__int_as_float(-1), 0.f, 0.f, 0.f);
+                        *reinterpret_cast<float4 *>(st.hits + e) = miss_record();
                 }
             }
         }
