@@ -232,3 +232,21 @@ def test_room2m_full_frame_sparse_pixels(kernel):
     ref, _ = helpers.oracle_render(run.path, W, H, P, pixels=pixels)
     helpers.assert_bitwise(gpu, ref, pixels=pixels, what="room2m")
     assert np.all(gpu[2] == P)
+
+
+@pytest.mark.timeout(240)
+def test_room2m_glass_adaptive_full_frame_sparse_pixels():
+    """BASELINE configs[4] setting per GPU: the dielectric stress scene
+    (2M-triangle glass mesh, smooth normals) at 1920x1080, adaptive sampling
+    on (engaging after min_samples), max depth 32, wavefront kernel with its
+    default pipelines / long-path hand-off; every 3001st pixel re-rendered by
+    the oracle.  Pixels are independent, so the sparse check covers the
+    full-frame launch."""
+    run = helpers.GpuRun("room2m_glass")
+    W, H, P, MS = 1920, 1080, 24, 16
+    gpu, _, _ = run.render(W, H, P, adaptive=True, min_samples=MS, max_depth=32, kernel=rt.KERNEL_WAVEFRONT)
+    pixels = np.arange(0, W * H, 3001, dtype=np.int32)
+    ref, rcnt = helpers.oracle_render(run.path, W, H, P, adaptive=True, min_samples=MS, max_depth=32, pixels=pixels)
+    helpers.assert_bitwise(gpu, ref, pixels=pixels, what="room2m_glass adaptive")
+    assert rcnt["skip"] > 0  # the adaptive test really skipped pixel-passes
+    assert helpers.rel_linf(gpu[0][pixels], gpu[2][pixels], ref[0][pixels], ref[2][pixels]) < 1e-4
