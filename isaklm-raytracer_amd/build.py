@@ -15,6 +15,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 BUILD = os.path.join(HERE, "_build")
 LIB = os.path.join(HERE, "libisaklm_rt.so")
+APP = os.path.join(HERE, "rt_render")  # C++ driver binary (apps/rt_render_main.cpp)
 ROOT = os.path.dirname(HERE)
 INCLUDE = os.path.join(ROOT, "include")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
@@ -55,8 +56,8 @@ STAMP = LIB + ".stamp"
 
 def _digest(extra_hip_flags):
     h = hashlib.sha256()
-    files = [os.path.join(CSRC, f) for f in HOST_SOURCES + HIP_SOURCES + HEADERS] + [os.path.join(INCLUDE,
-                                                                                                  "isaklm_rt.h")]
+    files = [os.path.join(CSRC, f) for f in HOST_SOURCES + HIP_SOURCES + HEADERS] + [
+        os.path.join(INCLUDE, "isaklm_rt.h"), os.path.join(HERE, "apps", "rt_render_main.cpp")]
     for f in files:
         with open(f, "rb") as fh:
             h.update(os.path.relpath(f, ROOT).encode() + fh.read())
@@ -68,7 +69,7 @@ def _digest(extra_hip_flags):
 def build(verbose=False, extra_hip_flags=()):
     """Builds libisaklm_rt.so unless the stamp shows it was built from these exact sources."""
     digest = _digest(extra_hip_flags)
-    if os.path.exists(LIB) and os.path.exists(STAMP) and open(STAMP).read().strip() == digest:
+    if os.path.exists(LIB) and os.path.exists(APP) and os.path.exists(STAMP) and open(STAMP).read().strip() == digest:
         return LIB
     os.makedirs(BUILD, exist_ok=True)
     headers = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(INCLUDE, "isaklm_rt.h")]
@@ -90,6 +91,11 @@ def build(verbose=False, extra_hip_flags=()):
         _run(["g++", "-shared", "-o", LIB] + objs +
              ["-L" + os.path.join(ROCM, "lib"), "-lamdhip64", "-lrccl", "-fopenmp",
               "-Wl,-rpath," + os.path.join(ROCM, "lib")], verbose)
+    # the C++ driver (the reference's main() without GLFW) over the C-ABI
+    app_src = os.path.join(HERE, "apps", "rt_render_main.cpp")
+    if _stale(APP, [LIB, app_src, os.path.join(INCLUDE, "isaklm_rt.h")]):
+        _run(["g++", "-O2", "-std=c++17", "-Wall", "-I" + INCLUDE, app_src, "-o", APP, "-L" + HERE, "-lisaklm_rt",
+              "-Wl,-rpath,$ORIGIN", "-Wl,-rpath," + os.path.join(ROCM, "lib")], verbose)
     with open(STAMP, "w") as fh:
         fh.write(digest + "\n")
     return LIB
