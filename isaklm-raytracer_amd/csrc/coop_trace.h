@@ -18,9 +18,6 @@
 #pragma once
 
 #define WF_COOP_LIST 128 // per-wave LDS list of plane-test candidates
-// A/B switches (default off): RT_COOP_NO_PREFETCH (no software pipelining of
-// the chunk loop's plane loads, -4.5 % trace time when on), RT_COOP_BRANCHY
-// (plane prescreen with branches instead of selects, with NO_PREFETCH only)
 
 namespace rtk {
 
@@ -79,7 +76,7 @@ __device__ __forceinline__ bool plane_maybe_sel(float num, float dn, float ex)
 struct CoopLds {
     unsigned long long *key; // 64: per-lane winner key (atomicMin)
     CoopCand *list;          // WF_COOP_LIST plane-test candidates
-    int *mark;               // 64: chunk_owner marks
+    int *mark;               // 128: chunk_owner marks (64) + junk slots (64)
 };
 
 // per-lane traversal state
@@ -208,9 +205,34 @@ __device__ __forceinline__ bool coop_leaves(const RtDevScene &sc, CoopRay &r, ST
     lds_vu64 *vkey = (lds_vu64 *)wkey; // set and read per lane, lowered by other lanes: see chunk_owner
     vkey[lane] = (unsigned long long)(uint32_t)vconst(-1) << 32 | (uint32_t)vconst(-1);
     int list_n = 0, carry = -1;
-#ifndef RT_COOP_NO_PREFETCH
-    // software pipeline: the owner, entry and plane load of chunk c + 1 are
-    // issued before chunk c's plane test, so its load latency overlaps it
+    // exact plane + barycentric stage over the first min(list_n, 64) listed
+    // candidates; the rest (< 64) moves to the front of the list
+    auto bary_stage = [&]() {
+        if (COUNT && lane == 0) c.v[RT_CNT_BARY]++;
+        const int take = list_n < 64 ? list_n : 64;
+        const CoopCand it = list[lane < take ? lane : 0];
+        const int j = (int)(it.key & 63u);
+        const Vec3D oo = rt_v3(__shfl(r.o.x, j), __shfl(r.o.y, j), __shfl(r.o.z, j));
+        const Vec3D dd = rt_v3(__shfl(r.d.x, j), __shfl(r.d.y, j), __shfl(r.d.z, j));
+        const float ex = __shfl(r.exit_, j);
+        if (lane < take) {
+            const float dn = __uint_as_float(it.dn);
+            const float s = __uint_as_float(it.num) / dn; // intersect_triangle (:95-98)
+            float cx, cy, cz;
+            int t;
+            const bool plane = dn != 0 && s >= 0.00001f && s < ex;
+            if (COUNT && plane) c.v[RT_CNT_PLANE]++;
+            if (plane && coop_bary(sc, it.key >> 6, oo, dd, s, cx, cy, cz, t))
+                atomicMin(wkey + j, ((unsigned long long)__float_as_uint(s) << 32) | (it.key >> 6));
+        }
+        const int rest = list_n - take;
+        CoopCand mv = CoopCand{0u, 0u, 0u};
+        if (lane < rest) mv = list[take + lane];
+        if (lane < rest) list[lane] = mv;
+        list_n = rest;
+    };
+    // Software pipeline: the owner, entry and plane load of chunk c + 1 are
+    // issued before chunk c's plane test, so its load latency overlaps it.
     int nj = 0;
     uint32_t nk = 0;
     RtF4 nA = RtF4{0.0f, 0.0f, 0.0f, 0.0f};
@@ -221,90 +243,36 @@ __device__ __forceinline__ bool coop_leaves(const RtDevScene &sc, CoopRay &r, ST
         // the shuffle runs on every lane: behind a `p < total` branch it would
         // read 0 from owners whose own position is past the end of the chunk
         const uint32_t k = (uint32_t)__shfl((int)kbase, nj) + (uint32_t)p;
-        nk = p < total ? k : 0u;
+        nk = p < total ? k : 0u; // past the last pair: entry 0, a valid address
         nA = ldf4(sc.isect_a + nk);
     };
     if (total > 0) setup(0);
-#endif
-    for (int base = 0; base < total || list_n > 0; base += 64) {
-#ifndef RT_COOP_NO_PREFETCH
-        if (base < total) {
-            if (COUNT && lane == 0) c.v[RT_CNT_CHUNKS]++;
-            const int j = nj;
-            const uint32_t k = nk;
-            const RtF4 A = nA;
-            const bool valid = base + lane < total;
-            if (base + 64 < total) setup(base + 64);
-            const Vec3D oo = rt_v3(__shfl(r.o.x, j), __shfl(r.o.y, j), __shfl(r.o.z, j));
-            const Vec3D dd = rt_v3(__shfl(r.d.x, j), __shfl(r.d.y, j), __shfl(r.d.z, j));
-            const float ex = __shfl(r.exit_, j);
-            const float dn = dd.x * A.x + dd.y * A.y + dd.z * A.z;
-            const float num = A.w - (oo.x * A.x + oo.y * A.y + oo.z * A.z);
-            const bool cand = valid & plane_maybe_sel(num, dn, ex);
-#else
-        if (base < total) {
-            if (COUNT && lane == 0) c.v[RT_CNT_CHUNKS]++;
-            const int p = base + lane;
-            const int j = chunk_owner(w.mark, start, leaf_count, base, carry); // owner lane of pair p
-            carry = lane63(j);
-            const uint32_t k = (uint32_t)__shfl((int)kbase, j) + (uint32_t)p;
-            const Vec3D oo = rt_v3(__shfl(r.o.x, j), __shfl(r.o.y, j), __shfl(r.o.z, j));
-            const Vec3D dd = rt_v3(__shfl(r.d.x, j), __shfl(r.d.y, j), __shfl(r.d.z, j));
-            const float ex = __shfl(r.exit_, j);
-#ifndef RT_COOP_BRANCHY
-            // every lane loads (past the last pair: entry 0, a
-            // valid address) and the prescreen is a chain of selects: no exec-mask
-            // branches in the hot loop
-            const bool valid = p < total;
-            const uint32_t kk = valid ? k : 0u;
-            const RtF4 A = ldf4(sc.isect_a + kk); // n, d
-            const float dn = dd.x * A.x + dd.y * A.y + dd.z * A.z;
-            const float num = A.w - (oo.x * A.x + oo.y * A.y + oo.z * A.z);
-            const bool cand = valid & plane_maybe_sel(num, dn, ex);
-#else
-            bool cand = false;
-            float num = 0.0f, dn = 0.0f;
-            if (p < total) {
-                const RtF4 A = ldf4(sc.isect_a + k); // n, d
-                dn = dd.x * A.x + dd.y * A.y + dd.z * A.z;
-                num = A.w - (oo.x * A.x + oo.y * A.y + oo.z * A.z);
-                cand = plane_maybe(num, dn, ex);
-            }
-#endif
-#endif
-            const unsigned long long pm = __ballot(cand);
-            if (cand)
-                list[list_n + __popcll(pm & ((1ull << lane) - 1ull))] =
-                    CoopCand{(k << 6) | (uint32_t)j, __float_as_uint(num), __float_as_uint(dn)};
-            if (COUNT && cand) c.v[RT_CNT_CAND]++;
-            list_n += __popcll(pm);
-        }
-        // exact plane + barycentric stage over up to 64 listed candidates
-        if (list_n >= 64 || (base + 64 >= total && list_n > 0)) {
-            if (COUNT && lane == 0) c.v[RT_CNT_BARY]++;
-            const int take = list_n < 64 ? list_n : 64;
-            const CoopCand it = list[lane < take ? lane : 0];
-            const int j = (int)(it.key & 63u);
-            const Vec3D oo = rt_v3(__shfl(r.o.x, j), __shfl(r.o.y, j), __shfl(r.o.z, j));
-            const Vec3D dd = rt_v3(__shfl(r.d.x, j), __shfl(r.d.y, j), __shfl(r.d.z, j));
-            const float ex = __shfl(r.exit_, j);
-            if (lane < take) {
-                const float dn = __uint_as_float(it.dn);
-                const float s = __uint_as_float(it.num) / dn; // intersect_triangle (:95-98)
-                float cx, cy, cz;
-                int t;
-                const bool plane = dn != 0 && s >= 0.00001f && s < ex;
-                if (COUNT && plane) c.v[RT_CNT_PLANE]++;
-                if (plane && coop_bary(sc, it.key >> 6, oo, dd, s, cx, cy, cz, t))
-                    atomicMin(wkey + j, ((unsigned long long)__float_as_uint(s) << 32) | (it.key >> 6));
-            }
-            const int rest = list_n - take; // move the rest (< 64) to the front
-            CoopCand mv = CoopCand{0u, 0u, 0u};
-            if (lane < rest) mv = list[take + lane];
-            if (lane < rest) list[lane] = mv;
-            list_n = rest;
-        }
+    for (int base = 0; base < total; base += 64) {
+        if (COUNT && lane == 0) c.v[RT_CNT_CHUNKS]++;
+        const int j = nj;
+        const uint32_t k = nk;
+        const RtF4 A = nA;
+        const bool valid = base + lane < total;
+        if (base + 64 < total) setup(base + 64);
+        const Vec3D oo = rt_v3(__shfl(r.o.x, j), __shfl(r.o.y, j), __shfl(r.o.z, j));
+        const Vec3D dd = rt_v3(__shfl(r.d.x, j), __shfl(r.d.y, j), __shfl(r.d.z, j));
+        const float ex = __shfl(r.exit_, j);
+        const float dn = dd.x * A.x + dd.y * A.y + dd.z * A.z;
+        const float num = A.w - (oo.x * A.x + oo.y * A.y + oo.z * A.z);
+        const bool cand = valid & plane_maybe_sel(num, dn, ex);
+        // append without an exec-mask branch: candidates take the next slots
+        // in lane order, the other lanes write junk after them (slots below
+        // list_n + 64 <= 127, overwritten before they are read)
+        const unsigned long long pm = __ballot(cand);
+        const int below = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)pm, 0u));
+        const int npm = __popcll(pm);
+        const int slot = list_n + (cand ? below : npm + lane - below);
+        list[slot] = CoopCand{(k << 6) | (uint32_t)j, __float_as_uint(num), __float_as_uint(dn)};
+        if (COUNT && cand) c.v[RT_CNT_CAND]++;
+        list_n += npm;
+        if (list_n >= 64) bary_stage();
     }
+    if (list_n > 0) bary_stage();
     // ---- per-lane result: winner, or pop, or miss
     const unsigned long long key = vkey[lane];
     bool done = false;
@@ -399,7 +367,7 @@ struct WideLds {
     int cap;
     unsigned long long *key; // 1: winner key
     float *best;             // 4: winner barycentrics + triangle bits
-    int *mark;               // 64: chunk_owner marks
+    int *mark;               // 128: chunk_owner marks (64) + junk slots (64)
 };
 
 // an item whose node fetch (and, for a leaf, its triangle tests) the

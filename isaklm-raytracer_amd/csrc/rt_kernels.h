@@ -585,11 +585,12 @@ __device__ __forceinline__ int chunk_owner(int *mark_, int start, int count, int
     // relative to the lane's own slot (no second base-address register).
     lds_vint *mine = mark + lane;
     mine[0] = 0;
-    if (count > 0 && start >= base && start < base + 64) {
-        int rel = start - base - lane;
-        asm volatile("" : "+v"(rel)); // keep `mine + rel` (the compiler would re-derive the base)
-        mine[rel] = lane + 1;
-    }
+    // every lane stores: a lane whose segment does not start in this chunk
+    // writes 0 to its own junk slot 64 + lane (the mark array has 128 slots)
+    const bool marks = count > 0 && start >= base && start < base + 64;
+    int rel = marks ? start - base - lane : 64;
+    asm volatile("" : "+v"(rel)); // keep `mine + rel` (the compiler would re-derive the base)
+    mine[rel] = marks ? lane + 1 : 0;
     const int m = (int)wave_incl_umax((uint32_t)mine[0]) - 1;
     return max(m, carry);
 #endif

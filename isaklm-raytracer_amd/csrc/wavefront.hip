@@ -377,7 +377,7 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_TRACE_WAVES) wf_trace_coop(RtDevS
     __shared__ float s_entry[WF_LDS_STACK * WF_BLOCK];
     __shared__ unsigned long long s_key[WF_BLOCK];
     __shared__ CoopCand s_list[(WF_BLOCK / 64) * WF_COOP_LIST];
-    __shared__ int s_mark[WF_BLOCK];
+    __shared__ int s_mark[2 * WF_BLOCK]; // 128 per wave: chunk_owner marks + junk slots
     const int tid = threadIdx.x;
     const int gtid = blockIdx.x * WF_BLOCK + tid;
     const int lane = __lane_id();
@@ -385,7 +385,7 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_TRACE_WAVES) wf_trace_coop(RtDevS
     Stack<WF_LDS_STACK> stk{s_node + tid, s_entry + tid, WF_BLOCK, st.spill + gtid, st.spill_threads};
     unsigned long long *wkey = s_key + wave * 64;
     CoopCand *list = s_list + wave * WF_COOP_LIST;
-    const CoopLds w{wkey, list, s_mark + wave * 64};
+    const CoopLds w{wkey, list, s_mark + wave * 128};
     Cnt c;
     if (COUNT) c.zero();
     const uint32_t n = st.counts[q];
@@ -673,7 +673,7 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_finish_coop(RtDevScene sc, RtDevF
     __shared__ float s_entry[WF_LDS_STACK * WF_BLOCK];
     __shared__ unsigned long long s_key[WF_BLOCK];
     __shared__ CoopCand s_list[(WF_BLOCK / 64) * WF_COOP_LIST];
-    __shared__ int s_mark[WF_BLOCK];
+    __shared__ int s_mark[2 * WF_BLOCK]; // 128 per wave: chunk_owner marks + junk slots
     __shared__ WideItem s_wide[(WF_BLOCK / 64) * WIDE_CAP];
     const int tid = threadIdx.x;
     const int gtid = blockIdx.x * WF_BLOCK + tid;
@@ -682,7 +682,7 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_finish_coop(RtDevScene sc, RtDevF
     Stack<WF_LDS_STACK> stk{s_node + tid, s_entry + tid, WF_BLOCK, st.spill + gtid, st.spill_threads};
     unsigned long long *wkey = s_key + wave * 64;
     CoopCand *list = s_list + wave * WF_COOP_LIST;
-    const CoopLds w{wkey, list, s_mark + wave * 64};
+    const CoopLds w{wkey, list, s_mark + wave * 128};
     Cnt c;
     if (COUNT) c.zero();
     const uint32_t n = st.counts[q];
@@ -794,11 +794,11 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_long(RtDevScene sc, RtDevFrame fr
 {
     __shared__ WideItem s_wide[(WF_BLOCK / 64) * WIDE_CAP];
     __shared__ unsigned long long s_key[(WF_BLOCK / 64) * 4];
-    __shared__ int s_mark[WF_BLOCK];
+    __shared__ int s_mark[2 * WF_BLOCK]; // 128 per wave: chunk_owner marks + junk slots
     const int lane = __lane_id();
     const int wave = threadIdx.x >> 6;
     const WideLds W{s_wide + wave * WIDE_CAP, WIDE_CAP, s_key + wave * 4,
-                    reinterpret_cast<float *>(s_key + wave * 4 + 1), s_mark + wave * 64};
+                    reinterpret_cast<float *>(s_key + wave * 4 + 1), s_mark + wave * 128};
     Cnt c;
     if (COUNT) c.zero();
     const int limit = fr.max_depth > 0 ? fr.max_depth : RT_WATCHDOG_BOUNCES;
