@@ -142,7 +142,11 @@ __device__ __forceinline__ bool coop_descend(const RtDevScene &sc, CoopRay &r, S
     // dynamically indexed (scratch) load
     const float ox = r.o.x, oy = r.o.y, oz = r.o.z, dx = r.d.x, dy = r.d.y, dz = r.d.z;
     const float yx = r.yx, yy = r.yy, yz = r.yz;
-    for (int k = 0; k < cap; ++k) {
+    // one flag per lane instead of early returns: the loop has a single
+    // (wave-uniform) exit, which keeps the exec-mask bookkeeping small
+    bool act = r.live && !r.pend, ended = false;
+    for (int k = 0; k < cap && __any(act); ++k) {
+        if (!act) continue;
         const uint2 nd = *reinterpret_cast<const uint2 *>(sc.nodes + 2 * (size_t)r.node);
         if (COUNT) c.v[RT_CNT_NODE]++;
         if ((nd.y & 3u) == RT_LEAF_TAG) {
@@ -152,13 +156,14 @@ __device__ __forceinline__ bool coop_descend(const RtDevScene &sc, CoopRay &r, S
                 r.leaf_begin = nd.x;
                 r.leaf_count = cnt;
                 if (COUNT) c.v[RT_CNT_TRI] += (unsigned long long)cnt;
-                return false;
-            }
-            if (r.sp == 0) {
+                act = false;
+            } else if (r.sp == 0) {
                 r.live = false;
-                return true;
+                ended = true;
+                act = false;
+            } else {
+                coop_pop(r, stk);
             }
-            coop_pop(r, stk);
             continue;
         }
         const uint32_t axis = nd.y & 3u;
@@ -183,7 +188,7 @@ __device__ __forceinline__ bool coop_descend(const RtDevScene &sc, CoopRay &r, S
             r.exit_ = t;
         }
     }
-    return false;
+    return ended;
 }
 
 // The wave-cooperative test of every pending lane's leaf (call with all 64
