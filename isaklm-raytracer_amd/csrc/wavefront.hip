@@ -38,8 +38,8 @@ using namespace rtk;
 #endif
 #define WF_TAIL_DEFAULT 65536u       // RtOptions.wf_tail
 #define WF_FINISH_WAVES_DEFAULT 2048u // RtOptions.wf_finish_waves
-#define WF_DESCENT_CAP_DEFAULT 8      // RtOptions.wf_descent_cap
-#define WF_POSTPONE_DEFAULT 32        // RtOptions.wf_postpone
+#define WF_DESCENT_CAP_DEFAULT 5      // RtOptions.wf_descent_cap
+#define WF_POSTPONE_DEFAULT 20        // RtOptions.wf_postpone
 #define WF_TIMELINE_LAUNCHES 4096     // debug timeline: 3 u64 per trace launch in RtOptions.wave_times_device
 #define WF_WIDE_TAIL_LANES 32         // RtOptions.wf_wide > 0
 #define WF_MAX_PIPES 6                // concurrent pipelines (RtOptions.wf_pipelines); more than 3 need GPU_MAX_HW_QUEUES > 4
