@@ -1035,7 +1035,9 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return -1;
     Workspace &w = g_ws[dev];
-    const int grid = 2048; // persistent-ish grid for trace/shade (grid-stride over the queue)
+    // persistent-ish grid for trace/shade (grid-stride over the queue); RT_WF_GRID overrides (experiments)
+    static const int grid_env = getenv("RT_WF_GRID") ? atoi(getenv("RT_WF_GRID")) : 0;
+    const int grid = grid_env >= 256 && grid_env <= 16384 ? grid_env : 1536; // = 6 blocks x 256 CUs
     const size_t slots = (size_t)fr.width * fr.height;
     const bool count = fr.counters != nullptr;
     const bool prof = profile != 0;
