@@ -155,8 +155,8 @@ const char *rt_version(void);
 /* ---------------- texture decoding ----------------
  * stbi_load(path, &w, &h, &n, 4) as make_texture (rt/scene.cuh:25-63) calls
  * it: RGBA8 rows in file order (no flip).  PNG (all colour types / depths,
- * Adam7, tRNS) and baseline / extended-sequential JPEG, bit-identical to
- * stb_image v2.28; other formats and progressive JPEG -> RT_E_UNSUPPORTED.
+ * Adam7, tRNS) and baseline / extended-sequential / progressive JPEG,
+ * bit-identical to stb_image v2.28; other formats -> RT_E_UNSUPPORTED.
  * The pixels are a host array (rt_host_free).  rt_host_scene_load_mesh decodes
  * a material's `texture` with it, and rt_create_scene uploads each texture
  * with width + 1 zero texels after the image: mod(uv, 1) can return 1.0, so

@@ -12,7 +12,7 @@
 //    g,g,g,255; low bit depth grey scaled by 0xff/0x55/0x11; 16 -> 8 bit by
 //    v >> 8; tRNS colour key -> alpha 0).  Inflate is written here (RFC 1951);
 //    like stb, the zlib Adler-32 and the chunk CRCs are not verified.
-//  * JPEG, baseline and extended-sequential Huffman (SOF0/SOF1): the
+//  * JPEG, baseline, extended-sequential and progressive Huffman (SOF0-2): the
 //    arithmetic follows stb's pipeline, because a JPEG decoder's output is
 //    defined by its IDCT, upsampler and colour conversion: dequantise into
 //    16-bit coefficients, the jidctint-derived integer IDCT with 12-bit
@@ -20,8 +20,9 @@
 //    "fancy" upsampling for h2v1 / h1v2 / h2v2 (:3487-3550) and nearest for
 //    other ratios (:3668), the reduced-precision fixed-point YCbCr->RGB
 //    (:3679-3705), Adobe/JFIF/'RGB' colour-space rules and CMYK/YCCK via the
-//    8x8 "blinn" product (:3881-4040).  Progressive JPEG (SOF2) is reported
-//    as unsupported.
+//    8x8 "blinn" product (:3881-4040); progressive JPEG (SOF2) with stb's
+//    spectral-selection / successive-approximation decode (:2269-2425,
+//    :3097-3114).
 //
 // Pinned against stb_image itself: tests/test_textures.py compares every
 // texture the reference ships plus synthetic PNG/JPEG variants with
@@ -519,6 +520,8 @@ struct JComp {
     int id, h, v, tq, hd, ha, dc_pred;
     int x, y, w2, h2;
     std::vector<uint8_t> data;
+    std::vector<short> coeff; // progressive: 64 coefficients per block, coeff_w blocks per row
+    int coeff_w;
 };
 
 struct Jpeg {
@@ -534,6 +537,7 @@ struct Jpeg {
     JComp comp[4];
     int img_x = 0, img_y = 0, img_n = 0, h_max = 1, v_max = 1, mcu_x = 0, mcu_y = 0;
     int scan_n = 0, order[4] = {0, 0, 0, 0};
+    int spec_start = 0, spec_end = 63, succ_high = 0, succ_low = 0, eob_run = 0; // progressive scans
     int restart_interval = 0, todo = 0;
     int jfif = 0, app14 = -1, rgb = 0, progressive = 0;
     uint32_t code_buffer = 0;
@@ -593,8 +597,28 @@ struct Jpeg {
                                      -255, -511, -1023, -2047, -4095, -8191, -16383, -32767};
         return (int)k + (bias[nb] & (sgn - 1));
     }
+    int get_bits(int nb) // unsigned bits (stbi__jpeg_get_bits)
+    {
+        if (code_bits < nb) grow();
+        if (code_bits < nb) return 0;
+        uint32_t k = (code_buffer << nb) | (code_buffer >> ((32 - nb) & 31));
+        const uint32_t mask = (1u << nb) - 1u;
+        code_buffer = k & ~mask;
+        code_bits -= nb;
+        return (int)(k & mask);
+    }
+    int get_bit()
+    {
+        if (code_bits < 1) grow();
+        if (code_bits < 1) return 0;
+        const uint32_t k = code_buffer;
+        code_buffer <<= 1;
+        --code_bits;
+        return (k & 0x80000000u) ? 1 : 0;
+    }
     void reset()
     {
+        eob_run = 0;
         code_bits = 0;
         code_buffer = 0;
         nomore = false;
@@ -620,6 +644,9 @@ struct Jpeg {
         return false;
     }
     bool decode_block(short *data, int b);
+    bool decode_block_prog_dc(short *data, int b);
+    bool decode_block_prog_ac(short *data, int b);
+    void finish();
     bool process_marker(int m);
     bool frame_header();
     bool scan_header();
@@ -664,6 +691,110 @@ bool Jpeg::decode_block(short *data, int b)
             data[zig] = (short)(extend_receive(s) * dq[zig]);
         }
     } while (k < 64);
+    return true;
+}
+
+// progressive JPEG (stb_image.h:2269-2425): DC first / refinement, AC first
+// (with end-of-band runs) / refinement; coefficients are kept per block and
+// dequantised + transformed once all scans are in (finish)
+bool Jpeg::decode_block_prog_dc(short *data, int b)
+{
+    if (spec_end != 0) return fail("can't merge dc and ac");
+    if (code_bits < 16) grow();
+    JComp &c = comp[b];
+    if (succ_high == 0) {
+        const JHuff &hd = hdc[c.hd];
+        if (!hd.ok) return fail("missing Huffman table");
+        memset(data, 0, 64 * sizeof(short));
+        const int t = huff_decode(hd);
+        if (t < 0 || t > 15) return fail("can't merge dc and ac");
+        const int diff = t ? extend_receive(t) : 0;
+        if (!add_ok(c.dc_pred, diff)) return fail("bad delta");
+        const int dc = c.dc_pred + diff;
+        c.dc_pred = dc;
+        if (!mul_short_ok(dc, 1 << succ_low)) return fail("can't merge dc and ac");
+        data[0] = (short)(dc * (1 << succ_low));
+    } else if (get_bit()) {
+        data[0] = (short)(data[0] + (1 << succ_low));
+    }
+    return true;
+}
+
+bool Jpeg::decode_block_prog_ac(short *data, int b)
+{
+    if (spec_start == 0) return fail("can't merge dc and ac");
+    const JHuff &ha = hac[comp[b].ha];
+    if (!ha.ok) return fail("missing Huffman table");
+    if (succ_high == 0) {
+        const int shift = succ_low;
+        if (eob_run) {
+            --eob_run;
+            return true;
+        }
+        int k = spec_start;
+        do {
+            if (code_bits < 16) grow();
+            const int rs = huff_decode(ha);
+            if (rs < 0) return fail("bad huffman code");
+            const int s = rs & 15, r = rs >> 4;
+            if (s == 0) {
+                if (r < 15) {
+                    eob_run = 1 << r;
+                    if (r) eob_run += get_bits(r);
+                    --eob_run;
+                    break;
+                }
+                k += 16;
+            } else {
+                k += r;
+                const int zig = kDezigzag[k++];
+                data[zig] = (short)(extend_receive(s) * (1 << shift));
+            }
+        } while (k <= spec_end);
+        return true;
+    }
+    // refinement of these AC coefficients
+    const short bit = (short)(1 << succ_low);
+    auto refine = [&](short *p) {
+        if (get_bit() && (*p & bit) == 0) *p = (short)(*p > 0 ? *p + bit : *p - bit);
+    };
+    if (eob_run) {
+        --eob_run;
+        for (int k = spec_start; k <= spec_end; ++k) {
+            short *p = &data[kDezigzag[k]];
+            if (*p != 0) refine(p);
+        }
+        return true;
+    }
+    int k = spec_start;
+    do {
+        const int rs = huff_decode(ha);
+        if (rs < 0) return fail("bad huffman code");
+        int s = rs & 15, r = rs >> 4;
+        if (s == 0) {
+            if (r < 15) {
+                eob_run = (1 << r) - 1;
+                if (r) eob_run += get_bits(r);
+                r = 64; // the rest of the band: refinement bits only
+            }
+            // r == 15: a run of 16 zeros (15 skipped, then s = 0 written)
+        } else {
+            if (s != 1) return fail("bad huffman code");
+            s = get_bit() ? bit : -bit;
+        }
+        while (k <= spec_end) {
+            short *p = &data[kDezigzag[k++]];
+            if (*p != 0) {
+                refine(p);
+            } else {
+                if (r == 0) {
+                    *p = (short)s;
+                    break;
+                }
+                --r;
+            }
+        }
+    } while (k <= spec_end);
     return true;
 }
 
@@ -870,6 +1001,10 @@ bool Jpeg::frame_header()
         k.w2 = mcu_x * k.h * 8;
         k.h2 = mcu_y * k.v * 8;
         k.data.assign((size_t)k.w2 * k.h2, 0);
+        if (progressive) {
+            k.coeff_w = k.w2 / 8;
+            k.coeff.assign((size_t)k.w2 * k.h2, 0); // 64 per 8x8 block
+        }
     }
     return true;
 }
@@ -892,16 +1027,61 @@ bool Jpeg::scan_header()
         if (comp[which].ha > 3) return fail("bad AC huff");
         order[i] = which;
     }
-    const int ss = get8();
-    get8(); // spectral end (63 for sequential)
+    spec_start = get8();
+    spec_end = get8(); // 63 for sequential, but might be 0
     const int aa = get8();
-    if (ss != 0 || aa != 0) return fail("bad SOS");
+    succ_high = aa >> 4;
+    succ_low = aa & 15;
+    if (progressive) {
+        if (spec_start > 63 || spec_end > 63 || spec_start > spec_end || succ_high > 13 || succ_low > 13)
+            return fail("bad SOS");
+    } else {
+        if (spec_start != 0 || succ_high != 0 || succ_low != 0) return fail("bad SOS");
+        spec_end = 63;
+    }
     return true;
 }
 
 bool Jpeg::entropy_data()
 {
     reset();
+    if (progressive) {
+        if (scan_n == 1) {
+            const int nn = order[0];
+            JComp &c = comp[nn];
+            const int w = (c.x + 7) >> 3, h = (c.y + 7) >> 3;
+            for (int j = 0; j < h; ++j)
+                for (int i = 0; i < w; ++i) {
+                    short *data = c.coeff.data() + 64 * ((size_t)i + (size_t)j * c.coeff_w);
+                    if (spec_start == 0 ? !decode_block_prog_dc(data, nn) : !decode_block_prog_ac(data, nn))
+                        return false;
+                    if (--todo <= 0) {
+                        if (code_bits < 24) grow();
+                        if (!(marker >= 0xd0 && marker <= 0xd7)) return true;
+                        reset();
+                    }
+                }
+            return true;
+        }
+        for (int j = 0; j < mcu_y; ++j)
+            for (int i = 0; i < mcu_x; ++i) {
+                for (int k = 0; k < scan_n; ++k) {
+                    const int nn = order[k];
+                    JComp &c = comp[nn];
+                    for (int y = 0; y < c.v; ++y)
+                        for (int x = 0; x < c.h; ++x) {
+                            const size_t x2 = (size_t)i * c.h + x, y2 = (size_t)j * c.v + y;
+                            if (!decode_block_prog_dc(c.coeff.data() + 64 * (x2 + y2 * c.coeff_w), nn)) return false;
+                        }
+                }
+                if (--todo <= 0) {
+                    if (code_bits < 24) grow();
+                    if (!(marker >= 0xd0 && marker <= 0xd7)) return true;
+                    reset();
+                }
+            }
+        return true;
+    }
     short data[64];
     if (scan_n == 1) {
         const int nn = order[0];
@@ -938,6 +1118,22 @@ bool Jpeg::entropy_data()
             }
         }
     return true;
+}
+
+// progressive: dequantise and transform the blocks inside each component
+// (stbi__jpeg_finish, stb_image.h:3097-3114)
+void Jpeg::finish()
+{
+    for (int n = 0; n < img_n; ++n) {
+        JComp &c = comp[n];
+        const int w = (c.x + 7) >> 3, h = (c.y + 7) >> 3;
+        for (int j = 0; j < h; ++j)
+            for (int i = 0; i < w; ++i) {
+                short *data = c.coeff.data() + 64 * ((size_t)i + (size_t)j * c.coeff_w);
+                for (int t = 0; t < 64; ++t) data[t] = (short)(data[t] * dequant[c.tq][t]);
+                idct_block(c.data.data() + (size_t)c.w2 * j * 8 + i * 8, c.w2, data);
+            }
+    }
 }
 
 // ---- upsampling (one output row from the component's near/far rows)
@@ -1037,10 +1233,7 @@ int jpeg_decode(const uint8_t *p, size_t n, std::vector<uint8_t> &rgba, int &w, 
             m = j.get_marker();
         }
     }
-    if (m == 0xC2) {
-        err = "progressive JPEG not supported";
-        return RT_E_UNSUPPORTED;
-    }
+    j.progressive = m == 0xC2;
     if (!j.frame_header()) return bad(j.err);
     m = j.get_marker();
     while (m != 0xD9) {
@@ -1077,6 +1270,7 @@ int jpeg_decode(const uint8_t *p, size_t n, std::vector<uint8_t> &rgba, int &w, 
             m = j.get_marker();
         }
     }
+    if (j.progressive) j.finish();
     // ---- resample + colour convert to RGBA (load_jpeg_image, n = 4)
     const int is_rgb = j.img_n == 3 && (j.rgb == 3 || (j.app14 == 0 && !j.jfif));
     const int decode_n = j.img_n;

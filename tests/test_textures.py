@@ -56,11 +56,23 @@ def _expect(fn, code):
     assert f"({code})" in str(e.value) or str(code) in str(e.value), str(e.value)
 
 
-def test_progressive_jpeg_is_unsupported():
+def test_arithmetic_coded_jpeg_is_rejected():
+    """SOF9 (arithmetic coding) is not decoded, by stb_image either ("unknown marker")."""
     data = bytearray(VARIANTS["jpeg_ycc444"])
     k = data.index(b"\xff\xc0")
-    data[k + 1] = 0xC2
-    _expect(lambda: rt.decode_image(data=bytes(data)), -5)
+    data[k + 1] = 0xC9
+    _expect(lambda: rt.decode_image(data=bytes(data)), -4)
+
+
+def test_progressive_equals_baseline_of_same_coefficients():
+    """A progressive stream (spectral selection + successive approximation,
+    EOB runs, refinement scans) carries the same quantised coefficients as the
+    baseline stream of the same image, so both decode to the same pixels."""
+    for name in ("prog_ycc420", "prog_ycc422_big", "prog_grey"):
+        kw = dict(texture_fixtures.JPEG_VARIANTS[name])
+        kw["progressive"] = False
+        np.testing.assert_array_equal(rt.decode_image(data=VARIANTS["jpeg_" + name]),
+                                      rt.decode_image(data=texture_fixtures.jpeg(**kw)))
 
 
 def test_unknown_format_is_unsupported():

@@ -213,8 +213,9 @@ def _magnitude(v):
 
 
 def jpeg(w, h, sampling=((1, 1), (1, 1), (1, 1)), quality=75, restart=0, interleaved=True, kind="ycc",
-         q16=False, seed=2):
-    """Returns baseline JPEG bytes.  kind: 'ycc' (JFIF), 'grey', 'rgb' (ids R,G,B, no JFIF), 'cmyk' (Adobe 0)."""
+         q16=False, seed=2, progressive=False):
+    """Returns baseline (or progressive) JPEG bytes.  kind: 'ycc' (JFIF), 'grey', 'rgb' (ids R,G,B, no JFIF),
+    'cmyk' (Adobe 0)."""
     nc = {"ycc": 3, "grey": 1, "rgb": 3, "cmyk": 4}[kind]
     sampling = list(sampling)[:nc] + [(1, 1)] * max(0, nc - len(sampling))
     img = _pattern(h, w, 4, seed).astype(np.float64)
@@ -270,6 +271,8 @@ def jpeg(w, h, sampling=((1, 1), (1, 1), (1, 1)), quality=75, restart=0, interle
     sof = struct.pack(">BHHB", 8, h, w, nc)
     for k in range(nc):
         sof += bytes([ids[k], (sampling[k][0] << 4) | sampling[k][1], comps[k]["q"]])
+    if progressive:
+        return out + seg(0xC2, sof) + _progressive_scans(comps, ids, w, h, hmax, vmax, mcux, mcuy, seg) + b"\xff\xd9"
     out += seg(0xC0, sof)
     for t in range(2 if kind == "ycc" else 1):
         for cls, spec in ((0, (_DC_L, _DC_C)[t]), (1, (_AC_L, _AC_C)[t])):
@@ -346,6 +349,156 @@ def jpeg(w, h, sampling=((1, 1), (1, 1), (1, 1)), quality=75, restart=0, interle
     return out + b"\xff\xd9"
 
 
+# progressive coding (ITU T.81 G.1.2; the encoder side of libjpeg's
+# jcphuff.c restated): one DC table (categories 0-11, 4-bit codes) and one AC
+# table holding every run/size symbol plus EOB0-EOB14 and ZRL (8-bit codes)
+_P_DC = ([0, 0, 0, 12] + [0] * 12, list(range(12)))
+_P_AC_SYMS = [r << 4 for r in range(16)] + [(r << 4) | s for r in range(16) for s in range(1, 11)]
+_P_AC = ([0] * 7 + [len(_P_AC_SYMS)] + [0] * 8, _P_AC_SYMS)
+
+
+def _pt(v, al):
+    """point transform of an AC coefficient: magnitude >> al, sign kept"""
+    return -((-v) >> al) if v < 0 else v >> al
+
+
+def _progressive_scans(comps, ids, w, h, hmax, vmax, mcux, mcuy, seg):
+    dc_t, ac_t = _codes(_P_DC), _codes(_P_AC)
+    out = seg(0xC4, bytes([0x00]) + bytes(_P_DC[0]) + bytes(_P_DC[1]))
+    out += seg(0xC4, bytes([0x10]) + bytes(_P_AC[0]) + bytes(_P_AC[1]))
+    nc = len(comps)
+    zz = [c["coef"][..., _ZIGZAG].astype(np.int64) for c in comps]  # [by, bx, 64] in zigzag order
+
+    def blocks_of(k):  # a non-interleaved scan covers the component's own blocks only
+        c = comps[k]
+        cx = -(-(-(-w * c["h"] // hmax)) // 8)
+        cy = -(-(-(-h * c["v"] // vmax)) // 8)
+        return [(by, bx) for by in range(cy) for bx in range(cx)]
+
+    def header(members, ss, se, ah, al):
+        d = struct.pack(">B", len(members))
+        for k in members:
+            d += bytes([ids[k], 0x00])
+        return d + bytes([ss, se, (ah << 4) | al])
+
+    def dc_scan(ah, al):
+        bw = _BitWriter()
+        pred = [0] * nc
+        for my in range(mcuy):
+            for mx in range(mcux):
+                for k, c in enumerate(comps):
+                    for y in range(c["v"]):
+                        for x in range(c["h"]):
+                            v = int(zz[k][my * c["v"] + y, mx * c["h"] + x, 0])
+                            if ah == 0:
+                                t = v >> al  # DC point transform: arithmetic shift
+                                s, m = _magnitude(t - pred[k])
+                                bw.put(*dc_t[s])
+                                if s:
+                                    bw.put(m, s)
+                                pred[k] = t
+                            else:
+                                bw.put((v >> al) & 1, 1)
+        bw.flush()
+        return seg(0xDA, header(list(range(nc)), 0, 0, ah, al)) + bytes(bw.out)
+
+    def ac_first(k, ss, se, al):
+        bw = _BitWriter()
+        st = {"eobrun": 0}
+
+        def flush():
+            if st["eobrun"]:
+                n = st["eobrun"].bit_length() - 1
+                bw.put(*ac_t[n << 4])
+                if n:
+                    bw.put(st["eobrun"] & ((1 << n) - 1), n)
+                st["eobrun"] = 0
+
+        for b in blocks_of(k):
+            v = [_pt(int(x), al) for x in zz[k][b][ss:se + 1]]
+            r = 0
+            for t in v:
+                if t == 0:
+                    r += 1
+                    continue
+                flush()
+                while r > 15:
+                    bw.put(*ac_t[0xF0])
+                    r -= 16
+                s, m = _magnitude(t)
+                bw.put(*ac_t[(r << 4) | s])
+                bw.put(m, s)
+                r = 0
+            if r:
+                st["eobrun"] += 1
+                if st["eobrun"] == 0x7FFF:
+                    flush()
+        flush()
+        bw.flush()
+        return seg(0xDA, header([k], ss, se, 0, al)) + bytes(bw.out)
+
+    def ac_refine(k, ss, se, al):
+        bw = _BitWriter()
+        st = {"eobrun": 0, "be": []}
+
+        def flush():
+            if st["eobrun"]:
+                n = st["eobrun"].bit_length() - 1
+                bw.put(*ac_t[n << 4])
+                if n:
+                    bw.put(st["eobrun"] & ((1 << n) - 1), n)
+                st["eobrun"] = 0
+                for bit in st["be"]:
+                    bw.put(bit, 1)
+                st["be"] = []
+
+        for b in blocks_of(k):
+            coefs = [int(x) for x in zz[k][b][ss:se + 1]]
+            absv = [abs(x) >> al for x in coefs]
+            eob = max([i for i, a in enumerate(absv) if a == 1], default=-1)
+            r, br = 0, []
+            for i, t in enumerate(absv):
+                if t == 0:
+                    r += 1
+                    continue
+                while r > 15 and i <= eob:
+                    flush()
+                    bw.put(*ac_t[0xF0])
+                    r -= 16
+                    for bit in br:
+                        bw.put(bit, 1)
+                    br = []
+                if t > 1:
+                    br.append(t & 1)  # correction bit of a previously nonzero coefficient
+                    continue
+                flush()
+                bw.put(*ac_t[(r << 4) | 1])
+                bw.put(1 if coefs[i] > 0 else 0, 1)
+                for bit in br:
+                    bw.put(bit, 1)
+                br, r = [], 0
+            if r > 0 or br:
+                st["eobrun"] += 1
+                st["be"] += br
+                if st["eobrun"] == 0x7FFF or len(st["be"]) > 900:
+                    flush()
+        flush()
+        bw.flush()
+        return seg(0xDA, header([k], ss, se, al + 1, al)) + bytes(bw.out)
+
+    out += dc_scan(0, 1)
+    out += ac_first(0, 1, 5, 2)
+    for k in range(1, nc):
+        out += ac_first(k, 1, 63, 1)
+    out += ac_first(0, 6, 63, 2)
+    out += ac_refine(0, 1, 63, 1)
+    out += dc_scan(1, 0)
+    for k in range(1, nc):
+        out += ac_refine(k, 1, 63, 0)
+    out += ac_refine(0, 1, 63, 0)
+    return out
+
+
 JPEG_VARIANTS = {
     "ycc444": dict(w=40, h=24),
     "ycc422_odd": dict(w=37, h=23, sampling=((2, 1), (1, 1), (1, 1))),
@@ -362,6 +515,10 @@ JPEG_VARIANTS = {
     "grey_restart": dict(w=64, h=8, kind="grey", restart=2),
     "rgb_ids": dict(w=20, h=20, kind="rgb"),
     "cmyk": dict(w=18, h=22, kind="cmyk"),
+    "prog_ycc420": dict(w=45, h=29, sampling=((2, 2), (1, 1), (1, 1)), quality=90, progressive=True),
+    "prog_ycc444_q100": dict(w=24, h=24, quality=100, progressive=True),
+    "prog_grey": dict(w=37, h=21, kind="grey", progressive=True),
+    "prog_ycc422_big": dict(w=130, h=70, sampling=((2, 1), (1, 1), (1, 1)), quality=60, progressive=True, seed=5),
 }
 
 
