@@ -29,7 +29,9 @@ HEADERS = sorted(os.path.relpath(f, os.path.join(os.path.dirname(os.path.abspath
                                     recursive=True))
 
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-I" + INCLUDE, "-I" + CSRC]
-HOST_FLAGS = ["-fopenmp", "-Wall", "-Wno-unused-function"]
+# -fwrapv: the JPEG IDCT wraps on corrupt coefficients as stb_image's does on
+# the reference's x86 build, instead of signed-overflow UB
+HOST_FLAGS = ["-fopenmp", "-Wall", "-Wno-unused-function", "-fwrapv"]
 HIP_FLAGS = ["--offload-arch=gfx950", "-fno-gpu-rdc", "-munsafe-fp-atomics", "-Wno-unused-command-line-argument"]
 
 
