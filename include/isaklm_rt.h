@@ -190,6 +190,14 @@ int rt_gbuffer_seeds(uint32_t *host_out, size_t count, uint64_t skip);
  * seeds */
 int rt_gbuffer_create(int width, int height, uint64_t seed_skip, G_Buffer *out);
 int rt_gbuffer_destroy(G_Buffer *g);
+/* checkpoint / resume: the G_Buffer is a frame's whole
+ * progressive state (the reference keeps it in device memory only).  Save it
+ * with the caller's sample count; loading it into a G_Buffer of the same size
+ * and calling rt_render with that sample count continues the render bit for
+ * bit.  Errors: RT_E_IO (file), RT_E_PARSE (not a checkpoint / truncated),
+ * RT_E_INVALID (size mismatch). */
+int rt_gbuffer_save(G_Buffer g_buffer, int width, int height, int sample_count, const char *path);
+int rt_gbuffer_load(const char *path, G_Buffer g_buffer, int width, int height, int *sample_count_out);
 
 /* ---------------- host scene path ---------------- */
 typedef struct RtHostScene RtHostScene;

@@ -249,6 +249,79 @@ int rt_gbuffer_destroy(G_Buffer *g)
     return RT_OK;
 }
 
+// ---------------- checkpoint / resume ----------------
+// file: "RTGBUF01", int32 width, height, sample_count, 0; then fb (12 B/px),
+// sq, count, rng (4 B/px each), host byte order
+static const char kGbufMagic[8] = {'R', 'T', 'G', 'B', 'U', 'F', '0', '1'};
+
+int rt_gbuffer_save(G_Buffer g, int width, int height, int sample_count, const char *path)
+{
+    if (!path || width <= 0 || height <= 0 || !g.frame_buffer || !g.squared_luminance || !g.sample_count ||
+        !g.random_numbers) {
+        rt_set_error("rt_gbuffer_save: bad arguments");
+        return RT_E_INVALID;
+    }
+    const size_t n = (size_t)width * height;
+    std::vector<uint8_t> buf(n * 24);
+    HIPCHK(hipMemcpy(buf.data(), g.frame_buffer, n * 12, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(buf.data() + n * 12, g.squared_luminance, n * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(buf.data() + n * 16, g.sample_count, n * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(buf.data() + n * 20, g.random_numbers, n * 4, hipMemcpyDeviceToHost));
+    FILE *f = fopen(path, "wb");
+    if (!f) {
+        rt_set_error("rt_gbuffer_save: cannot write %s", path);
+        return RT_E_IO;
+    }
+    const int32_t hdr[4] = {width, height, sample_count, 0};
+    const bool ok = fwrite(kGbufMagic, 1, 8, f) == 8 && fwrite(hdr, 4, 4, f) == 4 &&
+                    fwrite(buf.data(), 1, buf.size(), f) == buf.size();
+    if (fclose(f) != 0 || !ok) {
+        rt_set_error("rt_gbuffer_save: write error on %s", path);
+        return RT_E_IO;
+    }
+    return RT_OK;
+}
+
+int rt_gbuffer_load(const char *path, G_Buffer g, int width, int height, int *sample_count_out)
+{
+    if (!path) {
+        rt_set_error("rt_gbuffer_load: null path");
+        return RT_E_INVALID;
+    }
+    FILE *f = fopen(path, "rb");
+    if (!f) {
+        rt_set_error("rt_gbuffer_load: cannot read %s", path);
+        return RT_E_IO;
+    }
+    char magic[8];
+    int32_t hdr[4];
+    if (fread(magic, 1, 8, f) != 8 || memcmp(magic, kGbufMagic, 8) != 0 || fread(hdr, 4, 4, f) != 4) {
+        fclose(f);
+        rt_set_error("rt_gbuffer_load: %s is not a G_Buffer checkpoint", path);
+        return RT_E_PARSE;
+    }
+    if (hdr[0] != width || hdr[1] != height || !g.frame_buffer || !g.squared_luminance || !g.sample_count ||
+        !g.random_numbers) {
+        fclose(f);
+        rt_set_error("rt_gbuffer_load: checkpoint is %dx%d, G_Buffer %dx%d", hdr[0], hdr[1], width, height);
+        return RT_E_INVALID;
+    }
+    const size_t n = (size_t)width * height;
+    std::vector<uint8_t> buf(n * 24);
+    const bool ok = fread(buf.data(), 1, buf.size(), f) == buf.size();
+    fclose(f);
+    if (!ok) {
+        rt_set_error("rt_gbuffer_load: %s is truncated", path);
+        return RT_E_PARSE;
+    }
+    HIPCHK(hipMemcpy(g.frame_buffer, buf.data(), n * 12, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(g.squared_luminance, buf.data() + n * 12, n * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(g.sample_count, buf.data() + n * 16, n * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(g.random_numbers, buf.data() + n * 20, n * 4, hipMemcpyHostToDevice));
+    if (sample_count_out) *sample_count_out = hdr[2];
+    return RT_OK;
+}
+
 // ---------------- host scene ----------------
 int rt_host_scene_create(RtHostScene **out)
 {

@@ -105,6 +105,8 @@ def lib():
         L.rt_set_device.argtypes = [i]
         L.rt_host_free.argtypes = [vp]
         L.rt_host_free.restype = None
+        L.rt_gbuffer_save.argtypes = [G_Buffer, i, i, i, ctypes.c_char_p]
+        L.rt_gbuffer_load.argtypes = [ctypes.c_char_p, G_Buffer, i, i, ctypes.POINTER(i)]
         L.rt_decode_image.argtypes = [ctypes.c_char_p, ctypes.POINTER(vp), ctypes.POINTER(i), ctypes.POINTER(i)]
         L.rt_decode_image_memory.argtypes = [vp, sz, ctypes.POINTER(vp), ctypes.POINTER(i), ctypes.POINTER(i)]
         L.rt_gbuffer_seeds.argtypes = [vp, sz, ctypes.c_uint64]
@@ -291,6 +293,16 @@ class GBuffer:
         check(L.rt_upload(self.g.squared_luminance, _ptr(sq), sq.nbytes))
         check(L.rt_upload(self.g.sample_count, _ptr(cnt), cnt.nbytes))
         check(L.rt_upload(self.g.random_numbers, _ptr(rng), rng.nbytes))
+
+    def save(self, path, sample_count):
+        """checkpoint (rt_gbuffer_save): the whole progressive state + the caller's sample count"""
+        check(lib().rt_gbuffer_save(self.g, self.width, self.height, sample_count, str(path).encode()))
+
+    def load(self, path):
+        """resume (rt_gbuffer_load); returns the saved sample count"""
+        sc = ctypes.c_int()
+        check(lib().rt_gbuffer_load(str(path).encode(), self.g, self.width, self.height, ctypes.byref(sc)))
+        return sc.value
 
     def free(self):
         if getattr(self, "g", None) is not None and self.g.frame_buffer:

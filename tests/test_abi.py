@@ -101,3 +101,18 @@ def test_ctypes_binding_matches_header_layout(tmp_path):
         cls = structs[cname]
         want = ctypes.sizeof(cls) if fname == "size" else getattr(cls, fname).offset
         assert int(val) == want, (cname, fname, int(val), want)
+
+
+def test_gbuffer_checkpoint_errors(tmp_path):
+    """rt_gbuffer_load rejects what is not a matching checkpoint before touching
+    the device (no GPU needed)."""
+    import struct
+
+    L = rt.lib()
+    g = rt.G_Buffer()
+    sc = ctypes.c_int()
+    assert L.rt_gbuffer_load(str(tmp_path / "missing.gbuf").encode(), g, 4, 4, ctypes.byref(sc)) == -3
+    (tmp_path / "junk.gbuf").write_bytes(b"not a checkpoint at all")
+    assert L.rt_gbuffer_load(str(tmp_path / "junk.gbuf").encode(), g, 4, 4, ctypes.byref(sc)) == -4
+    (tmp_path / "other.gbuf").write_bytes(b"RTGBUF01" + struct.pack("<4i", 5, 5, 7, 0) + bytes(25 * 24))
+    assert L.rt_gbuffer_load(str(tmp_path / "other.gbuf").encode(), g, 4, 4, ctypes.byref(sc)) == -1  # RT_E_INVALID

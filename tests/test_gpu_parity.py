@@ -150,6 +150,23 @@ def test_textured_scene_bitwise(kernel, tmp_path):
     assert rcnt["texel"] > 0
 
 
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_checkpoint_resume_bitwise(cornell, kernel, tmp_path):
+    """rt_gbuffer_save after 3 passes, rt_gbuffer_load into a fresh G_Buffer
+    (other seeds), 4 more passes == 7 passes in one G_Buffer (adaptive on)."""
+    W, H = 40, 24
+    opt = lambda p: rt.options(W, H, p, adaptive=True, min_samples=4, kernel=kernel)  # noqa: E731
+    a = rt.GBuffer(W, H)
+    rt.render(cornell.dev, a, cornell.camera, 0, opt(3))
+    a.save(tmp_path / "ck.gbuf", 3)
+    b = rt.GBuffer(W, H, seed_skip=12345)
+    assert b.load(tmp_path / "ck.gbuf") == 3
+    rt.render(cornell.dev, b, cornell.camera, 3, opt(4))
+    c = rt.GBuffer(W, H)
+    rt.render(cornell.dev, c, cornell.camera, 0, opt(7))
+    helpers.assert_bitwise(b.download(), c.download(), what="resume")
+
+
 def test_kernels_agree_multi_call(cornell):
     """Megakernel and wavefront give the same bits across calls with reset."""
     W, H = 33, 31
