@@ -12,6 +12,10 @@
 //                  [--spp N] [--passes P] [--adaptive 0|1] [--min-samples N]
 //                  [--tolerance T] [--max-depth D] [--kernel mega|wavefront]
 //                  [--shard G N] [--device D] [--out PNG] [--quiet]
+//                  [--checkpoint FILE] [--resume FILE]
+// --checkpoint writes the G_Buffer + sample count after every rt_render call
+// (rt_gbuffer_save); --resume continues from such a file (rt_gbuffer_load),
+// bit-identical to a render that never stopped.
 // Defaults are the reference's macros (rt/macros.h): 1920x1080, MAX_SAMPLES
 // 5000, MIN_SAMPLES 100, MAX_TOLERANCE 0.05, adaptive sampling on.
 #include <stdio.h>
@@ -36,14 +40,15 @@ void usage()
     fprintf(stderr,
             "usage: rt_render [--scene FILE | --generate NAME DIR] [--width W] [--height H] [--spp N]\n"
             "                 [--passes P] [--adaptive 0|1] [--min-samples N] [--tolerance T] [--max-depth D]\n"
-            "                 [--kernel mega|wavefront] [--shard G N] [--device D] [--out PNG] [--quiet]\n");
+            "                 [--kernel mega|wavefront] [--shard G N] [--device D] [--out PNG] [--quiet]\n"
+            "                 [--checkpoint FILE] [--resume FILE]\n");
 }
 
 } // namespace
 
 int main(int argc, char **argv)
 {
-    std::string scene_path, gen_name, gen_dir, out = "render.png";
+    std::string scene_path, gen_name, gen_dir, out = "render.png", checkpoint, resume;
     int width = 1920, height = 1080, spp = 5000, passes = 64, adaptive = 1, min_samples = 100, max_depth = 0;
     int device = 0, shard_id = 0, num_shards = 1, kernel = RT_KERNEL_WAVEFRONT;
     float tolerance = 0.05f;
@@ -72,6 +77,8 @@ int main(int argc, char **argv)
         else if (a == "--device") device = atoi(next());
         else if (a == "--out") out = next();
         else if (a == "--quiet") quiet = true;
+        else if (a == "--checkpoint") checkpoint = next();
+        else if (a == "--resume") resume = next();
         else {
             usage();
             return 2;
@@ -121,10 +128,16 @@ int main(int argc, char **argv)
     // the frame loop (rt/main.cu:114-155): call_render, ++sample_count, save at MAX_SAMPLES
     const auto t1 = std::chrono::steady_clock::now();
     int sample_count = 0;
+    if (!resume.empty()) {
+        if (rt_gbuffer_load(resume.c_str(), g_buffer, width, height, &sample_count) != RT_OK) return fail("resume");
+        if (!quiet) printf("resumed at %d samples per pixel\n", sample_count);
+    }
     while (sample_count < spp) {
         opt.passes = passes < spp - sample_count ? passes : spp - sample_count;
         if (rt_render(prepared, g_buffer, camera, sample_count, &opt) != RT_OK) return fail("render");
         sample_count += opt.passes;
+        if (!checkpoint.empty() && rt_gbuffer_save(g_buffer, width, height, sample_count, checkpoint.c_str()) != RT_OK)
+            return fail("checkpoint");
         if (!quiet) printf("samples per pixel: %d\n", sample_count);
     }
     if (rt_synchronize() != RT_OK) return fail("synchronize");

@@ -263,19 +263,24 @@ int rt_gbuffer_save(G_Buffer g, int width, int height, int sample_count, const c
     }
     const size_t n = (size_t)width * height;
     std::vector<uint8_t> buf(n * 24);
+    HIPCHK(hipDeviceSynchronize()); // rt_render's pipelines run on their own non-blocking streams
     HIPCHK(hipMemcpy(buf.data(), g.frame_buffer, n * 12, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(buf.data() + n * 12, g.squared_luminance, n * 4, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(buf.data() + n * 16, g.sample_count, n * 4, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(buf.data() + n * 20, g.random_numbers, n * 4, hipMemcpyDeviceToHost));
-    FILE *f = fopen(path, "wb");
+    // write beside the target and rename over it: an interrupted save never
+    // leaves a torn checkpoint in place of the previous one
+    const std::string tmp = std::string(path) + ".tmp";
+    FILE *f = fopen(tmp.c_str(), "wb");
     if (!f) {
-        rt_set_error("rt_gbuffer_save: cannot write %s", path);
+        rt_set_error("rt_gbuffer_save: cannot write %s", tmp.c_str());
         return RT_E_IO;
     }
     const int32_t hdr[4] = {width, height, sample_count, 0};
     const bool ok = fwrite(kGbufMagic, 1, 8, f) == 8 && fwrite(hdr, 4, 4, f) == 4 &&
                     fwrite(buf.data(), 1, buf.size(), f) == buf.size();
-    if (fclose(f) != 0 || !ok) {
+    if (fclose(f) != 0 || !ok || rename(tmp.c_str(), path) != 0) {
+        remove(tmp.c_str());
         rt_set_error("rt_gbuffer_save: write error on %s", path);
         return RT_E_IO;
     }
@@ -314,6 +319,7 @@ int rt_gbuffer_load(const char *path, G_Buffer g, int width, int height, int *sa
         rt_set_error("rt_gbuffer_load: %s is truncated", path);
         return RT_E_PARSE;
     }
+    HIPCHK(hipDeviceSynchronize()); // no render may still be writing this G_Buffer
     HIPCHK(hipMemcpy(g.frame_buffer, buf.data(), n * 12, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(g.squared_luminance, buf.data() + n * 12, n * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(g.sample_count, buf.data() + n * 16, n * 4, hipMemcpyHostToDevice));

@@ -47,3 +47,24 @@ def test_driver_png_matches_oracle(tmp_path, kernel):
     rgba = oracle.tonemap(fb, cnt).reshape(H, W, 4)[::-1]  # save_render flips (rt/save_render.cuh:55)
     assert np.all(cnt == SPP)
     np.testing.assert_array_equal(png, rgba)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(180)
+def test_driver_checkpoint_resume(tmp_path):
+    """--checkpoint after 6 of 10 spp, then --resume to 10: the PNG equals a
+    straight 10-spp run bit for bit (adaptive sampling on, so the resumed
+    count/sq planes matter)."""
+    W, H = 64, 48
+    scene = helpers.scene_path("cornell")
+    base = [APP, "--scene", scene, "--width", str(W), "--height", str(H), "--passes", "3", "--min-samples", "4",
+            "--quiet"]
+    straight, resumed, ck = tmp_path / "straight.png", tmp_path / "resumed.png", tmp_path / "g.ckpt"
+    for args in (["--spp", "10", "--out", str(straight)],
+                 ["--spp", "6", "--checkpoint", str(ck), "--out", str(tmp_path / "half.png")],
+                 ["--spp", "10", "--resume", str(ck), "--out", str(resumed)]):
+        r = subprocess.run(base + args, capture_output=True, text=True, timeout=150)
+        assert r.returncode == 0, r.stdout + r.stderr
+    assert ck.stat().st_size == 8 + 16 + W * H * 24 and not os.path.exists(str(ck) + ".tmp")
+    np.testing.assert_array_equal(rt.decode_image(str(resumed)), rt.decode_image(str(straight)))
+    assert not np.array_equal(rt.decode_image(str(tmp_path / "half.png")), rt.decode_image(str(straight)))
