@@ -63,6 +63,7 @@ def main():
                   "msamples_s_best": round(W * H * P / ts.min() / 1e6, 3),
                   "s": [round(x, 3) for x in ts], "maxdepth": c["maxdepth"],
                   "trace_ms": [round(p["trace_ms"]) for p in profs[v]],
+                  "shade_ms": [round(p["shade_ms"]) for p in profs[v]],
                   "finish_ms": [round(p["finish_ms"]) for p in profs[v]],
                   "iterations": [p["iterations"] for p in profs[v]],
                   "per_sample": {k: round(c[k] / max(c["sample"], 1), 2) for k in ("ray", "node", "tri", "cand", "plane", "rounds", "chunks", "bary")},
