@@ -1202,6 +1202,12 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
         }
         if (rc != 0) return rc;
         if (hipEventRecord(pp.join, s) != hipSuccess) return -1;
+        if (trace_iters) {
+            (void)hipStreamSynchronize(s);
+            timespec ts;
+            clock_gettime(CLOCK_MONOTONIC, &ts);
+            fprintf(stderr, "[wf] pipe %d finished t %.4f\n", pi, ts.tv_sec + ts.tv_nsec * 1e-9);
+        }
         if (prof) {
             if (!mark(4) || hipEventSynchronize(pp.ev[4]) != hipSuccess) return -1;
             P.trace_launches = P.shade_launches = P.iterations;

@@ -45,7 +45,8 @@ def harness(tmp_path_factory):
         pytest.skip("g++ not available")
     d = tmp_path_factory.mktemp("fuzz")
     exe = str(d / "decode_harness")
-    cmd = ["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined",
+    cmd = ["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined,float-cast-overflow",
+           "-fno-sanitize-recover=undefined,float-cast-overflow",
            "-fno-omit-frame-pointer", "-fwrapv", "-I" + os.path.join(ROOT, "include"), "-I" + CSRC,
            os.path.join(HERE, "fuzz", "decode_harness.cpp"), os.path.join(CSRC, "host", "image_decode.cpp"),
            "-o", exe]

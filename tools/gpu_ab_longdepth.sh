@@ -1,0 +1,8 @@
+# long-path hand-off depth (wf_long_depth) sweep, room2m 64 spp, 3 interleaved rounds
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 600 python -u tools/ab.py room2m 64 0 3 "1:0:0:0:0:0:0:64,1:0:0:0:0:0:0:32,1:0:0:0:0:0:0:16,1:0:0:0:0:0:0:128" > gpurun_out/ab_longdepth.log 2>&1 || { tail -20 gpurun_out/ab_longdepth.log; exit 1; }
+python3 -c "
+import json; d=json.load(open('gpurun_out/ab_longdepth.log'))
+for k,v in d['variants'].items(): print(k, v['msamples_s_median'], v['msamples_s_best'], v['s'], 'finish', v['finish_ms'])"

@@ -17,5 +17,5 @@ for l in L:
 for p, (it, live, t) in sorted(last.items()): print("pipe", p, "last it", it, "live", live, "t", round(t - t0, 3))
 for l in L:
     m = re.search(r"t ([\d.]+)$", l)
-    if ("done" in l or "long" in l) and m: print(l.split(" t ")[0], round(float(m[1]) - t0, 3))
+    if ("done" in l or "long" in l or "finished" in l) and m: print(l.split(" t ")[0], round(float(m[1]) - t0, 3))
 PY
