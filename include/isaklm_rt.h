@@ -313,9 +313,10 @@ typedef struct RtOptions {
      * round, and pending lanes (of 64) before a wave's leaf test runs */
     int wf_descent_cap;
     int wf_postpone;
-    int wf_wide;         /* wide single-ray traversal (all 64 lanes on one ray): < 0 off; else on for a
-                          * finisher wave's lone ray and, once a trace launch's queue is empty, for the
-                          * rays of waves with at most wf_wide (0 = default 32) left */
+    int wf_wide;         /* wide single-ray traversal (all 64 lanes on one ray, one ray after the other):
+                          * < 0 off; else for the rays of a finisher wave with at most wf_wide live rays
+                          * and, once a trace launch's queue is empty, of a trace wave with at most
+                          * wf_wide rays left (0 = default 32) */
     /* row-interleaved sharding (the parity-exact option): with
      * num_shards > 1 only rows y % num_shards == shard_id are rendered (the
      * others are left untouched); every shard uses the single-stream seeds,

@@ -744,16 +744,21 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_finish_coop(RtDevScene sc, RtDevF
             if (__all(exhausted)) break;
             continue;
         }
-        if (wide && __popcll(lm) == 1) { // a lone ray, not yet started: the whole wave traces it
-            const int owner = __ffsll((long long)lm) - 1;
-            if (__shfl((int)(r.node == 0 && !r.pend), owner)) {
-                const Vec3D o = rt_v3(__shfl(r.o.x, owner), __shfl(r.o.y, owner), __shfl(r.o.z, owner));
-                const Vec3D d = rt_v3(__shfl(r.d.x, owner), __shfl(r.d.y, owner), __shfl(r.d.z, owner));
+        if (__popcll(lm) <= wide) {
+            // few rays left in the wave: each is traced by all 64 lanes, one
+            // after the other (wide_resume picks up a ray mid-traversal from
+            // its lane's stack) — a cooperative round would advance them
+            // together, but at ~5 node fetches per round instead of a level
+            // of the whole frontier
+            const WideLds W{s_wide + wave * WIDE_CAP, WIDE_CAP, wkey, reinterpret_cast<float *>(wkey + 1), w.mark};
+            for (unsigned long long mm = lm; mm; mm &= mm - 1) {
+                const int owner = __ffsll((long long)mm) - 1;
+                const int ot = wave * 64 + owner;
+                const Stack<WF_LDS_STACK> so{s_node + ot, s_entry + ot, WF_BLOCK,
+                                             st.spill + blockIdx.x * WF_BLOCK + ot, st.spill_threads};
                 int t;
                 float x, y, z;
-                const WideLds W{s_wide + wave * WIDE_CAP, WIDE_CAP, wkey, reinterpret_cast<float *>(wkey + 1), w.mark};
-                wide_trace<COUNT>(sc, o, d, __shfl(r.entry, owner), __shfl(r.exit_, owner), W, lane == owner, t, x, y,
-                                  z, c);
+                wide_resume<COUNT>(sc, r, owner, so, W, t, x, y, z, c);
                 if (lane == owner) {
                     hit = t;
                     bx = x;
@@ -762,8 +767,8 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_finish_coop(RtDevScene sc, RtDevF
                     r.live = false;
                     pending = true;
                 }
-                continue;
             }
+            continue;
         }
         if (coop_round<COUNT>(sc, r, stk, w, cap, postpone, hit, bx, by, bz, c)) pending = true;
     }
@@ -1053,9 +1058,10 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
     // cooperative traversal: node fetches per descent round, pending lanes before a leaf test
     const int cap = cap_opt > 0 ? cap_opt : WF_DESCENT_CAP_DEFAULT;
     const int postpone = postpone_opt > 0 ? (postpone_opt > 64 ? 64 : postpone_opt) : WF_POSTPONE_DEFAULT;
-    const int wide = wide_opt >= 0 ? 1 : 0; // finisher: lone rays traced by the whole wave
-    // trace launches: once the queue is empty, a wave with at most this many rays left finishes them wide
+    // trace launches: once the queue is empty, a wave with at most this many rays left finishes them wide;
+    // finisher: a wave with at most this many live rays traces them one by one with all lanes
     const int wide_lanes = wide_opt < 0 ? 0 : (wide_opt > 0 ? (wide_opt > 64 ? 64 : wide_opt) : WF_WIDE_TAIL_LANES);
+    const int wide = wide_lanes;
     static const bool trace_iters = getenv("RT_WF_TRACE_ITERS") != nullptr; // debug: per-iteration queue sizes
     // paths deeper than this leave their pipeline for wf_long (cooperative trace only)
     const int long_depth = trace_kind == 1 && long_opt >= 0 ? (long_opt > 0 ? long_opt : WF_LONG_DEPTH_DEFAULT) : 0;
