@@ -73,15 +73,17 @@ def test_other_trace_variants(variant):
 
 
 @pytest.mark.parametrize("scene", ["room_small", "cornell_blob"])
-@pytest.mark.parametrize("tail,waves,wide", [(1 << 30, 3, 0), (1 << 30, 1 << 20, 0), (1 << 30, 1 << 20, -1),
-                                             (700, 5, 0), (1, 0, 0)],
-                         ids=["finisher-only-refetch", "finisher-only-wide", "finisher-only-1-per-wave-narrow",
-                              "late-handoff-refetch", "queues-only"])
+@pytest.mark.parametrize("tail,waves,wide", [(1 << 30, 3, 0), (1 << 30, 3, 3), (1 << 30, 1 << 20, 0),
+                                             (1 << 30, 1 << 20, -1), (700, 5, 0), (1, 0, 0)],
+                         ids=["finisher-only-refetch", "finisher-only-refetch-wide-3", "finisher-only-wide",
+                              "finisher-only-1-per-wave-narrow", "late-handoff-refetch", "queues-only"])
 def test_wavefront_finisher_modes(scene, tail, waves, wide):
     """The cooperative finisher (wf_finish_coop) at every hand-off point and
-    width: whole call in the finisher with few waves (lanes refetch paths),
-    one path per wave (every ray traced by a whole wave: wide_trace, or
-    not), a late hand-off, and no finisher at all."""
+    width: whole call in the finisher with few waves (lanes refetch paths;
+    waves with at most 32 — or 3 — live rays trace them one by one with all
+    lanes, resuming rays in mid-traversal), one path per wave (every ray
+    traced by a whole wave: wide_trace, or not), a late hand-off, and no
+    finisher at all."""
     run = helpers.GpuRun(scene)
     W, H, P = 48, 27, 3
     gpu, gcnt, _ = run.render(W, H, P, count=True, kernel=rt.KERNEL_WAVEFRONT, wf_tail=tail, wf_finish_waves=waves,
