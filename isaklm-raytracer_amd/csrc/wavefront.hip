@@ -42,6 +42,7 @@ using namespace rtk;
 #define WF_POSTPONE_DEFAULT 20        // RtOptions.wf_postpone
 #define WF_TIMELINE_LAUNCHES 4096     // debug timeline: 3 u64 per trace launch in RtOptions.wave_times_device
 #define WF_WIDE_TAIL_LANES 32         // RtOptions.wf_wide > 0
+#define WF_FIN_WIDE_MIN_ENTRIES (1 << 18) // finisher: multi-ray wide tracing only for trees with this many leaf entries
 #define WF_MAX_PIPES 6                // concurrent pipelines (RtOptions.wf_pipelines); more than 3 need GPU_MAX_HW_QUEUES > 4
 #define WF_PIPES_DEFAULT 3
 #define WF_LONG_DEPTH_DEFAULT 64      // RtOptions.wf_long_depth: paths deeper than this go to wf_long
@@ -1061,7 +1062,12 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
     // trace launches: once the queue is empty, a wave with at most this many rays left finishes them wide;
     // finisher: a wave with at most this many live rays traces them one by one with all lanes
     const int wide_lanes = wide_opt < 0 ? 0 : (wide_opt > 0 ? (wide_opt > 64 ? 64 : wide_opt) : WF_WIDE_TAIL_LANES);
-    const int wide = wide_lanes;
+    // (finisher: tracing several rays one after the other with all lanes pays off
+    // when a ray visits hundreds of nodes — large trees; on a small tree, e.g.
+    // the 36-triangle Cornell box, a cooperative round of a few lanes is
+    // cheaper, and only a lone ray goes wide.  Measured: room2m / cornell_blob
+    // finisher time -18 % / -30 % at 32, the Cornell box 2x slower)
+    const int wide = sc.index_count >= WF_FIN_WIDE_MIN_ENTRIES ? wide_lanes : (wide_lanes > 0 ? 1 : 0);
     static const bool trace_iters = getenv("RT_WF_TRACE_ITERS") != nullptr; // debug: per-iteration queue sizes
     // paths deeper than this leave their pipeline for wf_long (cooperative trace only)
     const int long_depth = trace_kind == 1 && long_opt >= 0 ? (long_opt > 0 ? long_opt : WF_LONG_DEPTH_DEFAULT) : 0;
