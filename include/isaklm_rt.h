@@ -302,10 +302,12 @@ typedef struct RtOptions {
     unsigned long long *wave_times_device; /* optional debug: megakernel (with counters): 2 u64 per wave;
                           * wavefront: 3 u64 per trace launch (first start, first queue
                           * exhaustion, ~last end; s_memrealtime, 100 MHz), pre-set to ~0 */
-    /* wavefront tuning (0 = default): below wf_tail live paths the rest of
-     * the call runs in one cooperative finisher launch on at most
-     * wf_finish_waves waves; wf_tail > width*height runs the whole call in
-     * the finisher (persistent per-wave path fetch, no queue iterations) */
+    /* wavefront tuning (0 = default): below wf_tail (default 65536) live
+     * paths the rest of the call runs in one cooperative finisher launch on at
+     * most wf_finish_waves waves (default 2048; 512 for trees with fewer than
+     * 2^18 leaf entries, whose short rays keep fuller waves busy);
+     * wf_tail > width*height runs the whole call in the finisher (persistent
+     * per-wave path fetch, no queue iterations) */
     int wf_tail;
     int wf_finish_waves;
     int profile;         /* 1: time the wavefront kernels with HIP events (rt_last_profile) */
