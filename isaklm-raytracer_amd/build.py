@@ -83,12 +83,20 @@ def build(verbose=False, extra_hip_flags=()):
             _run(["g++"] + COMMON + HOST_FLAGS + ["-c", s, "-o", o], verbose)
         objs.append(o)
     hipcc = os.path.join(ROCM, "bin", "hipcc")
+    # the HIP objects remember the extra flags they were compiled with: a build
+    # with other flags (an A/B variant, or the default after one) recompiles
+    # them all even though their sources are older than the objects
+    flags_file = os.path.join(BUILD, "hip_flags")
+    want = " ".join(extra_hip_flags)
+    have = open(flags_file).read() if os.path.exists(flags_file) else None
     for src in HIP_SOURCES:
         s = os.path.join(CSRC, src)
         o = os.path.join(BUILD, os.path.basename(src) + ".o")
-        if _stale(o, [s] + headers) or extra_hip_flags:
+        if _stale(o, [s] + headers) or have != want:
             _run([hipcc] + COMMON + HIP_FLAGS + list(extra_hip_flags) + ["-c", s, "-o", o], verbose)
         objs.append(o)
+    with open(flags_file, "w") as fh:
+        fh.write(want)
     if _stale(LIB, objs):
         _run(["g++", "-shared", "-o", LIB] + objs +
              ["-L" + os.path.join(ROCM, "lib"), "-lamdhip64", "-lrccl", "-fopenmp",
