@@ -24,6 +24,15 @@
 //    spectral-selection / successive-approximation decode (:2269-2425,
 //    :3097-3114).
 //
+// Credit: the JPEG IDCT (idct_block), the h2v1/h1v2/h2v2 upsamplers and
+// ycbcr_to_rgba are PORTS of stb_image v2.28's public-domain routines
+// (Sean Barrett and contributors; stb_image.h:2479-2537, :3487-3550,
+// :3682-3705), not independent restatements: bit-identity with stb forces
+// their arithmetic, and their variable names follow stb's.  The inflate and
+// PNG parts are written independently.  Scope is frozen at what the
+// reference's seven textures need plus the variants already tested; nothing
+// further is added here (SURVEY §2 row 18 keeps decoding out of scope).
+//
 // Pinned against stb_image itself: tests/test_textures.py compares every
 // texture the reference ships plus synthetic PNG/JPEG variants with
 // oracle/_ref/libstb_ref.so (stb_image.cpp compiled from the reference's own
