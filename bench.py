@@ -4,23 +4,44 @@ Workload (BASELINE.json configs[2]): the README-like 2M-triangle synthetic
 room ("room2m": room + 1,997,568-triangle displaced gold mesh + two glass
 spheres + emissive quad), 1920x1080, adaptive sampling off.  One step = one
 rt_render call of `--passes` passes (spp) over the full frame (default 64:
-16 steps are the config's 1024 spp).  With --gpus N
-each rank renders its own spp slice (seeds = mt19937 outputs [rank*W*H,
-(rank+1)*W*H)) and one RCCL reduce (sum) of fb/sq/count into
-rank 0 plus the tonemap closes the timed region.  value = samples of all ranks
-/ max-over-ranks wall time.
+16 steps are the config's 1024 spp), inputs resident in HBM.
 
-Also reported: the roofline of the dominant kernel (wavefront: wf_trace_coop,
-whose SURVEY §8d traversal bytes 8*node + 40*tri come from the work counters
-of one counted call, over its launches' HIP-event time inside the timed
-steps, against 8 TB/s HBM) and the CPU oracle's rate on a bounded pixel
-sample (rank 0, N=1).
+Multi-GPU (`--gpus N`): one process per GPU.  Without WORLD_SIZE in the
+environment this script starts the N ranks itself (children with RANK /
+LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 set, before any GPU call in
+the parent); under torch.distributed.run it is one of them.  Rank r renders
+its spp slice (seeds = mt19937 outputs [r*W*H, (r+1)*W*H)) and
+the timed region closes with the product's ONE RCCL reduce of fb/sq/count
+into rank 0 (rt_reduce_shards, csrc/shards.hip) plus the tonemap.  value =
+samples of all ranks / max-over-ranks wall time.  The host-side barrier and
+the max use a gloo process group (no data moves through it).
+
+Roofline (north_star: "achieved HBM GB/s vs peak"): measured, not modelled.
+Before this process touches the GPU (rank 0, N=1), the same render runs in
+child processes under `rocprofv3 --pmc` (FETCH_SIZE; WRITE_SIZE; SQ
+counters), one call of the bench's passes between two tonemap marker
+dispatches; HBM bytes per sample = the sum of FETCH_SIZE (x2 on gfx950,
+MI355X_MICROARCH.md HBM section; the raw figure is reported beside it) and
+WRITE_SIZE over EVERY dispatch of that call / its samples.  achieved = those
+bytes per sample x the timed samples/s: chip-wide, call-level, <= peak by
+construction of the counters.  The SURVEY §8d algorithmic bytes (which the
+caches serve, mostly) are reported separately as `algorithmic_GBps`.
+
+cpu_baseline: the C oracle (OpenMP) on the host cores of the GPU box on a
+bounded pixel sample of the same frame, beside the reference's own
+single-core rate measured in the survey container.
 """
 import argparse
+import csv
 import ctypes
+import glob
 import json
 import os
+import shutil
+import socket
+import subprocess
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -29,11 +50,17 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 for p in (os.path.join(ROOT, "isaklm-raytracer_amd"), os.path.join(ROOT, "oracle")):
     sys.path.insert(0, p)
 
-import rt  # noqa: E402
-import shard  # noqa: E402
-
 METRIC = "Msamples/sec (W×H×spp/s) at 1920×1080; achieved HBM GB/s vs peak"
-HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+# the reference's own source compiled for the CPU (g++ -O2,
+# -ffp-contract=off) in the survey container, 1 core, 2.0M-tri displaced
+# mesh room, 255x255 x 1 spp
+REF_SINGLE_CORE = {"value": 0.0054, "unit": "Msamples/s", "cores": 1,
+                   "source": "SURVEY.md §6: reference source built for the CPU, Intel Xeon (family 6 model 207), "
+                             "1 thread, 2.0M-triangle synthetic room, 255x255 x 1 spp"}
+SQ_COUNTERS = ["SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_ANY",
+               "SQ_ACTIVE_INST_VALU", "SQ_THREAD_CYCLES_VALU"]
+MARKER = "rt_tonemap_kernel"
 
 
 def algorithmic_bytes(c):
@@ -42,33 +69,251 @@ def algorithmic_bytes(c):
             20 * c["skip"])
 
 
-class TorchGBuffer:
-    """G_Buffer whose four arrays are torch tensors (so RCCL can reduce them)."""
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=4)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--passes", type=int, default=64, help="spp per step (passes per rt_render call)")
+    ap.add_argument("--scene", default="room2m")
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 counter passes (roofline traffic)")
+    ap.add_argument("--pmc-save", default=None, help="directory to keep the parsed counter summaries in")
+    ap.add_argument("--pmc-child", default=None, help=argparse.SUPPRESS)  # internal: the profiled render
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher/rank wiring only (no GPU): ranks meet over gloo, rank 0 prints the line")
+    ap.add_argument("--kernel", choices=["mega", "wavefront"], default="wavefront")
+    ap.add_argument("--adaptive", action="store_true", help="adaptive sampling (configs[4]); value stays nominal "
+                    "W*H*spp/s, value_actual = accumulated samples/s")
+    ap.add_argument("--min-samples", type=int, default=100)
+    ap.add_argument("--max-depth", type=int, default=0, help="0 = unbounded (reference)")
+    ap.add_argument("--scene-dir", default=os.environ.get("RT_SCENE_DIR", os.path.join(ROOT, "build", "scenes")))
+    return ap.parse_args(argv)
 
-    def __init__(self, torch, n, seed_skip):
-        self.fb = torch.zeros(n * 3, dtype=torch.float32, device="cuda")
-        self.sq = torch.zeros(n, dtype=torch.float32, device="cuda")
-        self.cnt = torch.zeros(n, dtype=torch.int32, device="cuda")
-        self.rng = torch.from_numpy(rt.seeds(n, seed_skip).view(np.int32)).cuda()
-        self.g = rt.G_Buffer(self.fb.data_ptr(), self.sq.data_ptr(), self.cnt.data_ptr(), self.rng.data_ptr())
+
+# ------------------------------------------------------------------ launcher
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
 
 
-def pmc_traffic(kernel_name):
-    """HBM bytes per launch of `kernel_name` from the newest committed rocprofv3
-    PMC summary (profiles/r*/pmc_traffic_*.json: FETCH_SIZE / WRITE_SIZE passes
-    of this bench command, corrected as MI355X_MICROARCH.md prescribes)."""
-    import glob
+def launch_ranks(n, argv):
+    """Start n ranks of this script (one per GPU) and wait for them.  Runs in
+    a parent that never touches the GPU; rank 0 prints the JSON line."""
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                for q in live:  # a failed rank leaves the others waiting in a collective
+                    q.terminate()
+        time.sleep(0.2)
+    return rc
 
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic_*.json")), reverse=True):
-        d = json.load(open(f))
-        if d.get("kernel") == kernel_name:
-            return d["traffic_bytes_per_launch"], os.path.relpath(f, ROOT)
-    return None, None
+
+# ------------------------------------------------------------------ counters
+def _collect_csv(d, name):
+    hits = glob.glob(os.path.join(d, "**", f"*{name}.csv"), recursive=True)
+    return hits[0] if hits else None
 
 
-def cpu_baseline(scene_path, W, H, seconds, threads):
+def _window_sums(cc_csv, trace_csv):
+    """Counter sums over the dispatches strictly between the two marker
+    dispatches (the profiled call), per counter and per kernel."""
+    rows = list(csv.DictReader(open(cc_csv)))
+    marks = sorted({int(r["Dispatch_Id"]) for r in rows if MARKER in r["Kernel_Name"]})
+    if len(marks) < 2 and trace_csv:
+        marks = sorted({int(r["Dispatch_Id"]) for r in csv.DictReader(open(trace_csv)) if MARKER in r["Kernel_Name"]})
+    if len(marks) < 2:
+        raise RuntimeError(f"marker dispatches not found in {cc_csv}")
+    lo, hi = marks[-2], marks[-1]
+    total, per_kernel, dispatches = {}, {}, set()
+    for r in rows:
+        i = int(r["Dispatch_Id"])
+        if lo < i < hi:
+            v = float(r["Counter_Value"])
+            c = r["Counter_Name"]
+            total[c] = total.get(c, 0.0) + v
+            k = r["Kernel_Name"].split("(")[0].replace("void ", "")[:48]
+            per_kernel.setdefault(k, {}).setdefault(c, 0.0)
+            per_kernel[k][c] += v
+            dispatches.add(i)
+    kt = {}
+    if trace_csv:
+        for r in csv.DictReader(open(trace_csv)):
+            i = int(r["Dispatch_Id"])
+            if lo < i < hi:
+                k = r["Kernel_Name"].split("(")[0].replace("void ", "")[:48]
+                e = kt.setdefault(k, {"dispatches": 0, "ns": 0.0, "vgpr": None, "lds": None})
+                e["dispatches"] += 1
+                e["ns"] += float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
+                for key, col in (("vgpr", "Arch_VGPR_Count"), ("lds", "LDS_Block_Size")):
+                    if col in r and r[col] != "":
+                        e[key] = int(float(r[col]))
+    return total, per_kernel, len(dispatches), kt
+
+
+def measure_pmc(args, save_dir):
+    """rocprofv3 counter passes over one render call (child processes, run
+    before this process initialises the GPU).  Returns a dict or an error."""
+    child = ["--pmc-child", "1", "--passes", str(args.passes), "--scene", args.scene, "--width", str(args.width),
+             "--height", str(args.height), "--scene-dir", args.scene_dir, "--kernel", args.kernel,
+             "--max-depth", str(args.max_depth), "--min-samples", str(args.min_samples)]
+    if args.adaptive:
+        child.append("--adaptive")
+    res = {"passes": {}}
+    env = dict(os.environ, TMPDIR="/tmp")
+    for tag, ctrs in (("fetch", ["FETCH_SIZE"]), ("write", ["WRITE_SIZE"]), ("sq", SQ_COUNTERS)):
+        d = tempfile.mkdtemp(prefix=f"rtpmc_{tag}_", dir="/tmp")
+        cmd = ["timeout", "-s", "KILL", "240", "rocprofv3", "--pmc", *ctrs, "--kernel-trace", "-d", d, "-o", "run",
+               "--output-format", "csv", "--", sys.executable, os.path.abspath(__file__)] + child
+        t = time.perf_counter()
+        r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True)
+        if r.returncode != 0:
+            shutil.rmtree(d, ignore_errors=True)
+            return {"error": f"rocprofv3 {tag} pass rc={r.returncode}: {(r.stderr or r.stdout)[-400:]}"}
+        cc, kt = _collect_csv(d, "counter_collection"), _collect_csv(d, "kernel_trace")
+        try:
+            total, per_kernel, ndisp, ktrace = _window_sums(cc, kt)
+            info = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{\"pmc_child\"")][-1])
+        except Exception as e:  # noqa: BLE001
+            shutil.rmtree(d, ignore_errors=True)
+            return {"error": f"parsing the {tag} pass: {e}"}
+        res["passes"][tag] = {"counters": total, "per_kernel": per_kernel, "dispatches": ndisp,
+                              "kernel_trace": ktrace, "wall_s": round(time.perf_counter() - t, 1), **info}
+        shutil.rmtree(d, ignore_errors=True)
+    if save_dir:
+        os.makedirs(save_dir, exist_ok=True)
+        with open(os.path.join(save_dir, "bench_pmc_summary.json"), "w") as f:
+            json.dump(res, f, indent=1)
+    return res
+
+
+def pmc_child(args):
+    """The profiled render: warm-up call, marker, ONE call of the bench's
+    passes, marker.  Prints the call's sample count."""
+    import rt
+
+    rt.check(rt.lib().rt_set_device(0))
+    scene_file = ensure_scene(args)
+    host = rt.HostScene(scene_file)
+    dscene = rt.DeviceScene(host)
+    W, H = args.width, args.height
+    g = rt.GBuffer(W, H)
+    kernel = rt.KERNEL_WAVEFRONT if args.kernel == "wavefront" else rt.KERNEL_MEGA
+    kw = dict(adaptive=args.adaptive, min_samples=args.min_samples, max_depth=args.max_depth, kernel=kernel)
+    rt.render(dscene, g, host.camera, 0, rt.options(W, H, 8, **kw))
+    rgba = ctypes.c_void_p()
+    rt.check(rt.lib().rt_device_alloc(ctypes.byref(rgba), W * H * 4))
+    rt.check(rt.lib().rt_synchronize())
+    before = int(g.download()[2].sum(dtype=np.int64))
+    rt.check(rt.lib().rt_tonemap(g.g, rgba, W, H, None))
+    rt.render(dscene, g, host.camera, 1, rt.options(W, H, args.passes, **kw))
+    rt.check(rt.lib().rt_synchronize())
+    rt.check(rt.lib().rt_tonemap(g.g, rgba, W, H, None))
+    rt.check(rt.lib().rt_synchronize())
+    samples = int(g.download()[2].sum(dtype=np.int64)) - before
+    print(json.dumps({"pmc_child": 1, "samples": samples}), flush=True)
+
+
+def roofline_from_pmc(pmc, samples_per_s):
+    """Chip-wide HBM rate of the whole call from the counter passes."""
+    f = pmc["passes"]["fetch"]
+    w = pmc["passes"]["write"]
+    sq = pmc["passes"]["sq"]["counters"]
+    fetch_kb, write_kb = f["counters"].get("FETCH_SIZE", 0.0), w["counters"].get("WRITE_SIZE", 0.0)
+    raw = (1024.0 * fetch_kb + 1024.0 * write_kb) / f["samples"]
+    corr = (2 * 1024.0 * fetch_kb + 1024.0 * write_kb) / f["samples"]
+    achieved = corr * samples_per_s / 1e9
+    trace = {k: v for k, v in f["kernel_trace"].items()}
+    dom = max(trace.items(), key=lambda kv: kv[1]["ns"])[0] if trace else None
+    lat = {}
+    if sq.get("SQ_WAVE_CYCLES"):
+        lat["wait_frac"] = round(sq["SQ_WAIT_ANY"] / sq["SQ_WAVE_CYCLES"], 3)
+        lat["issue_frac"] = round(sq["SQ_ACTIVE_INST_ANY"] / sq["SQ_WAVE_CYCLES"], 3)
+    if sq.get("SQ_ACTIVE_INST_VALU"):
+        lat["valu_lane_util"] = round(sq["SQ_THREAD_CYCLES_VALU"] / (64.0 * sq["SQ_ACTIVE_INST_VALU"]), 3)
+    if dom and trace[dom].get("vgpr"):
+        v = trace[dom]["vgpr"]
+        alloc = -(-v // 8) * 8
+        lat["dominant_vgpr"] = v
+        lat["dominant_waves_per_simd_vgpr_limit"] = min(8, 512 // max(alloc, 1))
+    pk = {}
+    for k, c in f["per_kernel"].items():
+        pk[k] = {"fetch_GB": round(2 * 1024.0 * c.get("FETCH_SIZE", 0.0) / 1e9, 3)}
+    for k, c in w["per_kernel"].items():
+        pk.setdefault(k, {})["write_GB"] = round(1024.0 * c.get("WRITE_SIZE", 0.0) / 1e9, 3)
+    for k, t in trace.items():
+        pk.setdefault(k, {})["profiled_ms"] = round(t["ns"] / 1e6, 2)
+        pk[k]["dispatches"] = t["dispatches"]
+    return achieved, {
+        "hbm_bytes_per_sample": round(corr, 1),
+        "hbm_bytes_per_sample_raw": round(raw, 1),
+        "achieved_raw_GBps": round(raw * samples_per_s / 1e9, 1),
+        "correction": "FETCH_SIZE (KiB) x2: gfx950 tallies 128-B requests at 64 B (MI355X_MICROARCH.md HBM section; "
+                      "calibrated for this kernel's gather widths in profiles/r02/fetch_calibration.json); "
+                      "WRITE_SIZE x1; Infinity-Cache hits are counted as fetches, so both are upper bounds on HBM",
+        "dominant_kernel": dom,
+        "latency": lat,
+        "per_kernel": pk,
+        "counter_passes": {k: {"wall_s": v["wall_s"], "dispatches": v["dispatches"]} for k, v in pmc["passes"].items()},
+    }
+
+
+# ------------------------------------------------------------------ helpers
+def ensure_scene(args):
+    import rt
+
+    scene_dir = os.path.join(args.scene_dir, args.scene)
+    scene_file = os.path.join(scene_dir, "scene.txt")
+    if not os.path.exists(scene_file):
+        os.makedirs(scene_dir, exist_ok=True)
+        rt.generate_scene(args.scene, scene_dir)
+    return scene_file
+
+
+def cpu_info():
+    model = None
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count() or 1
+    return model, os.cpu_count() or 1, usable
+
+
+def cpu_baseline(scene_path, W, H, seconds):
+    """The C oracle (OpenMP) on a bounded sample of the same frame.  Threads:
+    the CPU share this job was given (OMP_NUM_THREADS on the GPU box, which
+    sets it to the box's share), else every usable core."""
     import oracle
 
+    model, nproc, usable = cpu_info()
+    omp = os.environ.get("OMP_NUM_THREADS")
+    threads = min(usable, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else usable
     sc = oracle.OracleScene(scene_path)
     n = W * H
 
@@ -88,52 +333,66 @@ def cpu_baseline(scene_path, W, H, seconds, threads):
     count = int(min(n, max(len(probe), rate * seconds)))
     pixels = np.linspace(0, n - 1, count).astype(np.int32)
     dt = run(pixels)
-    return {"value": round(count / dt / 1e6, 6), "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "sample": f"{count} pixels spread over the {W}x{H} frame x 1 spp ({dt:.1f} s, OpenMP {threads} threads, "
-                      f"oracle/rt_oracle.c)"}
+    value = count / dt / 1e6
+    return {"value": round(value, 6), "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "per_core": round(value / threads, 6), "cpu_model": model, "nproc": nproc, "usable_cpus": usable,
+            "sample": f"{count} pixels spread over the {W}x{H} frame x 1 spp ({dt:.1f} s, OpenMP {threads} threads "
+                      f"= the job's CPU share, oracle/rt_oracle.c)",
+            "reference_single_core": REF_SINGLE_CORE}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=4)
-    ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--passes", type=int, default=64, help="spp per step (passes per rt_render call)")
-    ap.add_argument("--scene", default="room2m")
-    ap.add_argument("--width", type=int, default=1920)
-    ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--kernel", choices=["mega", "wavefront"], default="wavefront")
-    ap.add_argument("--adaptive", action="store_true", help="adaptive sampling (configs[4]); value stays nominal "
-                    "W*H*spp/s, value_actual = accumulated samples/s")
-    ap.add_argument("--min-samples", type=int, default=100)
-    ap.add_argument("--max-depth", type=int, default=0, help="0 = unbounded (reference)")
-    ap.add_argument("--shard-mode", choices=["spp", "rows"], default="spp",
-                    help="N>1: spp slices (north star, seeds skipped per rank) or row-interleaved shards "
-                         "(bit-identical to one GPU)")
-    ap.add_argument("--scene-dir", default=os.environ.get("RT_SCENE_DIR", os.path.join(ROOT, "build", "scenes")))
-    args = ap.parse_args()
-
-    rank = int(os.environ.get("RANK", 0))
+# ------------------------------------------------------------------ main
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    args = parse_args(argv)
+    if args.pmc_child:
+        return pmc_child(args)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(args.gpus, argv)
     world = int(os.environ.get("WORLD_SIZE", 1))
+    rank = int(os.environ.get("RANK", 0))
     local = int(os.environ.get("LOCAL_RANK", 0))
-    import torch
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        return 2
 
-    torch.cuda.set_device(local)
-    rt.check(rt.lib().rt_set_device(local))
     dist = None
     if world > 1:
+        import datetime
+
         import torch.distributed as dist
 
-        dist.init_process_group("nccl")
+        dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=900))
+    parallelism = f"spp-sliced x{world} + RCCL reduce" if world > 1 else "single GPU"
+    if args.dry_run:
+        return dry_run(args, dist, world, rank, local, parallelism)
 
-    scene_dir = os.path.join(args.scene_dir, args.scene)
-    scene_file = os.path.join(scene_dir, "scene.txt")
-    if local == 0 and not os.path.exists(scene_file):
-        rt.generate_scene(args.scene, scene_dir)
+    # counter passes first: the children must own the GPU alone, and this
+    # process must not have initialised it yet
+    pmc = None
+    if rank == 0 and world == 1 and not args.no_pmc:
+        ensure_scene(args)  # host-only scene generation, once, outside the profiled children
+        pmc = measure_pmc(args, args.pmc_save)
+
+    import rt
+
+    ndev = ctypes.c_int(0)
+    rt.check(rt.lib().rt_device_count(ctypes.byref(ndev)))
+    if local >= ndev.value:
+        print(f"bench.py: rank {rank} needs device {local}, {ndev.value} visible", file=sys.stderr)
+        return 2
+    rt.check(rt.lib().rt_set_device(local))
+    comm = None
+    if world > 1:
+        uid = [rt.Comm.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        comm = rt.Comm(world, rank, uid[0])
+
+    if local == 0:
+        ensure_scene(args)
     if dist:
         dist.barrier()
+    scene_file = ensure_scene(args)
     t = time.perf_counter()
     host = rt.HostScene(scene_file)
     dscene = rt.DeviceScene(host)
@@ -142,15 +401,11 @@ def main():
 
     W, H, P = args.width, args.height, args.passes
     n = W * H
-    rows = args.shard_mode == "rows" and world > 1
-    gb = TorchGBuffer(torch, n, 0 if rows else shard.seed_skip(rank, W, H))
-    stream = torch.cuda.current_stream()
+    gb = rt.GBuffer(W, H, rank * n)  # spp slice r: mt19937 outputs [r*W*H, (r+1)*W*H) (shard.seed_skip)
     kernel = rt.KERNEL_WAVEFRONT if args.kernel == "wavefront" else rt.KERNEL_MEGA
     wavefront = kernel == rt.KERNEL_WAVEFRONT
-    shard_kw = dict(shard_id=rank, num_shards=world) if rows else {}
-    render_kw = dict(adaptive=args.adaptive, min_samples=args.min_samples, max_depth=args.max_depth, kernel=kernel,
-                     **shard_kw)
-    opt = rt.options(W, H, P, stream=ctypes.c_void_p(stream.cuda_stream), profile=wavefront, **render_kw)
+    render_kw = dict(adaptive=args.adaptive, min_samples=args.min_samples, max_depth=args.max_depth, kernel=kernel)
+    opt = rt.options(W, H, P, profile=wavefront, **render_kw)
     profiles = []
 
     def step(i):
@@ -161,92 +416,98 @@ def main():
     for i in range(args.warmup):
         step(i)
     profiles.clear()
-    torch.cuda.synchronize()
-    cnt_before = gb.cnt.sum(dtype=torch.int64)  # accumulated samples before the timed steps (adaptive: actual)
+    rt.check(rt.lib().rt_synchronize())
+    cnt_before = int(gb.download()[2].sum(dtype=np.int64))  # accumulated samples (adaptive: actual)
     if dist:
-        dist.all_reduce(cnt_before)
+        import torch
+
+        cb = torch.tensor([cnt_before], dtype=torch.int64)
+        dist.all_reduce(cb)  # every rank's warm-up samples: rank 0 holds them all after the reduce
+        cnt_before = int(cb.item())
+    rgba = ctypes.c_void_p()
+    rt.check(rt.lib().rt_device_alloc(ctypes.byref(rgba), n * 4))
+    rt.check(rt.lib().rt_synchronize())
+    if dist:
         dist.barrier()
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    rgba = torch.empty(n * 4, dtype=torch.uint8, device="cuda")
-    torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        starts[k].record(stream)
         step(args.warmup + k)
-        ends[k].record(stream)
-    if dist:  # one RCCL reduce over xGMI into rank 0's accumulation buffers
-        shard.reduce_to_root(dist, gb.fb, gb.sq, gb.cnt, root=0)
+    if comm:  # ONE RCCL reduce over xGMI of fb/sq/count into rank 0 (rt_reduce_shards)
+        comm.reduce(gb.g, W, H, root=0, stream=None)
     if rank == 0:
-        rt.check(rt.lib().rt_tonemap(gb.g, ctypes.c_void_p(rgba.data_ptr()), W, H,
-                                     ctypes.c_void_p(stream.cuda_stream)))
-    torch.cuda.synchronize()
+        rt.check(rt.lib().rt_tonemap(gb.g, rgba, W, H, None))
+    rt.check(rt.lib().rt_synchronize())
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if dist:
-        e = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        import torch
+
+        e = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
-    kernel_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
-    total_samples = (1 if rows else world) * n * P * args.steps
+    total_samples = world * n * P * args.steps
     value = total_samples / elapsed / 1e6
-    actual_samples = int((gb.cnt.sum(dtype=torch.int64) - cnt_before).item()) if rank == 0 else None
+    acc = gb.download()[2]
+    got = int(acc.sum(dtype=np.int64)) if rank == 0 else None
+    # rank 0 after the reduce holds every rank's counts
+    actual_samples = got - cnt_before if rank == 0 else None
+    expect = world * P * (args.warmup + args.steps)
 
-    # samples actually accumulated (every pixel, every pass: adaptive off)
-    expect = (1 if rows else world) * P * (args.warmup + args.steps)
-    got = int(gb.cnt.sum().item()) if rank == 0 else None
-
-    # work counters on one extra (untimed) step -> algorithmic bytes per call
+    # work counters of one extra (untimed) call -> algorithmic bytes and the
+    # reference deviations (watchdog, longest path, pushes past the 19-entry stack)
     counters = rt.DeviceCounters()
     copt = rt.options(W, H, P, counters=counters.p, profile=wavefront, **render_kw)
     rt.render(dscene, gb, host.camera, 1, copt)
     c = counters.read(finisher=True)
     bytes_per_call = algorithmic_bytes(c)
     if wavefront:
-        # dominant kernel: wf_trace_coop.  achieved = its SURVEY §8d traversal
-        # bytes per launch (the finisher's share taken out, from the counted
-        # call) / its average launch duration (HIP events around every launch
-        # in the timed steps; rocprof's average must agree).  The concurrent
-        # pipelines' launches overlap, so the aggregate rate while any trace
-        # launch runs (bytes per call / union of the launch intervals) is
-        # reported beside it.
         cprof = rt.last_profile()
         trace_bytes = 8 * (c["node"] - c["finish_node"]) + 40 * (c["tri"] - c["finish_tri"])
         launches = sum(p["trace_launches"] for p in profiles)
-        trace_ms_call = float(np.mean([p["trace_ms"] for p in profiles]))
-        union_ms_call = float(np.mean([p["trace_union_ms"] for p in profiles]))
         avg_launch_ms = sum(p["trace_ms"] for p in profiles) / max(launches, 1)
         bytes_per_launch = trace_bytes / max(cprof["trace_launches"], 1)
-        achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9
-        roof_kernel = "wf_trace_coop<false>"
         kernel_detail = {
+            "kernel": "wf_trace_coop<false>",
             "pipelines": cprof["pipelines"],
-            "trace_launches_per_call": launches / len(profiles),
+            "trace_launches_per_call": launches / max(len(profiles), 1),
             "avg_launch_ms": round(avg_launch_ms, 4),
-            "trace_union_ms_per_call": round(union_ms_call, 3),
-            "aggregate_GBps": round(trace_bytes / (union_ms_call * 1e-3) / 1e9, 1),
-            "aggregate_definition": "trace algorithmic bytes per call / wall ms with >= 1 trace launch running "
-                                    "(can exceed HBM peak: the caches absorb the reference's re-reads)",
-            "trace_ms_per_call": round(trace_ms_call, 3),
+            "algorithmic_GBps_per_launch": round(bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9, 1),
+            "trace_union_ms_per_call": round(float(np.mean([p["trace_union_ms"] for p in profiles])), 3),
+            "trace_ms_per_call": round(float(np.mean([p["trace_ms"] for p in profiles])), 3),
             "shade_ms_per_call": round(float(np.mean([p["shade_ms"] for p in profiles])), 3),
             "finish_ms_per_call": round(float(np.mean([p["finish_ms"] for p in profiles])), 3),
             "call_ms": round(float(np.mean([p["call_ms"] for p in profiles])), 3),
-            "trace_bytes_per_call": trace_bytes,
-            "trace_bytes_per_launch": round(bytes_per_launch),
-            "finisher_ray_share": round(c["finish_ray"] / max(c["ray"], 1), 4),
-            "call_achieved_GBps": round(bytes_per_call / (kernel_ms * 1e-3) / 1e9, 1),
+            "iterations_per_call": round(float(np.mean([p["iterations"] for p in profiles])), 1),
         }
     else:
-        achieved = bytes_per_call / (kernel_ms * 1e-3) / 1e9
-        roof_kernel = "rt_path_kernel<false,20>"
-        kernel_detail = {"kernel_ms": round(kernel_ms, 3)}
+        kernel_detail = {"kernel": "rt_path_kernel<false,20>"}
 
+    if comm:
+        comm.close()
     if rank != 0:
         if dist:
             dist.destroy_process_group()
-        return
-    traffic, traffic_src = pmc_traffic(roof_kernel)
+        return 0
+    samples_per_s = total_samples / elapsed
+    algorithmic_GBps = bytes_per_call / c["sample"] * samples_per_s / 1e9 if c["sample"] else None
+    roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": None, "traffic": None}
+    if pmc and "error" not in pmc:
+        achieved, detail = roofline_from_pmc(pmc, samples_per_s)
+        roof.update(achieved=round(achieved, 1), frac=round(achieved / HBM_PEAK_GBPS, 4),
+                    traffic=round(detail["hbm_bytes_per_sample"] * n * P), **detail)
+        roof["traffic_unit"] = f"HBM bytes per call of {P} passes (whole frame, every kernel)"
+    elif pmc:
+        roof["pmc_error"] = pmc["error"]
+    roof.update({
+        "definition": "achieved = counter-measured HBM bytes per sample (FETCH_SIZE x2 + WRITE_SIZE over every "
+                      "dispatch of one profiled call) x timed samples/s; chip-wide, call-level",
+        "algorithmic_GBps": round(algorithmic_GBps, 1) if algorithmic_GBps else None,
+        "algorithmic_bytes_per_sample": round(bytes_per_call / max(c["sample"], 1), 1),
+        "algorithmic_note": "SURVEY §8d bytes the reference's algorithm touches; served mostly by L2/MALL, "
+                            "so this rate can exceed the HBM peak",
+        **kernel_detail,
+    })
     line = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -256,51 +517,69 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3),
         "higher_is_better": True,
-        "scaling": "strong" if rows else "weak",
+        "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic",
         "config": {
             "workload": (f"BASELINE configs[2]: README-like 2M-triangle synthetic room '{args.scene}', {W}x{H}, "
-                         f"{P} spp per step, adaptive off"
+                         f"{P} spp per step per GPU, adaptive off"
                          if not args.adaptive and args.max_depth == 0 and args.scene == "room2m" else
-                         f"scene '{args.scene}', {W}x{H}, {P} spp per step, adaptive "
+                         f"scene '{args.scene}', {W}x{H}, {P} spp per step per GPU, adaptive "
                          f"{'on (min ' + str(args.min_samples) + ')' if args.adaptive else 'off'}, "
                          f"max depth {args.max_depth or 'unbounded'}"),
             "adaptive": args.adaptive, "max_depth": args.max_depth,
             "scene": args.scene, "width": W, "height": H, "spp_per_step": P,
             "triangles": info["triangles"], "kd_nodes": info["nodes"], "kd_indices": info["indices"],
-            "parallelism": (f"{'row-interleaved' if rows else 'spp-sliced'} x{world} + RCCL reduce" if world > 1
-                            else "single GPU"),
+            "parallelism": parallelism,
         },
-        "roofline": {
-            "bound": "hbm",
-            "achieved": round(achieved, 1),
-            "peak": HBM_PEAK_GBPS,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBPS, 4),
-            "traffic": traffic,
-            "traffic_source": traffic_src,
-            "kernel": roof_kernel,
-            **kernel_detail,
-            "call_algorithmic_bytes": bytes_per_call,
-            "bytes_per_sample": round(bytes_per_call / max(c["sample"], 1), 1),
-        },
+        "roofline": roof,
         "per_sample": {k: round(c[k] / max(c["sample"], 1), 3) for k in ("ray", "node", "tri", "hit", "nee")},
+        "deviations": {"watchdog_paths": c["watchdog"], "max_path_depth": c["maxdepth"],
+                       "deep_pushes": c["deep_push"],
+                       "note": "counted over one extra call of the same options: paths cut by the 65,536-bounce "
+                               "watchdog (SURVEY H8; the reference loops unbounded), the longest path in bounces, "
+                               "traversal pushes at stack index >= 19 (past the reference's 19-entry arrays, "
+                               "SURVEY H16)"},
         "samples_check": {"accumulated": got, "expected": None if args.adaptive else expect * n},
         "actual_samples": actual_samples,
-        "value_actual": round(actual_samples / elapsed / 1e6, 3),
+        "value_actual": round(actual_samples / elapsed / 1e6, 3) if actual_samples is not None else None,
         "setup_s": round(setup_s, 2),
     }
     if world == 1 and not args.no_cpu_baseline:
-        threads = min(16, os.cpu_count() or 1)
-        line["cpu_baseline"] = cpu_baseline(scene_file, W, H, args.cpu_seconds, threads)
+        line["cpu_baseline"] = cpu_baseline(scene_file, W, H, args.cpu_seconds)
     else:
         line["cpu_baseline"] = None
     print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()
+    return 0
+
+
+def dry_run(args, dist, world, rank, local, parallelism):
+    """No GPU: the ranks meet (barrier, max of their clocks, who is who) and
+    rank 0 prints the line the real run would frame."""
+    t0 = time.perf_counter()
+    ranks = [(rank, local, world)]
+    if dist:
+        dist.barrier()
+        gathered = [None] * world
+        dist.all_gather_object(gathered, (rank, local, world))
+        ranks = gathered
+    elapsed = time.perf_counter() - t0
+    if dist:
+        import torch
+
+        e = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "Msamples/s", "n_gpus": world,
+                          "steps": args.steps, "warmup": args.warmup, "dry_run": True, "ranks": ranks,
+                          "config": {"parallelism": parallelism}, "barrier_s": round(elapsed, 3)}), flush=True)
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -234,8 +234,16 @@ int rt_destroy_scene(Scene *scene);
 typedef struct RtPreparedScene *rt_scene_t;
 /* Re-lays a reference-layout device Scene into the traversal layout (SoA
  * nodes, precomputed triangle planes).  Bit-preserving: every precomputed
- * value is the reference's own expression evaluated once. */
-int rt_scene_prepare(const Scene *device_scene, int node_count, int index_count, rt_scene_t *out);
+ * value is the reference's own expression evaluated once.  Takes the Scene
+ * exactly as the reference's `Scene create_scene()` (rt/create_scene.cuh:
+ * 18-73) returns it: the KD node and index counts, which Scene does not carry
+ * (rt/scene.cuh:107-121), are recovered by walking the device tree
+ * pre-order from node 0 within its device allocation.  The arrays must be
+ * device allocations of this process (rt_device_alloc / hipMalloc). */
+int rt_scene_prepare(const Scene *device_scene, rt_scene_t *out);
+/* the same with the counts given (e.g. memory from a sub-allocator that
+ * hipMemGetAddressRange cannot bound) */
+int rt_scene_prepare_counts(const Scene *device_scene, int node_count, int index_count, rt_scene_t *out);
 /* same from host arrays (skips a device round trip) */
 int rt_scene_prepare_host(const Triangle *triangles, int triangle_count, const KD_Tree_Node *nodes,
                           int node_count, const int *indices, int index_count, const int *lights,
@@ -267,6 +275,10 @@ enum {
      * exact plane-test passes (barycentric tests) */
     RT_CNT_CAND = 13,
     RT_CNT_PLANE = 14,
+    /* traversal pushes at stack index >= 19: each would write past the
+     * reference's 19-entry stack arrays (rt/trace_ray.cuh:246-248);
+     * reference-comparable, the oracle counts the same */
+    RT_CNT_DEEP_PUSH = 15,
     /* cooperative trace, counting build only: wave-time (shader clocks,
      * summed over waves) in descent / leaf tests / ray fetch, and the number
      * of rounds, 64-entry plane chunks and barycentric batches */

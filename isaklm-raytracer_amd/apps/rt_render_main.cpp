@@ -106,10 +106,9 @@ int main(int argc, char **argv)
     Camera camera = {{-2.1f, 1.7f, -1.2f}, 0.975f, 0.3f, 1.57079632679f, 0.002f}; // rt/main.cu:101-104
     if (rt_host_scene_load_file(host, scene_path.c_str(), &camera) != RT_OK) return fail("create_models");
     Scene scene;
-    int node_count = 0, index_count = 0;
-    if (rt_create_scene(host, &scene, &node_count, &index_count) != RT_OK) return fail("create_scene");
+    if (rt_create_scene(host, &scene, nullptr, nullptr) != RT_OK) return fail("create_scene");
     rt_scene_t prepared = nullptr;
-    if (rt_scene_prepare(&scene, node_count, index_count, &prepared) != RT_OK) return fail("prepare");
+    if (rt_scene_prepare(&scene, &prepared) != RT_OK) return fail("prepare"); // counts derived from the tree
     rt_host_scene_destroy(host);
     const double setup_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 

@@ -473,7 +473,77 @@ int rt_scene_prepare_host(const Triangle *tris, int ntris, const KD_Tree_Node *n
     return upload_prepared(h, ntris, nidx, out);
 }
 
-int rt_scene_prepare(const Scene *ds, int node_count, int index_count, rt_scene_t *out)
+// bytes from p to the end of the device allocation that holds it
+static int bytes_to_alloc_end(const void *p, size_t *bytes)
+{
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    if (!p || hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)p) != hipSuccess || !base) {
+        (void)hipGetLastError();
+        return -1;
+    }
+    *bytes = (size_t)((const char *)base + size - (const char *)p);
+    return 0;
+}
+
+// The reference's Scene (rt/scene.cuh:107-121) carries no node or index
+// count (they are locals of create_kd_tree, rt/create_kd_tree.cuh:286,300),
+// so they are recovered from the device tree itself: the tree is walked
+// pre-order from node 0 over a copy of its allocation (hipMemGetAddressRange
+// bounds the copy); node_count = highest reachable node + 1, index_count =
+// the largest offset + count of a non-empty leaf.  A child index outside the
+// allocation, a cycle or a shared subtree is an error.
+int rt_scene_prepare(const Scene *ds, rt_scene_t *out)
+{
+    if (!ds || !out || ds->triangle_count <= 0 || ds->light_count < 0 || !ds->kd_tree.nodes || !ds->triangles) {
+        rt_set_error("rt_scene_prepare: bad arguments");
+        return RT_E_INVALID;
+    }
+    size_t node_bytes = 0, index_bytes = 0;
+    if (bytes_to_alloc_end(ds->kd_tree.nodes, &node_bytes) != 0) {
+        rt_set_error("rt_scene_prepare: kd_tree.nodes is not a device allocation of this process");
+        return RT_E_INVALID;
+    }
+    const size_t max_nodes = node_bytes / sizeof(KD_Tree_Node);
+    if (max_nodes == 0 || max_nodes >= (1u << 30)) {
+        rt_set_error("rt_scene_prepare: node allocation of %zu bytes", node_bytes);
+        return RT_E_INVALID;
+    }
+    std::vector<KD_Tree_Node> nodes(max_nodes);
+    HIPCHK(hipMemcpy(nodes.data(), ds->kd_tree.nodes, max_nodes * sizeof(KD_Tree_Node), hipMemcpyDeviceToHost));
+    std::vector<uint8_t> seen(max_nodes, 0);
+    std::vector<int> stack{0};
+    long long max_node = 0, index_count = 0;
+    while (!stack.empty()) {
+        const int i = stack.back();
+        stack.pop_back();
+        if (i < 0 || (size_t)i >= max_nodes || seen[(size_t)i]) {
+            rt_set_error("rt_scene_prepare: KD node index %d outside the node allocation, or reached twice", i);
+            return RT_E_INVALID;
+        }
+        seen[(size_t)i] = 1;
+        max_node = i > max_node ? i : max_node;
+        const KD_Tree_Node &n = nodes[(size_t)i];
+        if (n.is_leaf_node) {
+            if (n.triangle_count > 0) {
+                const long long end = (long long)n.index_offset + n.triangle_count;
+                index_count = end > index_count ? end : index_count;
+            }
+        } else {
+            stack.push_back(n.child_index2);
+            stack.push_back(n.child_index1);
+        }
+    }
+    if (index_count > 0 && (bytes_to_alloc_end(ds->kd_tree.triangle_indicies, &index_bytes) != 0 ||
+                            (size_t)index_count > index_bytes / sizeof(int))) {
+        rt_set_error("rt_scene_prepare: leaves address %lld triangle indices beyond the index allocation",
+                     index_count);
+        return RT_E_INVALID;
+    }
+    return rt_scene_prepare_counts(ds, (int)(max_node + 1), (int)index_count, out);
+}
+
+int rt_scene_prepare_counts(const Scene *ds, int node_count, int index_count, rt_scene_t *out)
 {
     if (!ds || !out || ds->triangle_count <= 0 || node_count <= 0 || index_count < 0 || ds->light_count < 0) {
         rt_set_error("rt_scene_prepare: bad arguments");

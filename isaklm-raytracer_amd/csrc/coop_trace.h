@@ -182,6 +182,7 @@ __device__ __forceinline__ bool coop_descend(const RtDevScene &sc, CoopRay &r, S
         } else if (t <= r.entry) {
             r.node = far_c;
         } else {
+            if (COUNT && r.sp >= RT_REF_STACK) c.v[RT_CNT_DEEP_PUSH]++;
             stk.put(r.sp, far_c, t);
             ++r.sp;
             r.node = near_c;
@@ -356,7 +357,8 @@ __device__ __forceinline__ bool coop_round(const RtDevScene &sc, CoopRay &r, STK
 struct WideItem {
     uint32_t node;
     float entry, exit_;
-    uint32_t acc; // node fetches charged to this item (counters)
+    uint32_t acc; // counters charged to this item: node fetches (bits 0..15) and
+                  // deep pushes (bits 16..31, RT_CNT_DEEP_PUSH)
 };
 
 __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v)
@@ -479,11 +481,14 @@ __device__ __forceinline__ void wide_trace_from(const RtDevScene &sc, Vec3D o, V
             const int jstar = key != ~0ull ? (int)(key >> 58) : Le - 1;
             if (COUNT) { // leaves 0..jstar are the sequential traversal's next visits
                 const bool counted = it.acc == WIDE_COUNTED;
-                const unsigned long long nv = wave_sum(lane <= jstar && !counted ? it.acc + 1ull : 0ull);
-                const unsigned long long tv = wave_sum(lane <= jstar && !counted ? (unsigned long long)cnt : 0ull);
+                const bool commit = lane <= jstar && !counted;
+                const unsigned long long nv = wave_sum(commit ? (it.acc & 0xFFFFu) + 1ull : 0ull);
+                const unsigned long long tv = wave_sum(commit ? (unsigned long long)cnt : 0ull);
+                const unsigned long long dv = wave_sum(commit ? (unsigned long long)(it.acc >> 16) : 0ull);
                 if (counter_lane) {
                     c.v[RT_CNT_NODE] += nv;
                     c.v[RT_CNT_TRI] += tv;
+                    c.v[RT_CNT_DEEP_PUSH] += dv;
                 }
             }
             if (key != ~0ull) {
@@ -525,7 +530,11 @@ __device__ __forceinline__ void wide_trace_from(const RtDevScene &sc, Vec3D o, V
                 } else if (t <= it.entry) {
                     a = WideItem{far_c, it.entry, it.exit_, it.acc + 1u};
                 } else {
-                    a = WideItem{near_c, it.entry, t, it.acc + 1u};
+                    // the sequential traversal pushes the far child at stack
+                    // index = this item's frontier position (every item below
+                    // it is a pending stack entry, SURVEY H16 counter)
+                    const uint32_t deep = COUNT && n - 1 - lane >= RT_REF_STACK ? 1u << 16 : 0u;
+                    a = WideItem{near_c, it.entry, t, it.acc + 1u + deep};
                     b = WideItem{far_c, t, it.exit_, 0u};
                     c_out = 2;
                 }

@@ -33,6 +33,7 @@
 // for 20 (every create_kd_tree tree) and 32 (other trees).
 #define RT_STACK_SMALL 20
 #define RT_STACK_DEPTH 32
+#define RT_REF_STACK 19 // KD_TREE_DEPTH (rt/macros.h): the reference's stack arrays' length
 #define RT_LEAF_TAG 3u
 #define RT_WATCHDOG_BOUNCES 65536 // SURVEY H8; never reached by a parity config
 

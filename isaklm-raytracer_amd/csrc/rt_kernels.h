@@ -164,6 +164,7 @@ __device__ __forceinline__ int trace(const RtDevScene &sc, const Vec3D o, const 
             } else if (t <= entry) {
                 node = far_c;
             } else {
+                if (COUNT && sp >= RT_REF_STACK) c.v[RT_CNT_DEEP_PUSH]++;
                 stk.put(sp, far_c, t);
                 ++sp;
                 node = near_c;

@@ -278,6 +278,7 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_trace_dyn(RtDevScene sc, WfState 
             } else if (t <= entry) {
                 node = far_c;
             } else {
+                if (COUNT && sp >= RT_REF_STACK) c.v[RT_CNT_DEEP_PUSH]++;
                 stk.put(sp, far_c, t);
                 ++sp;
                 node = near_c;

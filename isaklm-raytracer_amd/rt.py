@@ -76,7 +76,7 @@ def last_profile():
 TRIANGLE_BYTES = 152
 NODE_BYTES = 20
 COUNTER_NAMES = ["node", "tri", "hit", "texel", "nee", "sample", "skip", "ray", "watchdog", "maxdepth"]
-FINISH_COUNTER_NAMES = ["finish_node", "finish_tri", "finish_ray", "cand", "plane", "", "t_descend", "t_leaves",
+FINISH_COUNTER_NAMES = ["finish_node", "finish_tri", "finish_ray", "cand", "plane", "deep_push", "t_descend", "t_leaves",
                         "t_fetch", "rounds", "chunks", "bary", "wide_calls", "wide_rounds", "t_wide", "t_wide_load", "t_wide_leaf", "t_wide_expand"]
 N_COUNTERS = 32
 
@@ -123,7 +123,8 @@ def lib():
                                        ctypes.POINTER(i), ctypes.POINTER(Bounding_Box)]
         L.rt_create_scene.argtypes = [vp, ctypes.POINTER(Scene), ctypes.POINTER(i), ctypes.POINTER(i)]
         L.rt_destroy_scene.argtypes = [ctypes.POINTER(Scene)]
-        L.rt_scene_prepare.argtypes = [ctypes.POINTER(Scene), i, i, ctypes.POINTER(vp)]
+        L.rt_scene_prepare.argtypes = [ctypes.POINTER(Scene), ctypes.POINTER(vp)]
+        L.rt_scene_prepare_counts.argtypes = [ctypes.POINTER(Scene), i, i, ctypes.POINTER(vp)]
         L.rt_scene_prepare_host.argtypes = [vp, i, vp, i, vp, i, vp, i, Bounding_Box, ctypes.POINTER(vp)]
         L.rt_scene_release.argtypes = [vp]
         L.rt_scene_info.argtypes = [vp, ctypes.POINTER(sz), ctypes.POINTER(i), ctypes.POINTER(i),
@@ -226,7 +227,9 @@ def build_kd_tree(tri_ptr, n):
 
 class DeviceScene:
     """create_scene (rt/create_scene.cuh:18) -> reference-layout device Scene,
-    then rt_scene_prepare -> traversal layout."""
+    then rt_scene_prepare -> traversal layout.  rt_scene_prepare takes the
+    Scene alone (the reference's Scene has no node/index counts); the counts
+    rt_create_scene reports are kept only to cross-check what prepare derived."""
 
     def __init__(self, host_scene):
         self.scene = Scene()
@@ -234,7 +237,7 @@ class DeviceScene:
         check(lib().rt_create_scene(host_scene.h, ctypes.byref(self.scene), ctypes.byref(nn), ctypes.byref(ni)))
         self.node_count, self.index_count = nn.value, ni.value
         self.prepared = ctypes.c_void_p()
-        check(lib().rt_scene_prepare(ctypes.byref(self.scene), nn, ni, ctypes.byref(self.prepared)))
+        check(lib().rt_scene_prepare(ctypes.byref(self.scene), ctypes.byref(self.prepared)))
 
     def info(self):
         b, t, n, i, d = ctypes.c_size_t(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
@@ -359,6 +362,7 @@ class DeviceCounters:
         a = np.zeros(N_COUNTERS, dtype=np.uint64)
         check(lib().rt_download(_ptr(a), self.p, a.nbytes))
         out = {k: int(a[i]) for i, k in enumerate(COUNTER_NAMES)}
+        out["deep_push"] = int(a[15])  # RT_CNT_DEEP_PUSH: reference-comparable (the oracle counts it too)
         if finisher:
             out.update({k: int(a[10 + i]) for i, k in enumerate(FINISH_COUNTER_NAMES) if k})
         return out

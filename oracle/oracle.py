@@ -15,6 +15,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liboracle.so")
 N_COUNTERS = 16
 COUNTER_NAMES = ["node", "tri", "hit", "texel", "nee", "sample", "skip", "ray", "watchdog", "maxdepth"]
+DEEP_PUSH = 15  # CNT_DEEP_PUSH / RT_CNT_DEEP_PUSH
 
 _lib = None
 
@@ -133,7 +134,9 @@ class OracleScene:
             assert a.dtype == dt and a.flags["C_CONTIGUOUS"]
         lib().or_render(self.h, _p(cam), _p(fb), _p(sq), _p(cnt), _p(rng), _p(px),
                         0 if px is None else len(px), sample_count_arg, ctypes.byref(o), _p(counters))
-        return {k: int(counters[i]) for i, k in enumerate(COUNTER_NAMES)}
+        out = {k: int(counters[i]) for i, k in enumerate(COUNTER_NAMES)}
+        out["deep_push"] = int(counters[DEEP_PUSH])
+        return out
 
     def __del__(self):
         try:

@@ -47,7 +47,8 @@ const char *or_last_error(void) { return g_err; }
 #define TAUF (PIF * 2)                   /* rt/math_library.cuh:10 */
 #define WATCHDOG_BOUNCES 65536           /* never fires in parity configs */
 
-enum { CNT_NODE = 0, CNT_TRI, CNT_HIT, CNT_TEXEL, CNT_NEE, CNT_SAMPLE, CNT_SKIP, CNT_RAY, CNT_WATCHDOG, CNT_MAXDEPTH };
+enum { CNT_NODE = 0, CNT_TRI, CNT_HIT, CNT_TEXEL, CNT_NEE, CNT_SAMPLE, CNT_SKIP, CNT_RAY, CNT_WATCHDOG, CNT_MAXDEPTH,
+       CNT_DEEP_PUSH = 15 /* pushes at stack index >= KD_TREE_DEPTH: past the reference's arrays */ };
 
 /* ------------------------------------------------ types (rt/scene.cuh etc.) */
 typedef struct { float x, y; } V2;                     /* rt/math_library.cuh:55-66 */
@@ -375,6 +376,7 @@ static bool trace_ray(const OrScene *sc, Ray ray, Sample *sm, unsigned long long
                 node = sc->nodes[far_i];
             } else {
                 if (sp >= KD_TREE_DEPTH + 8) abort(); /* reference: stack overflow is UB */
+                if (sp >= KD_TREE_DEPTH) cnt[CNT_DEEP_PUSH] += 1; /* rt/trace_ray.cuh:246-248 hold 19 */
                 node_idx[sp] = far_i;
                 entry_d[sp] = t;
                 exit_d[sp] = exit_;
