@@ -243,14 +243,16 @@ def roofline_from_pmc(pmc, samples_per_s):
     corr = (2 * 1024.0 * fetch_kb + 1024.0 * write_kb) / f["samples"]
     achieved = corr * samples_per_s / 1e9
     trace = {k: v for k, v in f["kernel_trace"].items()}
-    dom = max(trace.items(), key=lambda kv: kv[1]["ns"])[0] if trace else None
+    # dominant = the kernel that moves the most bytes (wf_long's slices poll for
+    # published paths, so their summed duration says nothing about work)
+    dom = max(f["per_kernel"].items(), key=lambda kv: kv[1].get("FETCH_SIZE", 0.0))[0] if f["per_kernel"] else None
     lat = {}
     if sq.get("SQ_WAVE_CYCLES"):
         lat["wait_frac"] = round(sq["SQ_WAIT_ANY"] / sq["SQ_WAVE_CYCLES"], 3)
         lat["issue_frac"] = round(sq["SQ_ACTIVE_INST_ANY"] / sq["SQ_WAVE_CYCLES"], 3)
     if sq.get("SQ_ACTIVE_INST_VALU"):
         lat["valu_lane_util"] = round(sq["SQ_THREAD_CYCLES_VALU"] / (64.0 * sq["SQ_ACTIVE_INST_VALU"]), 3)
-    if dom and trace[dom].get("vgpr"):
+    if dom and dom in trace and trace[dom].get("vgpr"):
         v = trace[dom]["vgpr"]
         alloc = -(-v // 8) * 8
         lat["dominant_vgpr"] = v
@@ -497,6 +499,14 @@ def main(argv=None):
         roof.update(achieved=round(achieved, 1), frac=round(achieved / HBM_PEAK_GBPS, 4),
                     traffic=round(detail["hbm_bytes_per_sample"] * n * P), **detail)
         roof["traffic_unit"] = f"HBM bytes per call of {P} passes (whole frame, every kernel)"
+        dk = detail["per_kernel"].get(detail["dominant_kernel"] or "", {})
+        if wavefront and dk.get("dispatches") and "wf_trace_coop" in (detail["dominant_kernel"] or ""):
+            # the dominant kernel alone: its counter bytes per launch / its live
+            # average launch time (HIP events on its pipeline's stream, timed steps)
+            per_launch = 1e9 * (dk.get("fetch_GB", 0.0) + dk.get("write_GB", 0.0)) / dk["dispatches"]
+            kernel_detail["hbm_bytes_per_launch"] = round(per_launch)
+            kernel_detail["hbm_GBps_per_launch"] = round(per_launch / (kernel_detail["avg_launch_ms"] * 1e-3) / 1e9, 1)
+            kernel_detail["hbm_frac_per_launch"] = round(kernel_detail["hbm_GBps_per_launch"] / HBM_PEAK_GBPS, 4)
     elif pmc:
         roof["pmc_error"] = pmc["error"]
     roof.update({

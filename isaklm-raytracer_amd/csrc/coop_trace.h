@@ -357,8 +357,10 @@ __device__ __forceinline__ bool coop_round(const RtDevScene &sc, CoopRay &r, STK
 struct WideItem {
     uint32_t node;
     float entry, exit_;
-    uint32_t acc; // counters charged to this item: node fetches (bits 0..15) and
-                  // deep pushes (bits 16..31, RT_CNT_DEEP_PUSH)
+    uint32_t acc; // counting build: counters charged to this item — node fetches
+                  // (bits 0..15), deep pushes (bits 16..23, RT_CNT_DEEP_PUSH) —, the
+                  // sequential stack size when the item becomes the current node
+                  // (bits 24..28) and WIDE_COUNTED (bit 31)
 };
 
 __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v)
@@ -379,7 +381,8 @@ struct WideLds {
 
 // an item whose node fetch (and, for a leaf, its triangle tests) the
 // sequential traversal already counted (a resumed ray's pending leaf)
-#define WIDE_COUNTED 0xFFFFFFFFu
+#define WIDE_COUNTED 0x80000000u
+#define WIDE_SP_SHIFT 24 // acc bits 24..28: the item's sequential stack size
 
 // Trace the wave-uniform ray (o, d) from a frontier of n items already in
 // W.F (F[n-1] is the next item in traversal order) with all 64 lanes.
@@ -480,11 +483,11 @@ __device__ __forceinline__ void wide_trace_from(const RtDevScene &sc, Vec3D o, V
             const unsigned long long key = vkey[0];
             const int jstar = key != ~0ull ? (int)(key >> 58) : Le - 1;
             if (COUNT) { // leaves 0..jstar are the sequential traversal's next visits
-                const bool counted = it.acc == WIDE_COUNTED;
+                const bool counted = (it.acc & WIDE_COUNTED) != 0;
                 const bool commit = lane <= jstar && !counted;
                 const unsigned long long nv = wave_sum(commit ? (it.acc & 0xFFFFu) + 1ull : 0ull);
                 const unsigned long long tv = wave_sum(commit ? (unsigned long long)cnt : 0ull);
-                const unsigned long long dv = wave_sum(commit ? (unsigned long long)(it.acc >> 16) : 0ull);
+                const unsigned long long dv = wave_sum(commit ? (unsigned long long)((it.acc >> 16) & 0xFFu) : 0ull);
                 if (counter_lane) {
                     c.v[RT_CNT_NODE] += nv;
                     c.v[RT_CNT_TRI] += tv;
@@ -514,6 +517,11 @@ __device__ __forceinline__ void wide_trace_from(const RtDevScene &sc, Vec3D o, V
         if (have && lane >= Le) {
             c_out = 1;
             if (!leaf) {
+                // counting build: this node's fetch is charged to its first child
+                // (nothing if it was counted already); a child becomes current
+                // with the parent's stack size, +1 for the near child of a push
+                const uint32_t sp_it = COUNT ? (it.acc >> WIDE_SP_SHIFT) & 31u : 0u;
+                const uint32_t acc1 = COUNT ? ((it.acc & WIDE_COUNTED) ? 0u : (it.acc & 0xFFFFFFu) + 1u) : 0u;
                 const uint32_t axis = nd.y & 3u;
                 const float split = as_float(nd.x);
                 const float oax = axis == 0 ? ox : (axis == 1 ? oy : oz);
@@ -526,16 +534,16 @@ __device__ __forceinline__ void wide_trace_from(const RtDevScene &sc, Vec3D o, V
                 }
                 const float t = rt_div_by(split - oax, dax, yax); // intersect_plane (:190-210)
                 if (t >= it.exit_ || t < 0) {
-                    a = WideItem{near_c, it.entry, it.exit_, it.acc + 1u};
+                    a = WideItem{near_c, it.entry, it.exit_, acc1 | sp_it << WIDE_SP_SHIFT};
                 } else if (t <= it.entry) {
-                    a = WideItem{far_c, it.entry, it.exit_, it.acc + 1u};
+                    a = WideItem{far_c, it.entry, it.exit_, acc1 | sp_it << WIDE_SP_SHIFT};
                 } else {
                     // the sequential traversal pushes the far child at stack
-                    // index = this item's frontier position (every item below
-                    // it is a pending stack entry, SURVEY H16 counter)
-                    const uint32_t deep = COUNT && n - 1 - lane >= RT_REF_STACK ? 1u << 16 : 0u;
-                    a = WideItem{near_c, it.entry, t, it.acc + 1u + deep};
-                    b = WideItem{far_c, t, it.exit_, 0u};
+                    // index sp_it (SURVEY H16 counter).  (Not the item's frontier
+                    // position: items below it may already be expanded.)
+                    const uint32_t deep = COUNT && sp_it >= RT_REF_STACK ? 1u << 16 : 0u;
+                    a = WideItem{near_c, it.entry, t, (acc1 + deep) | (sp_it + 1u) << WIDE_SP_SHIFT};
+                    b = WideItem{far_c, t, it.exit_, sp_it << WIDE_SP_SHIFT};
                     c_out = 2;
                 }
             }
@@ -583,8 +591,9 @@ __device__ __forceinline__ void wide_resume(const RtDevScene &sc, const CoopRay 
     if (lane < sp) stk_owner.get(lane, node, entry);
     const float below = __shfl_up(entry, 1); // entry of the stack entry below = this one's exit
     const float root_exit = __shfl(r.root_exit, owner);
-    if (lane < sp) W.F[lane] = WideItem{node, entry, lane > 0 ? below : root_exit, 0u};
-    if (lane == owner) W.F[sp] = WideItem{r.node, r.entry, r.exit_, r.pend ? WIDE_COUNTED : 0u};
+    if (lane < sp) W.F[lane] = WideItem{node, entry, lane > 0 ? below : root_exit, (uint32_t)lane << WIDE_SP_SHIFT};
+    if (lane == owner)
+        W.F[sp] = WideItem{r.node, r.entry, r.exit_, (r.pend ? WIDE_COUNTED : 0u) | (uint32_t)sp << WIDE_SP_SHIFT};
     wide_trace_from<COUNT>(sc, o, d, sp + 1, W, lane == owner, tri, hbx, hby, hbz, c);
 }
 

@@ -899,6 +899,7 @@ struct Pipe {
     uint32_t *host_count = nullptr;
     hipEvent_t ev[6] = {};   // RtOptions.profile
     hipEvent_t join = nullptr;
+    bool joined = false; // join recorded by a previous call
     RtProfile prof{};
 };
 
@@ -910,6 +911,7 @@ struct Workspace {
     bool streams_ok = false;
     hipEvent_t fork = nullptr, ev0 = nullptr, ev1 = nullptr;
     hipEvent_t long_ev = nullptr; // after the last wf_long slice on the caller's stream
+    bool recorded = false;   // long_ev recorded by a previous call
     RtProfile prof{};        // last profiled call
 };
 
@@ -1081,6 +1083,14 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
     for (int pi = 0; pi < WF_MAX_PIPES; ++pi) w.pipe[pi].st.long_depth = long_depth;
     const WfState &lst = w.pipe[0].st;
 
+    // the workspace (per-pixel path state, long-path hand-off) is shared by every
+    // call on this device: a call on another stream than the previous one must
+    // not start before that call's last wf_long slice and pipelines are done
+    if (w.recorded) {
+        if (hipStreamWaitEvent(stream, w.long_ev, 0) != hipSuccess) return -1;
+        for (int pi = 0; pi < WF_MAX_PIPES; ++pi)
+            if (w.pipe[pi].joined && hipStreamWaitEvent(stream, w.pipe[pi].join, 0) != hipSuccess) return -1;
+    }
     if (long_depth > 0) {
         if (hipMemsetAsync(lst.long_flag, 0, slots * 4, stream) != hipSuccess) return -1;
         if (hipMemsetAsync(lst.long_ctr, 0, 256, stream) != hipSuccess) return -1;
@@ -1108,7 +1118,9 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
             hipLaunchKernelGGL(wf_long<false>, dim3(WF_LONG_BLOCKS), dim3(WF_BLOCK), 0, stream, sc, fr, cam, lst, fin);
         if (hipGetLastError() != hipSuccess) return -1;
         long_final = final;
-        return hipEventRecord(w.long_ev, stream) == hipSuccess ? 0 : -1;
+        if (hipEventRecord(w.long_ev, stream) != hipSuccess) return -1;
+        w.recorded = true;
+        return 0;
     };
     std::atomic<int> producing(npipes);
     bool produced_done[WF_MAX_PIPES] = {};
@@ -1156,7 +1168,10 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
                     hipLaunchKernelGGL(wf_finish_coop<false>, dim3(fgrid), dim3(WF_BLOCK), 0, s, sc, fr, cam, st, qq,
                                        (int)ppw, cap, postpone, wide);
             } else {
-                const int fgrid = (int)((live + WF_BLOCK - 1) / WF_BLOCK);
+                // grid-stride loop: at most `grid` blocks, so gtid stays inside the spill area
+                // (sized for grid * WF_BLOCK threads)
+                int fgrid = (int)((live + WF_BLOCK - 1) / WF_BLOCK);
+                fgrid = fgrid > grid ? grid : fgrid;
                 if (count) hipLaunchKernelGGL(wf_finish<true>, dim3(fgrid), dim3(WF_BLOCK), 0, s, sc, fr, cam, st, qq);
                 else hipLaunchKernelGGL(wf_finish<false>, dim3(fgrid), dim3(WF_BLOCK), 0, s, sc, fr, cam, st, qq);
             }
@@ -1221,6 +1236,7 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
         }
         if (rc != 0) return rc;
         if (hipEventRecord(pp.join, s) != hipSuccess) return -1;
+        pp.joined = true;
         if (trace_iters) {
             (void)hipStreamSynchronize(s);
             timespec ts;

@@ -59,6 +59,8 @@ def lib():
         L.or_scatter.argtypes = [vp, vp, i, ctypes.c_uint32, vp, ctypes.POINTER(ctypes.c_uint32),
                                  ctypes.POINTER(i), ctypes.POINTER(i)]
         L.or_scatter.restype = None
+        L.or_direct_light.argtypes = [vp, vp, vp, ctypes.POINTER(ctypes.c_uint32), vp]
+        L.or_direct_light.restype = None
         L.or_render.argtypes = [vp, vp, vp, vp, vp, vp, vp, i, i, ctypes.POINTER(OrOptions), vp]
         L.or_default_options.argtypes = [ctypes.POINTER(OrOptions)]
         L.or_default_options.restype = None
@@ -118,6 +120,15 @@ class OracleScene:
         out = np.zeros((len(rays), 12), dtype=np.float32)
         lib().or_trace_rays(self.h, _p(rays), len(rays), _p(out))
         return out
+
+    def direct_light(self, pos, normal, rng):
+        """sample_direct_light at one point -> (radiance float32[3], rng after)."""
+        p = np.ascontiguousarray(pos, dtype=np.float32)
+        n = np.ascontiguousarray(normal, dtype=np.float32)
+        out = np.zeros(3, dtype=np.float32)
+        st = ctypes.c_uint32(int(rng))
+        lib().or_direct_light(self.h, _p(p), _p(n), ctypes.byref(st), _p(out))
+        return out, st.value
 
     def render(self, camera, fb, sq, cnt, rng, width, height, passes, sample_count_arg=1, pixels=None,
                adaptive=True, min_samples=100, tolerance=0.05, max_depth=0, threads=0):

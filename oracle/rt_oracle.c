@@ -672,6 +672,16 @@ static V3 sample_direct_light(const OrScene *sc, V3 pos, V3 normal, uint32_t *rn
     return v3(0.0f, 0.0f, 0.0f);
 }
 
+/* sample_direct_light for one shading point (tests' independent NEE restatement) */
+void or_direct_light(const OrScene *s, const float pos[3], const float normal[3], uint32_t *rng, float out[3])
+{
+    unsigned long long cnt[OR_CNT_COUNT] = {0};
+    V3 r = sample_direct_light(s, v3(pos[0], pos[1], pos[2]), v3(normal[0], normal[1], normal[2]), rng, cnt);
+    out[0] = r.x;
+    out[1] = r.y;
+    out[2] = r.z;
+}
+
 /* trace_path (:268-325); returns the sample's radiance */
 static V3 trace_path(const OrScene *sc, Ray primary, uint32_t *rng, int max_depth, unsigned long long *cnt)
 {

@@ -78,6 +78,10 @@ void or_trace_rays(const OrScene *s, const float *rays6, int n, float *out12);
 void or_scatter(const float ray_dir[3], const float sample[22], int inside, uint32_t rng, float out[12],
                 uint32_t *rng_out, int *inside_out, int *type_out);
 
+/* sample_direct_light (rt/path_tracing.cuh:235-265) at one shading point:
+ * radiance out[3], *rng advanced by the draws the reference makes */
+void or_direct_light(const OrScene *s, const float pos[3], const float normal[3], uint32_t *rng, float out[3]);
+
 /* path_tracing (rt/path_tracing.cuh:338-395) over `passes` passes, for the
  * pixels in `pixels` (NULL = all W*H), on G_Buffer-layout host arrays.
  * sample_count_arg == 0 resets fb/sq/count of the listed pixels first

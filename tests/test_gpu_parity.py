@@ -254,6 +254,31 @@ def test_room2m_full_frame_sparse_pixels(kernel):
 
 
 @pytest.mark.timeout(240)
+def test_room2m_bench_configuration_sparse_pixels():
+    """bench.py's timed configuration exactly: room2m at 1920x1080, two
+    rt_render calls of 64 passes (sample_count 0 then 1), wavefront kernel with
+    its defaults (3 pipelines, long-path hand-off at depth 64, wide tails,
+    cooperative finisher), no counters (the bench's kernels).  Every 4099th
+    pixel re-rendered by the oracle over the same 128 spp.  A counted call of
+    the same options must not fire the 65,536-bounce watchdog."""
+    run = helpers.GpuRun("room2m")
+    W, H, P = 1920, 1080, 64
+    gpu, _, g = run.render(W, H, P, calls=2, kernel=rt.KERNEL_WAVEFRONT)
+    pixels = np.arange(0, W * H, 4099, dtype=np.int32)
+    ref, rcnt = helpers.oracle_render(run.path, W, H, P, calls=2, pixels=pixels)
+    helpers.assert_bitwise(gpu, ref, pixels=pixels, what="room2m bench configuration")
+    assert np.all(gpu[2] == 2 * P)
+    assert helpers.rel_linf(gpu[0][pixels], gpu[2][pixels], ref[0][pixels], ref[2][pixels]) < 1e-4
+    assert rcnt["watchdog"] == 0
+    cnt = rt.DeviceCounters()
+    rt.render(run.dev, g, run.camera, 1, rt.options(W, H, P, counters=cnt.p, kernel=rt.KERNEL_WAVEFRONT))
+    c = cnt.read()
+    assert c["watchdog"] == 0, c
+    assert c["sample"] == W * H * P
+    assert c["maxdepth"] > 64  # glass paths run past the long-path hand-off depth
+
+
+@pytest.mark.timeout(240)
 def test_room2m_glass_adaptive_full_frame_sparse_pixels():
     """BASELINE configs[4] setting per GPU: the dielectric stress scene
     (2M-triangle glass mesh, smooth normals) at 1920x1080, adaptive sampling
@@ -268,4 +293,5 @@ def test_room2m_glass_adaptive_full_frame_sparse_pixels():
     ref, rcnt = helpers.oracle_render(run.path, W, H, P, adaptive=True, min_samples=MS, max_depth=32, pixels=pixels)
     helpers.assert_bitwise(gpu, ref, pixels=pixels, what="room2m_glass adaptive")
     assert rcnt["skip"] > 0  # the adaptive test really skipped pixel-passes
+    assert rcnt["watchdog"] == 0  # no path cut by the 65,536-bounce watchdog
     assert helpers.rel_linf(gpu[0][pixels], gpu[2][pixels], ref[0][pixels], ref[2][pixels]) < 1e-4

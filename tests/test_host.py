@@ -155,6 +155,26 @@ def test_png_writer_roundtrip(tmp_path, w, h):
     np.testing.assert_array_equal(_decode_png(path), img)
 
 
+def test_division_structured_cases(tmp_path):
+    """rt_div_by against IEEE '/' over structured operands rather than random
+    ones (tests/native/div_structured.cpp): all 2^23 divisor significands x
+    numerators at and around every quotient binade edge, near-midpoint
+    quotients, 16 exponent pairs including the guard boundaries 2^-60 / 2^40,
+    all sign combinations (1.2e10 pairs), plus the guard edges exhaustively
+    over the numerator significand.  Zero mismatches."""
+    import subprocess
+
+    ROOT = helpers.ROOT
+    src = os.path.join(ROOT, "tests", "native", "div_structured.cpp")
+    exe = str(tmp_path / "div_structured")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-fopenmp", "-ffp-contract=off", "-I", os.path.join(ROOT, "include"),
+                    "-I", os.path.join(ROOT, "isaklm-raytracer_amd", "csrc"), src, "-o", exe], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    tested, bad = (int(x) for x in r.stdout.split()[1:4:2])
+    assert tested > 12_000_000_000 and bad == 0, r.stdout
+
+
 def test_division_matches_ieee():
     """rt_div_by (reciprocal + Markstein correction, used for the KD split
     distance on the GPU) gives the bits of IEEE '/' on 2e7 random operand
