@@ -247,11 +247,17 @@ def roofline_from_pmc(pmc, samples_per_s):
     # published paths, so their summed duration says nothing about work)
     dom = max(f["per_kernel"].items(), key=lambda kv: kv[1].get("FETCH_SIZE", 0.0))[0] if f["per_kernel"] else None
     lat = {}
+    # latency evidence of the dominant kernel alone (wf_long's slices spend most
+    # of their wave-cycles polling, so whole-call SQ ratios mix in idle waves)
+    sqk = pmc["passes"]["sq"]["per_kernel"].get(dom, sq) if dom else sq
+    lat["scope"] = dom if dom and dom in pmc["passes"]["sq"]["per_kernel"] else "whole call"
+    if sqk.get("SQ_WAVE_CYCLES"):
+        lat["wait_frac"] = round(sqk["SQ_WAIT_ANY"] / sqk["SQ_WAVE_CYCLES"], 3)
+        lat["issue_frac"] = round(sqk["SQ_ACTIVE_INST_ANY"] / sqk["SQ_WAVE_CYCLES"], 3)
+    if sqk.get("SQ_ACTIVE_INST_VALU"):
+        lat["valu_lane_util"] = round(sqk["SQ_THREAD_CYCLES_VALU"] / (64.0 * sqk["SQ_ACTIVE_INST_VALU"]), 3)
     if sq.get("SQ_WAVE_CYCLES"):
-        lat["wait_frac"] = round(sq["SQ_WAIT_ANY"] / sq["SQ_WAVE_CYCLES"], 3)
-        lat["issue_frac"] = round(sq["SQ_ACTIVE_INST_ANY"] / sq["SQ_WAVE_CYCLES"], 3)
-    if sq.get("SQ_ACTIVE_INST_VALU"):
-        lat["valu_lane_util"] = round(sq["SQ_THREAD_CYCLES_VALU"] / (64.0 * sq["SQ_ACTIVE_INST_VALU"]), 3)
+        lat["call_wait_frac"] = round(sq["SQ_WAIT_ANY"] / sq["SQ_WAVE_CYCLES"], 3)
     if dom and dom in trace and trace[dom].get("vgpr"):
         v = trace[dom]["vgpr"]
         alloc = -(-v // 8) * 8

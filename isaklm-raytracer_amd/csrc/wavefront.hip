@@ -1047,7 +1047,13 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
     Workspace &w = g_ws[dev];
     // persistent-ish grid for trace/shade (grid-stride over the queue); RT_WF_GRID overrides (experiments)
     static const int grid_env = getenv("RT_WF_GRID") ? atoi(getenv("RT_WF_GRID")) : 0;
-    const int grid = grid_env >= 256 && grid_env <= 16384 ? grid_env : 1536; // = 6 blocks x 256 CUs
+    // 512 blocks = 2,048 waves = a third of the chip's 6,144 wave slots at the
+    // trace kernel's 6 waves/SIMD: the 3 pipelines' launches share the chip,
+    // and a launch's ~465k rays are ~3.5 per lane, so the lanes stay busy past
+    // the launch's first round of rays (1,536 blocks: ~1.2 rays per lane, most
+    // of the launch was its tail).  Measured 512 / 704 / 1,536: 37.5 / 37.6 /
+    // 33.1 Msamples/s on room2m 1080p (tools/gpu_sweep.sh, profiles/r02).
+    const int grid = grid_env >= 64 && grid_env <= 16384 ? grid_env : 512;
     const size_t slots = (size_t)fr.width * fr.height;
     const bool count = fr.counters != nullptr;
     const bool prof = profile != 0;

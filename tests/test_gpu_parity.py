@@ -271,7 +271,7 @@ def test_room2m_bench_configuration_sparse_pixels():
     assert helpers.rel_linf(gpu[0][pixels], gpu[2][pixels], ref[0][pixels], ref[2][pixels]) < 1e-4
     assert rcnt["watchdog"] == 0
     cnt = rt.DeviceCounters()
-    rt.render(run.dev, g, run.camera, 1, rt.options(W, H, P, counters=cnt.p, kernel=rt.KERNEL_WAVEFRONT))
+    rt.render(run.dev, g, run.camera, 1, rt.options(W, H, P, adaptive=False, counters=cnt.p, kernel=rt.KERNEL_WAVEFRONT))
     c = cnt.read()
     assert c["watchdog"] == 0, c
     assert c["sample"] == W * H * P
