@@ -27,7 +27,13 @@
  * thread).  Pointers named *_device are HIP device pointers.  The caller owns
  * every allocation and frees it explicitly (the reference leaks; see
  * rt/screen.cuh:24-31).  Calls are synchronous unless an RtOptions.stream is
- * given, in which case rt_render only enqueues.
+ * given, in which case the megakernel (RT_KERNEL_MEGA) only enqueues.  The
+ * wavefront kernels (the default) BLOCK the calling thread until the call's
+ * queue iterations are done: their host threads read each iteration's live
+ * path count to decide the next launch.  Only the last long-path slice and
+ * the pipelines' join are left enqueued on the given stream when they return.
+ * Consecutive calls may use different streams: a call waits for the previous
+ * call's device work first (they share the per-device workspace).
  */
 #ifndef ISAKLM_RT_H
 #define ISAKLM_RT_H

@@ -121,3 +121,21 @@ def test_two_rank_row_shards_equal_single_stream():
     np.testing.assert_array_equal(got[0].view(np.uint32), single[0].view(np.uint32))
     np.testing.assert_array_equal(got[1].view(np.uint32), single[1].view(np.uint32))
     np.testing.assert_array_equal(got[2], single[2])
+
+
+def test_bench_launcher_starts_n_ranks():
+    """`bench.py --gpus 2` (as the driver runs it, no WORLD_SIZE in the env)
+    starts its two ranks itself; they meet over gloo and rank 0 frames the
+    line with n_gpus 2 (--dry-run: the rank wiring only, no GPU)."""
+    import json
+    import subprocess
+    import sys
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(helpers.ROOT, "bench.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 2
+    assert line["config"]["parallelism"] == "spp-sliced x2 + RCCL reduce"
+    assert sorted(tuple(x) for x in line["ranks"]) == [(0, 0, 2), (1, 1, 2)]

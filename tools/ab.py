@@ -52,6 +52,12 @@ def main():
             if v.split(":")[0] != "0":
                 profs[v].append(rt.last_profile())
     out = {}
+    if os.environ.get("AB_NO_COUNT"):  # timing only (tools/gpu_ab_libs.sh)
+        for v in variants:
+            ts = np.array(times[v])
+            out[v] = {"msamples_s_median": round(W * H * P / np.median(ts) / 1e6, 3), "s": [round(x, 3) for x in ts]}
+        print(json.dumps({"scene": scene, "passes": P, "max_depth": maxd, "variants": out}, indent=1))
+        return
     for v in variants:
         cnt = rt.DeviceCounters()
         g.upload(zf3, zf, zi, rt.seeds(n, 0))
