@@ -30,6 +30,18 @@
 using namespace rtk;
 
 #define WF_BLOCK 256
+#ifndef WF_TBLOCK
+#define WF_TBLOCK 256 // threads per block of the queue kernels (wf_trace_coop, wf_shade)
+#endif
+// wave priorities beside the other pipelines' trace waves (A/B, 4 rounds:
+// -1 % call time together): a pipeline's shade launch and the tail of its
+// trace launch are on its critical path, the other launches' bulk is not
+#ifndef WF_SHADE_PRIO
+#define WF_SHADE_PRIO 3
+#endif
+#ifndef WF_TAIL_PRIO
+#define WF_TAIL_PRIO 2
+#endif
 #ifndef WF_LDS_STACK
 #define WF_LDS_STACK 8  // stack entries in LDS; deeper ones spill to HBM (rare)
 #endif
@@ -368,7 +380,7 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_trace_dyn(RtDevScene sc, WfState 
 // capped at `cap` node fetches per round and the leaf test waits for
 // `postpone` pending lanes.
 template <bool COUNT>
-__global__ void __launch_bounds__(WF_BLOCK, WF_TRACE_WAVES) wf_trace_coop(RtDevScene sc, WfState st, int q,
+__global__ void __launch_bounds__(WF_TBLOCK, WF_TRACE_WAVES) wf_trace_coop(RtDevScene sc, WfState st, int q,
                                                           unsigned long long *counters, int cap, int postpone,
                                                           int wide_lanes, unsigned long long *timeline)
 {
@@ -376,16 +388,16 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_TRACE_WAVES) wf_trace_coop(RtDevS
     // launch's first wave start, first queue exhaustion, last wave end
     // (stored as ~t so that all three are atomicMin)
     if (timeline && __lane_id() == 0) atomicMin(timeline, __builtin_amdgcn_s_memrealtime());
-    __shared__ uint32_t s_node[WF_LDS_STACK * WF_BLOCK];
-    __shared__ float s_entry[WF_LDS_STACK * WF_BLOCK];
-    __shared__ unsigned long long s_key[WF_BLOCK];
-    __shared__ CoopCand s_list[(WF_BLOCK / 64) * WF_COOP_LIST];
-    __shared__ int s_mark[2 * WF_BLOCK]; // 128 per wave: chunk_owner marks + junk slots
+    __shared__ uint32_t s_node[WF_LDS_STACK * WF_TBLOCK];
+    __shared__ float s_entry[WF_LDS_STACK * WF_TBLOCK];
+    __shared__ unsigned long long s_key[WF_TBLOCK];
+    __shared__ CoopCand s_list[(WF_TBLOCK / 64) * WF_COOP_LIST];
+    __shared__ int s_mark[2 * WF_TBLOCK]; // 128 per wave: chunk_owner marks + junk slots
     const int tid = threadIdx.x;
-    const int gtid = blockIdx.x * WF_BLOCK + tid;
+    const int gtid = blockIdx.x * WF_TBLOCK + tid;
     const int lane = __lane_id();
     const int wave = tid >> 6;
-    Stack<WF_LDS_STACK> stk{s_node + tid, s_entry + tid, WF_BLOCK, st.spill + gtid, st.spill_threads};
+    Stack<WF_LDS_STACK> stk{s_node + tid, s_entry + tid, WF_TBLOCK, st.spill + gtid, st.spill_threads};
     unsigned long long *wkey = s_key + wave * 64;
     CoopCand *list = s_list + wave * WF_COOP_LIST;
     const CoopLds w{wkey, list, s_mark + wave * 128};
@@ -422,6 +434,7 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_TRACE_WAVES) wf_trace_coop(RtDevS
             }
         }
         if (COUNT && lane == 0) c.v[RT_CNT_T_FETCH] += __builtin_amdgcn_s_memtime() - tf;
+        if (WF_TAIL_PRIO > 0 && __any(exhausted)) __builtin_amdgcn_s_setprio(WF_TAIL_PRIO); // the launch's tail
         if (!__any(r.live)) {
             if (__all(exhausted)) break;
             continue;
@@ -444,7 +457,7 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_TRACE_WAVES) wf_trace_coop(RtDevS
         for (unsigned long long mm = lm; mm; mm &= mm - 1) {
             const int owner = __ffsll((long long)mm) - 1;
             const int ot = wave * 64 + owner;
-            const Stack<WF_LDS_STACK> so{s_node + ot, s_entry + ot, WF_BLOCK, st.spill + blockIdx.x * WF_BLOCK + ot,
+            const Stack<WF_LDS_STACK> so{s_node + ot, s_entry + ot, WF_TBLOCK, st.spill + blockIdx.x * WF_TBLOCK + ot,
                                          st.spill_threads};
             int tri = -1;
             float bx = 0.0f, by = 0.0f, bz = 0.0f;
@@ -596,14 +609,15 @@ __device__ __forceinline__ bool shade_step(const RtDevScene &sc, const RtDevFram
 } // namespace
 
 template <bool COUNT>
-__global__ void __launch_bounds__(WF_BLOCK) wf_shade(RtDevScene sc, RtDevFrame fr, RtDevCamera cam, WfState st, int q)
+__global__ void __launch_bounds__(WF_TBLOCK) wf_shade(RtDevScene sc, RtDevFrame fr, RtDevCamera cam, WfState st, int q)
 {
+    if (WF_SHADE_PRIO > 0) __builtin_amdgcn_s_setprio(WF_SHADE_PRIO); // ahead of co-resident trace waves
     Cnt c;
     if (COUNT) c.zero();
     const uint32_t n = st.counts[q];
     const int qn = q ^ 1;
     const int limit = fr.max_depth > 0 ? fr.max_depth : RT_WATCHDOG_BOUNCES;
-    for (uint32_t base = blockIdx.x * WF_BLOCK; base < n; base += gridDim.x * WF_BLOCK) {
+    for (uint32_t base = blockIdx.x * WF_TBLOCK; base < n; base += gridDim.x * WF_TBLOCK) {
         const uint32_t e = base + threadIdx.x;
         bool want = false;
         PathRegs p;
@@ -1054,6 +1068,7 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
     // of the launch was its tail).  Measured 512 / 704 / 1,536: 37.5 / 37.6 /
     // 33.1 Msamples/s on room2m 1080p (tools/gpu_sweep.sh, profiles/r02).
     const int grid = grid_env >= 64 && grid_env <= 16384 ? grid_env : 512;
+    const int tgrid = grid * (WF_BLOCK / WF_TBLOCK); // the same waves in WF_TBLOCK-thread blocks
     const size_t slots = (size_t)fr.width * fr.height;
     const bool count = fr.counters != nullptr;
     const bool prof = profile != 0;
@@ -1200,10 +1215,10 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
                     const int li = it * npipes + pi;
                     unsigned long long *tl = fr.wave_times && li < WF_TIMELINE_LAUNCHES ? fr.wave_times + 3 * li : nullptr;
                     if (count)
-                        hipLaunchKernelGGL(wf_trace_coop<true>, dim3(grid), dim3(WF_BLOCK), 0, s, sc, st, q,
+                        hipLaunchKernelGGL(wf_trace_coop<true>, dim3(tgrid), dim3(WF_TBLOCK), 0, s, sc, st, q,
                                            fr.counters, cap, postpone, wide_lanes, tl);
                     else
-                        hipLaunchKernelGGL(wf_trace_coop<false>, dim3(grid), dim3(WF_BLOCK), 0, s, sc, st, q,
+                        hipLaunchKernelGGL(wf_trace_coop<false>, dim3(tgrid), dim3(WF_TBLOCK), 0, s, sc, st, q,
                                            fr.counters, cap, postpone, wide_lanes, tl);
                 } else if (trace_kind == 3) {
                     if (count) hipLaunchKernelGGL(wf_trace_dyn<true>, dim3(grid), dim3(WF_BLOCK), 0, s, sc, st, q, fr.counters);
@@ -1213,8 +1228,8 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
                     else hipLaunchKernelGGL(wf_trace<false>, dim3(grid), dim3(WF_BLOCK), 0, s, sc, st, q, fr.counters);
                 }
                 if (!mark(5)) return -1;
-                if (count) hipLaunchKernelGGL(wf_shade<true>, dim3(grid), dim3(WF_BLOCK), 0, s, sc, fr, cam, st, q);
-                else hipLaunchKernelGGL(wf_shade<false>, dim3(grid), dim3(WF_BLOCK), 0, s, sc, fr, cam, st, q);
+                if (count) hipLaunchKernelGGL(wf_shade<true>, dim3(tgrid), dim3(WF_TBLOCK), 0, s, sc, fr, cam, st, q);
+                else hipLaunchKernelGGL(wf_shade<false>, dim3(tgrid), dim3(WF_TBLOCK), 0, s, sc, fr, cam, st, q);
                 if (hipGetLastError() != hipSuccess) return -1;
                 if (!mark(2)) return -1;
                 if (hipMemcpyAsync(pp.host_count, st.counts + (q ^ 1), 4, hipMemcpyDeviceToHost, s) != hipSuccess)
