@@ -7,7 +7,11 @@
  * (rt/trace_ray.cuh:244-318) and, at every non-empty leaf it tests, checks
  * whether the ray segment [0, leaf exit] meets the union AABB of the leaf's
  * triangles (grown by a relative margin).  Prints the share of leaf tests and
- * of triangle tests in leaves whose box the segment misses.
+ * of triangle tests in leaves whose box the segment misses, and the share of
+ * triangle tests that repeat a triangle the same ray already tested in an
+ * earlier leaf (the KD builder duplicates straddling triangles into both
+ * children: a per-ray mailbox could skip those whose first test failed for a
+ * leaf-independent reason).
  * Build: gcc -O2 -fopenmp tools/leaf_cull_probe.c -o /tmp/leaf_cull_probe -lm */
 #include <float.h>
 #include <math.h>
@@ -76,9 +80,11 @@ int main(int argc, char **argv)
             lbox[i][3 + c] = b[3 + c] + g;
         }
     }
-    unsigned long long leaves = 0, culled = 0, tris = 0, tris_culled = 0, win_culled = 0;
-#pragma omp parallel for schedule(dynamic, 256) reduction(+ : leaves, culled, tris, tris_culled, win_culled)
+    unsigned long long leaves = 0, culled = 0, tris = 0, tris_culled = 0, win_culled = 0, repeats = 0;
+#pragma omp parallel for schedule(dynamic, 256) reduction(+ : leaves, culled, tris, tris_culled, win_culled, repeats)
     for (int r = 0; r < nr; ++r) {
+        int seen_ids[4096];
+        int nseen = 0;
         const float *o = rays + 6 * r, *d = rays + 6 * r + 3;
         /* scene box: the root box is not needed for the statistics, start at [0, inf) */
         int ni[64];
@@ -115,6 +121,14 @@ int main(int argc, char **argv)
                 if (b < t1) t1 = b;
             }
             const int miss = t0 > t1;
+            /* mailbox probe: triangles of this leaf already tested earlier along this ray */
+            for (int k = 0; k < L->b; ++k) {
+                const int tt = idx[L->a + k];
+                int seen = 0;
+                for (int m = 0; m < nseen && !seen; ++m) seen = seen_ids[m] == tt;
+                if (seen) ++repeats;
+                else if (nseen < 4096) seen_ids[nseen++] = tt;
+            }
             ++leaves;
             tris += (unsigned long long)L->b;
             /* the reference's leaf test: hit = any triangle with 1e-5 <= s < exit inside */
@@ -148,7 +162,9 @@ int main(int argc, char **argv)
         }
     }
     printf("{\"rays\": %d, \"leaf_tests\": %llu, \"leaf_tests_box_missed\": %llu, \"tri_tests\": %llu, "
-           "\"tri_tests_box_missed\": %llu, \"frac_leaves\": %.4f, \"frac_tris\": %.4f, \"hits_in_missed_boxes\": %llu}\n",
-           nr, leaves, culled, tris, tris_culled, (double)culled / leaves, (double)tris_culled / tris, win_culled);
+           "\"tri_tests_box_missed\": %llu, \"frac_leaves\": %.4f, \"frac_tris\": %.4f, \"hits_in_missed_boxes\": %llu, "
+           "\"repeat_tests\": %llu, \"frac_repeat\": %.4f}\n",
+           nr, leaves, culled, tris, tris_culled, (double)culled / leaves, (double)tris_culled / tris, win_culled,
+           repeats, (double)repeats / tris);
     return 0;
 }
