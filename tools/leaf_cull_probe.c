@@ -80,11 +80,12 @@ int main(int argc, char **argv)
             lbox[i][3 + c] = b[3 + c] + g;
         }
     }
-    unsigned long long leaves = 0, culled = 0, tris = 0, tris_culled = 0, win_culled = 0, repeats = 0;
-#pragma omp parallel for schedule(dynamic, 256) reduction(+ : leaves, culled, tris, tris_culled, win_culled, repeats)
+    unsigned long long leaves = 0, culled = 0, tris = 0, tris_culled = 0, win_culled = 0, repeats = 0, cands = 0,
+                       cand_repeats = 0;
+#pragma omp parallel for schedule(dynamic, 256) reduction(+ : leaves, culled, tris, tris_culled, win_culled, repeats, cands, cand_repeats)
     for (int r = 0; r < nr; ++r) {
-        int seen_ids[4096];
-        int nseen = 0;
+        int seen_ids[4096], bary_failed[4096];
+        int nseen = 0, nbf = 0;
         const float *o = rays + 6 * r, *d = rays + 6 * r + 3;
         /* scene box: the root box is not needed for the statistics, start at [0, inf) */
         int ni[64];
@@ -133,7 +134,7 @@ int main(int argc, char **argv)
             tris += (unsigned long long)L->b;
             /* the reference's leaf test: hit = any triangle with 1e-5 <= s < exit inside */
             int hit = 0;
-            for (int k = 0; k < L->b && !hit; ++k) {
+            for (int k = 0; k < L->b; ++k) {
                 const uint8_t *T = traw + 152 * (size_t)idx[L->a + k];
                 float p[9];
                 memcpy(p, T, 36);
@@ -151,7 +152,13 @@ int main(int argc, char **argv)
                 float d20 = q[0] * e1[0] + q[1] * e1[1] + q[2] * e1[2], d21 = q[0] * e2[0] + q[1] * e2[1] + q[2] * e2[2];
                 float rd = 1.0f / (d00 * d11 - d01 * d01);
                 float v = (d11 * d20 - d01 * d21) * rd, w = (d00 * d21 - d01 * d20) * rd, u = 1.0f - v - w;
+                ++cands;
+                const int tt = idx[L->a + k];
+                int seen = 0;
+                for (int m = 0; m < nbf && !seen; ++m) seen = bary_failed[m] == tt;
+                if (seen) ++cand_repeats;
                 if (u >= 0 && u <= 1 && v >= 0 && v <= 1 && w >= 0 && w <= 1) hit = 1;
+                else if (!seen && nbf < 4096) bary_failed[nbf++] = tt;
             }
             if (miss) {
                 ++culled;
@@ -163,8 +170,9 @@ int main(int argc, char **argv)
     }
     printf("{\"rays\": %d, \"leaf_tests\": %llu, \"leaf_tests_box_missed\": %llu, \"tri_tests\": %llu, "
            "\"tri_tests_box_missed\": %llu, \"frac_leaves\": %.4f, \"frac_tris\": %.4f, \"hits_in_missed_boxes\": %llu, "
-           "\"repeat_tests\": %llu, \"frac_repeat\": %.4f}\n",
+           "\"repeat_tests\": %llu, \"frac_repeat\": %.4f, \"bary_tests\": %llu, "
+           "\"bary_repeats_of_failed\": %llu, \"frac_bary_repeat\": %.4f}\n",
            nr, leaves, culled, tris, tris_culled, (double)culled / leaves, (double)tris_culled / tris, win_culled,
-           repeats, (double)repeats / tris);
+           repeats, (double)repeats / tris, cands, cand_repeats, (double)cand_repeats / cands);
     return 0;
 }
