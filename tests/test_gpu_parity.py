@@ -295,3 +295,31 @@ def test_room2m_glass_adaptive_full_frame_sparse_pixels():
     assert rcnt["skip"] > 0  # the adaptive test really skipped pixel-passes
     assert rcnt["watchdog"] == 0  # no path cut by the 65,536-bounce watchdog
     assert helpers.rel_linf(gpu[0][pixels], gpu[2][pixels], ref[0][pixels], ref[2][pixels]) < 1e-4
+
+
+def test_consecutive_calls_on_different_streams():
+    """rt_render on stream A, then at once on stream B (no host sync between):
+    the second call shares the device workspace (path state, long-path
+    hand-off) and must wait for the first call's last wf_long slice and
+    pipelines.  Every path deeper than 1 bounce goes through wf_long here, so
+    the first call's slices are still running when the second starts."""
+    import ctypes
+
+    hip = ctypes.CDLL("libamdhip64.so")
+    streams = [ctypes.c_void_p(), ctypes.c_void_p()]
+    for s in streams:
+        assert hip.hipStreamCreate(ctypes.byref(s)) == 0
+    try:
+        run = helpers.GpuRun("room_small")
+        W, H, P = 48, 27, 3
+        g = rt.GBuffer(W, H)
+        for c, s in enumerate(streams):
+            opt = rt.options(W, H, P, adaptive=False, kernel=rt.KERNEL_WAVEFRONT, wf_long_depth=1, stream=s)
+            rt.render(run.dev, g, run.camera, 0 if c == 0 else 1, opt)
+        rt.check(rt.lib().rt_synchronize())
+        gpu = g.download()
+        ref, _ = helpers.oracle_render(run.path, W, H, P, calls=2)
+        helpers.assert_bitwise(gpu, ref, what="two streams")
+    finally:
+        for s in streams:
+            hip.hipStreamDestroy(s)
