@@ -253,18 +253,33 @@ def test_room2m_full_frame_sparse_pixels(kernel):
     assert np.all(gpu[2] == P)
 
 
+@pytest.mark.timeout(280)
+def test_room2m_every_pixel_bench_options():
+    """Every one of the 2,073,600 pixels of the 1920x1080 room2m frame, 2
+    passes with the bench's kernel and defaults (pipelines, long-path
+    hand-off, wide tails, finisher), bit-identical to the oracle (~25 s of
+    oracle time on the GPU box's 16 cores)."""
+    run = helpers.GpuRun("room2m")
+    W, H, P = 1920, 1080, 2
+    gpu, _, _ = run.render(W, H, P, kernel=rt.KERNEL_WAVEFRONT)
+    ref, rcnt = helpers.oracle_render(run.path, W, H, P)
+    helpers.assert_bitwise(gpu, ref, what="room2m every pixel")
+    assert rcnt["sample"] == W * H * P and rcnt["watchdog"] == 0
+    assert helpers.rel_linf(gpu[0], gpu[2], ref[0], ref[2]) < 1e-4
+
+
 @pytest.mark.timeout(240)
 def test_room2m_bench_configuration_sparse_pixels():
     """bench.py's timed configuration exactly: room2m at 1920x1080, two
     rt_render calls of 64 passes (sample_count 0 then 1), wavefront kernel with
     its defaults (3 pipelines, long-path hand-off at depth 64, wide tails,
-    cooperative finisher), no counters (the bench's kernels).  Every 4099th
+    cooperative finisher), no counters (the bench's kernels).  Every 1031st
     pixel re-rendered by the oracle over the same 128 spp.  A counted call of
     the same options must not fire the 65,536-bounce watchdog."""
     run = helpers.GpuRun("room2m")
     W, H, P = 1920, 1080, 64
     gpu, _, g = run.render(W, H, P, calls=2, kernel=rt.KERNEL_WAVEFRONT)
-    pixels = np.arange(0, W * H, 4099, dtype=np.int32)
+    pixels = np.arange(0, W * H, 1031, dtype=np.int32)
     ref, rcnt = helpers.oracle_render(run.path, W, H, P, calls=2, pixels=pixels)
     helpers.assert_bitwise(gpu, ref, pixels=pixels, what="room2m bench configuration")
     assert np.all(gpu[2] == 2 * P)
