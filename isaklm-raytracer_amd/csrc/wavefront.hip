@@ -64,13 +64,15 @@ using namespace rtk;
 
 struct WfState {
     int *passes_left;
-    uint32_t *flags;   // bit0 shadow, bit1 inside, bits 2..4 prev_type, bits 8.. depth
+    uint32_t *flags;   // bit0 shadow, bit1 inside, bits 2..4 prev_type, bit5 dual, bit6 ext_live, bits 8.. depth
     Vec3D *T, *L, *cont, *snorm, *rp;
+    Vec3D *ro;         // origin of the path's pending ray(s); cont = the pending extension direction
+    uint32_t *e_sh, *e_ext; // queue entries of the path's pending shadow / extension ray
     int *light;
-    uint32_t *q_slot[2];
-    RtF4 *q_ray[2];    // 2 per entry: {o.xyz, -}, {d.xyz, -}
-    RtF4 *hits;        // per queue entry: {tri bits, bx, by, bz}
-    uint32_t *counts;  // [0], [1]: queue sizes
+    uint32_t *q_slot[2]; // path lists: the pixels (slots) with rays in ray queue q
+    RtF4 *q_ray[2];    // ray queues, 2 RtF4 per entry: {o.xyz, -}, {d.xyz, -}
+    RtF4 *hits;        // per ray-queue entry: {tri bits, bx, by, bz}
+    uint32_t *counts;  // [0], [1]: ray queue sizes; [2], [3]: fetch cursors; [4] finisher fetch; [6], [7]: path list sizes
     uint2 *spill;      // traversal stack spill
     int spill_threads;
     // long-path hand-off (wf_long): a path deeper than long_depth leaves its
@@ -85,23 +87,36 @@ namespace {
 
 __device__ __forceinline__ uint32_t lanemask_lt() { return (uint32_t)__lane_id(); }
 
-// append `want` lanes' rays to queue q (wave-aggregated atomic)
-__device__ __forceinline__ void enqueue(const WfState &st, int q, bool want, uint32_t slot, Vec3D o, Vec3D d)
+// wave-aggregated append of `want` lanes to the list counted by *ctr: returns
+// each wanting lane's index
+__device__ __forceinline__ uint32_t wave_append(uint32_t *ctr, bool want)
 {
     const unsigned long long mask = __ballot(want);
-    if (mask == 0) return;
+    if (mask == 0) return 0;
     const int lane = __lane_id();
     const int leader = __ffsll((long long)mask) - 1;
-    const int rank = __popcll(mask & ((1ull << lane) - 1ull));
     uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(st.counts + q, (uint32_t)__popcll(mask));
+    if (lane == leader) base = atomicAdd(ctr, (uint32_t)__popcll(mask));
     base = __shfl(base, leader);
+    return base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+}
+
+// append `want` lanes' rays to ray queue q; returns the entry
+__device__ __forceinline__ uint32_t enqueue_ray(const WfState &st, int q, bool want, Vec3D o, Vec3D d)
+{
+    const uint32_t e = wave_append(st.counts + q, want);
     if (want) {
-        const uint32_t e = base + (uint32_t)rank;
-        st.q_slot[q][e] = slot;
         st.q_ray[q][2 * (size_t)e] = RtF4{o.x, o.y, o.z, 0.0f};
         st.q_ray[q][2 * (size_t)e + 1] = RtF4{d.x, d.y, d.z, 0.0f};
     }
+    return e;
+}
+
+// append `want` lanes' paths to path list q
+__device__ __forceinline__ void enqueue_path(const WfState &st, int q, bool want, uint32_t slot)
+{
+    const uint32_t i = wave_append(st.counts + 6 + q, want);
+    if (want) st.q_slot[q][i] = slot;
 }
 
 // hand `to_long` lanes' paths (state already stored) to wf_long: reserve an
@@ -184,8 +199,12 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_start(RtDevFrame fr, RtDevCamera 
         st.flags[slot] = 1u << 8; // depth 1 (first extension ray), prev PRIMARY
         st.T[slot] = rt_v3(1.0f, 1.0f, 1.0f);
         st.L[slot] = rt_v3(0.0f, 0.0f, 0.0f);
+        st.ro[slot] = ro;
+        st.cont[slot] = rd;
     }
-    enqueue(st, 0, want, (uint32_t)slot, ro, rd);
+    const uint32_t e = enqueue_ray(st, 0, want, ro, rd);
+    if (want) st.e_ext[slot] = e;
+    enqueue_path(st, 0, want, (uint32_t)slot);
     if (COUNT) flush_counters(c, fr.counters);
 }
 
@@ -475,6 +494,8 @@ namespace {
 struct PathRegs {
     uint32_t slot;
     bool shadow, inside;
+    bool dual;     // the roulette after this path's pending shadow ray was drawn when it was set up
+    bool ext_live; // ... and let the path continue: its extension ray (ro, cont) is pending too
     int prev_type, depth, passes_left, light;
     uint32_t rng;
     Vec3D T, L, rp, cont, snorm, ro, rd;
@@ -487,6 +508,8 @@ __device__ __forceinline__ void load_regs(const WfState &st, const RtDevFrame &f
     p.shadow = flags & 1u;
     p.inside = (flags >> 1) & 1u;
     p.prev_type = (int)((flags >> 2) & 7u);
+    p.dual = (flags >> 5) & 1u;
+    p.ext_live = (flags >> 6) & 1u;
     p.depth = (int)(flags >> 8);
     p.rng = fr.rng[slot];
     p.T = st.T[slot];
@@ -508,7 +531,7 @@ __device__ __forceinline__ void store_regs(const WfState &st, const RtDevFrame &
     st.L[slot] = p.L;
     st.passes_left[slot] = p.passes_left;
     st.flags[slot] = (p.shadow ? 1u : 0u) | (p.inside ? 2u : 0u) | ((uint32_t)p.prev_type << 2) |
-                     ((uint32_t)p.depth << 8);
+                     (p.dual ? 0x20u : 0u) | (p.ext_live ? 0x40u : 0u) | ((uint32_t)p.depth << 8);
     if (p.shadow) {
         st.light[slot] = p.light;
         st.rp[slot] = p.rp;
@@ -517,10 +540,27 @@ __device__ __forceinline__ void store_regs(const WfState &st, const RtDevFrame &
     }
 }
 
+// a path of a path list with its first pending ray in p.ro / p.rd (the
+// shadow ray if one is pending: its direction recomputed as it was set up)
+__device__ __forceinline__ void first_ray(const WfState &st, const RtDevFrame &fr, uint32_t slot, PathRegs &p)
+{
+    load_regs(st, fr, slot, p);
+    p.ro = st.ro[slot];
+    p.rd = p.shadow ? rt_normalize(p.rp - p.ro) : st.cont[slot];
+}
+
 // One event of trace_path (rt/path_tracing.cuh:268-325) for the hit of the
 // ray p.ro/p.rd: emission, BSDF, NEE set-up, roulette, accumulation and the
 // pixel's next pass.  Returns true with the next ray in p.ro/p.rd.
-template <bool COUNT>
+//
+// DUAL (the queue kernels): when NEE sets up a shadow ray, the Russian
+// roulette that the reference draws after the shadow ray (:309-318) is drawn
+// right away — nothing between consumes random numbers or changes the
+// throughput — so the extension ray (p.ro, p.cont) can be traced in the SAME
+// queue iteration as the shadow ray (p.dual, p.ext_live).  The shadow result
+// is still applied first (L += direct * T, then T /= p), in the reference's
+// order.  Any shade_step (DUAL or not) resumes such a path correctly.
+template <bool COUNT, bool DUAL = false>
 __device__ __forceinline__ bool shade_step(const RtDevScene &sc, const RtDevFrame &fr, const RtDevCamera &cam,
                                            PathRegs &p, int hit, float bx, float by, float bz, int limit, Cnt &c)
 {
@@ -554,6 +594,20 @@ __device__ __forceinline__ bool shade_step(const RtDevScene &sc, const RtDevFram
                     p.shadow = true;
                     roulette = false; // roulette after the shadow ray
                     want = true;
+                    if (DUAL) { // the roulette now (the same draw as after the shadow ray)
+                        const float pr = fmaxf(p.T.x, fmaxf(p.T.y, p.T.z));
+                        const float r = rng_next(p.rng);
+                        p.dual = true;
+                        p.ext_live = false;
+                        if (!(r > pr)) {
+                            if (p.depth == limit) { // max_depth / watchdog before the next extension ray
+                                if (COUNT && fr.max_depth <= 0) c.v[RT_CNT_WATCHDOG]++;
+                            } else {
+                                ++p.depth;
+                                p.ext_live = true;
+                            }
+                        }
+                    }
                 }
             }
         }
@@ -565,6 +619,17 @@ __device__ __forceinline__ bool shade_step(const RtDevScene &sc, const RtDevFram
         p.L = p.L + direct * p.T;
         p.rd = p.cont;
         p.shadow = false;
+        if (p.dual) { // the roulette was drawn at the set-up
+            p.dual = false;
+            roulette = false;
+            if (p.ext_live) {
+                p.T = p.T * (1.0f / fmaxf(p.T.x, fmaxf(p.T.y, p.T.z)));
+                want = true; // depth was advanced at the set-up
+            } else {
+                finish = true;
+            }
+            p.ext_live = false;
+        }
     }
     if (roulette) { // Russian roulette (:309-318)
         float pr = fmaxf(p.T.x, fmaxf(p.T.y, p.T.z));
@@ -614,25 +679,51 @@ __global__ void __launch_bounds__(WF_TBLOCK) wf_shade(RtDevScene sc, RtDevFrame 
     if (WF_SHADE_PRIO > 0) __builtin_amdgcn_s_setprio(WF_SHADE_PRIO); // ahead of co-resident trace waves
     Cnt c;
     if (COUNT) c.zero();
-    const uint32_t n = st.counts[q];
+    const uint32_t n = st.counts[6 + q]; // paths with rays in ray queue q
     const int qn = q ^ 1;
     const int limit = fr.max_depth > 0 ? fr.max_depth : RT_WATCHDOG_BOUNCES;
     for (uint32_t base = blockIdx.x * WF_TBLOCK; base < n; base += gridDim.x * WF_TBLOCK) {
-        const uint32_t e = base + threadIdx.x;
+        const uint32_t i = base + threadIdx.x;
         bool want = false;
         PathRegs p;
         p.slot = 0;
-        p.ro = p.rd = rt_v3(0, 0, 0);
-        if (e < n) {
-            load_regs(st, fr, st.q_slot[q][e], p);
-            const RtF4 h = ldf4(st.hits + e);
-            p.ro = ld3(ldf4(st.q_ray[q] + 2 * (size_t)e));
-            p.rd = ld3(ldf4(st.q_ray[q] + 2 * (size_t)e + 1));
-            want = shade_step<COUNT>(sc, fr, cam, p, __float_as_int(h.x), h.y, h.z, h.w, limit, c);
+        p.shadow = p.ext_live = false;
+        p.ro = p.rd = p.cont = rt_v3(0, 0, 0);
+        if (i < n) {
+            const uint32_t slot = st.q_slot[q][i];
+            load_regs(st, fr, slot, p);
+            p.ro = st.ro[slot];
+            if (p.shadow) {
+                // the shadow ray (set up DUAL: its roulette is drawn) and, if the
+                // path went on, its extension ray were traced in this iteration
+                const bool both = p.ext_live;
+                p.rd = rt_normalize(p.rp - p.ro); // the shadow ray's direction, as set up
+                const RtF4 h = ldf4(st.hits + st.e_sh[slot]);
+                want = shade_step<COUNT, true>(sc, fr, cam, p, __float_as_int(h.x), h.y, h.z, h.w, limit, c);
+                if (both) { // p.ro / p.rd = the extension ray: its hit is in too
+                    const RtF4 g = ldf4(st.hits + st.e_ext[slot]);
+                    want = shade_step<COUNT, true>(sc, fr, cam, p, __float_as_int(g.x), g.y, g.z, g.w, limit, c);
+                }
+            } else {
+                p.rd = st.cont[slot];
+                const RtF4 h = ldf4(st.hits + st.e_ext[slot]);
+                want = shade_step<COUNT, true>(sc, fr, cam, p, __float_as_int(h.x), h.y, h.z, h.w, limit, c);
+            }
             store_regs(st, fr, p);
+            if (want) { // the pending ray(s): extension = (ro, cont)
+                st.ro[slot] = p.ro;
+                st.cont[slot] = p.shadow ? p.cont : p.rd;
+            }
         }
         const bool to_long = want && st.long_depth > 0 && p.depth > st.long_depth;
-        enqueue(st, qn, want && !to_long, p.slot, p.ro, p.rd);
+        const bool go = want && !to_long;
+        const bool sh = go && p.shadow, ex = go && (!p.shadow || p.ext_live);
+        const uint32_t es = enqueue_ray(st, qn, sh, p.ro, p.rd);
+        const uint32_t ee = enqueue_ray(st, qn, ex, p.ro, p.shadow ? p.cont : p.rd);
+        if (sh) st.e_sh[p.slot] = es;
+        if (ex) st.e_ext[p.slot] = ee;
+        enqueue_path(st, qn, go, p.slot);
+        // wf_long takes the path with its first pending ray (the shadow ray if any)
         if (__any(to_long)) publish_long(st, to_long, p.slot, p.ro, p.rd);
     }
     if (COUNT) flush_counters(c, fr.counters);
@@ -652,15 +743,13 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_finish(RtDevScene sc, RtDevFrame 
     Stack<WF_LDS_STACK> stk{s_node + tid, s_entry + tid, WF_BLOCK, st.spill + gtid, st.spill_threads};
     Cnt c;
     if (COUNT) c.zero();
-    const uint32_t n = st.counts[q];
+    const uint32_t n = st.counts[6 + q]; // paths of path list q
     const int limit = fr.max_depth > 0 ? fr.max_depth : RT_WATCHDOG_BOUNCES;
     for (uint32_t base = blockIdx.x * WF_BLOCK; base < n; base += gridDim.x * WF_BLOCK) {
         const uint32_t e = base + tid;
         if (e < n) {
             PathRegs p;
-            load_regs(st, fr, st.q_slot[q][e], p);
-            p.ro = ld3(ldf4(st.q_ray[q] + 2 * (size_t)e));
-            p.rd = ld3(ldf4(st.q_ray[q] + 2 * (size_t)e + 1));
+            first_ray(st, fr, st.q_slot[q][e], p);
             while (true) {
                 float bx = 0.0f, by = 0.0f, bz = 0.0f;
                 const int hit = trace<COUNT>(sc, p.ro, p.rd, bx, by, bz, stk, c);
@@ -702,7 +791,7 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_finish_coop(RtDevScene sc, RtDevF
     const CoopLds w{wkey, list, s_mark + wave * 128};
     Cnt c;
     if (COUNT) c.zero();
-    const uint32_t n = st.counts[q];
+    const uint32_t n = st.counts[6 + q]; // paths of path list q
     uint32_t *fetch = st.counts + 4;
     const int limit = fr.max_depth > 0 ? fr.max_depth : RT_WATCHDOG_BOUNCES;
 
@@ -731,9 +820,7 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_finish_coop(RtDevScene sc, RtDevF
                     exhausted = true;
                 } else {
                     active = true;
-                    load_regs(st, fr, st.q_slot[q][e], p);
-                    p.ro = ld3(ldf4(st.q_ray[q] + 2 * (size_t)e));
-                    p.rd = ld3(ldf4(st.q_ray[q] + 2 * (size_t)e + 1));
+                    first_ray(st, fr, st.q_slot[q][e], p);
                     if (COUNT) c.v[RT_CNT_RAY]++;
                     if (!coop_begin(sc, r, p.ro, p.rd)) {
                         pending = true;
@@ -974,18 +1061,20 @@ int ensure(Workspace &w, size_t slots, int grid, int npipes)
     };
     // per pixel
     const size_t o_pl = take(slots * 4), o_fl = take(slots * 4), o_T = take(slots * 12), o_L = take(slots * 12),
-                 o_c = take(slots * 12), o_n = take(slots * 12), o_rp = take(slots * 12), o_li = take(slots * 4);
+                 o_c = take(slots * 12), o_n = take(slots * 12), o_rp = take(slots * 12), o_li = take(slots * 4),
+                 o_ro = take(slots * 12), o_es = take(slots * 4), o_ee = take(slots * 4);
     // long-path hand-off (shared by the pipelines), wf_long's stack-free wide traversal needs no spill
     const size_t o_lf = take(slots * 4), o_lr = take(slots * 32), o_lc = take(256);
-    // per pipeline (queues sized for every pixel: a pipeline never holds more)
+    // per pipeline (path lists sized for every pixel: a pipeline never holds
+    // more; ray queues for two rays per path: a shadow and an extension ray)
     size_t o_qs0[WF_MAX_PIPES], o_qs1[WF_MAX_PIPES], o_qr0[WF_MAX_PIPES], o_qr1[WF_MAX_PIPES], o_h[WF_MAX_PIPES],
         o_cnt[WF_MAX_PIPES], o_sp[WF_MAX_PIPES];
     for (int i = 0; i < WF_MAX_PIPES; ++i) {
         o_qs0[i] = take(slots * 4);
         o_qs1[i] = take(slots * 4);
-        o_qr0[i] = take(slots * 32);
-        o_qr1[i] = take(slots * 32);
-        o_h[i] = take(slots * 16);
+        o_qr0[i] = take(2 * slots * 32);
+        o_qr1[i] = take(2 * slots * 32);
+        o_h[i] = take(2 * slots * 16);
         o_cnt[i] = take(256);
         o_sp[i] = take(spill_threads * 8 * (RT_STACK_DEPTH - WF_LDS_STACK));
     }
@@ -1004,6 +1093,9 @@ int ensure(Workspace &w, size_t slots, int grid, int npipes)
         st.snorm = (Vec3D *)(b + o_n);
         st.rp = (Vec3D *)(b + o_rp);
         st.light = (int *)(b + o_li);
+        st.ro = (Vec3D *)(b + o_ro);
+        st.e_sh = (uint32_t *)(b + o_es);
+        st.e_ext = (uint32_t *)(b + o_ee);
         st.q_slot[0] = (uint32_t *)(b + o_qs0[i]);
         st.q_slot[1] = (uint32_t *)(b + o_qs1[i]);
         st.q_ray[0] = (RtF4 *)(b + o_qr0[i]);
@@ -1208,7 +1300,8 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
         } else {
             for (int it = 0;; ++it) {
                 const int q = it & 1;
-                if (hipMemsetAsync(st.counts + (q ^ 1), 0, 4, s) != hipSuccess) return -1;
+                if (hipMemsetAsync(st.counts + (q ^ 1), 0, 4, s) != hipSuccess) return -1;     // next ray queue
+                if (hipMemsetAsync(st.counts + 6 + (q ^ 1), 0, 4, s) != hipSuccess) return -1; // next path list
                 if (hipMemsetAsync(st.counts + 2 + q, 0, 4, s) != hipSuccess) return -1; // fetch cursor
                 if (!mark(4)) return -1;
                 if (trace_kind == 1) {
@@ -1232,10 +1325,10 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
                 else hipLaunchKernelGGL(wf_shade<false>, dim3(tgrid), dim3(WF_TBLOCK), 0, s, sc, fr, cam, st, q);
                 if (hipGetLastError() != hipSuccess) return -1;
                 if (!mark(2)) return -1;
-                if (hipMemcpyAsync(pp.host_count, st.counts + (q ^ 1), 4, hipMemcpyDeviceToHost, s) != hipSuccess)
+                if (hipMemcpyAsync(pp.host_count, st.counts, 32, hipMemcpyDeviceToHost, s) != hipSuccess)
                     return -1;
                 if (hipStreamSynchronize(s) != hipSuccess) return -1;
-                const uint32_t live = *pp.host_count;
+                const uint32_t live = pp.host_count[6 + (q ^ 1)]; // paths with rays in the next queue
                 P.iterations = it + 1;
                 if (prof) {
                     P.trace_ms += elapsed_ms(pp.ev[4], pp.ev[5]);
