@@ -3,8 +3,16 @@
 Workload (BASELINE.json configs[2]): the README-like 2M-triangle synthetic
 room ("room2m": room + 1,997,568-triangle displaced gold mesh + two glass
 spheres + emissive quad), 1920x1080, adaptive sampling off.  One step = one
-rt_render call of `--passes` passes (spp) over the full frame (default 64:
-16 steps are the config's 1024 spp), inputs resident in HBM.
+`--passes` passes (spp) over the full frame (default 64: 16 steps are the
+config's 1024 spp), inputs resident in HBM.  The renderer is called with up
+to `--steps-per-call` steps at once (default 4: rt_render calls of 256
+passes; RtOptions batches passes per call, SURVEY §3 "passes batched in one
+launch").  Each pixel's passes are a serial chain (its RNG state runs from
+one pass into the next), so a call ends with a tail in which only the
+pixels with the longest chains are still running; longer calls amortise it
+(room2m 1080p: 36.7 / 38.1 / 39.4 Msamples/s at 64 / 128 / 256 passes per
+call, profiles/r02/passes_per_call.json).  The image is bit-identical for any
+split of the passes into calls (tests/test_gpu_parity.py).
 
 Multi-GPU (`--gpus N`): one process per GPU.  Without WORLD_SIZE in the
 environment this script starts the N ranks itself (children with RANK /
@@ -74,7 +82,9 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--passes", type=int, default=64, help="spp per step (passes per rt_render call)")
+    ap.add_argument("--passes", type=int, default=64, help="spp per step")
+    ap.add_argument("--steps-per-call", type=int, default=4,
+                    help="steps rendered by one rt_render call (passes per call = passes x this)")
     ap.add_argument("--scene", default="room2m")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
@@ -413,16 +423,21 @@ def main(argv=None):
     kernel = rt.KERNEL_WAVEFRONT if args.kernel == "wavefront" else rt.KERNEL_MEGA
     wavefront = kernel == rt.KERNEL_WAVEFRONT
     render_kw = dict(adaptive=args.adaptive, min_samples=args.min_samples, max_depth=args.max_depth, kernel=kernel)
-    opt = rt.options(W, H, P, profile=wavefront, **render_kw)
+    spc = max(1, args.steps_per_call)
     profiles = []
 
-    def step(i):
-        rt.render(dscene, gb, host.camera, 0 if i == 0 else 1, opt)
-        if wavefront:
-            profiles.append(rt.last_profile())
+    def steps(first, count):
+        """render steps [first, first + count) in calls of up to spc steps"""
+        done = 0
+        while done < count:
+            k = min(spc, count - done)
+            rt.render(dscene, gb, host.camera, 0 if first + done == 0 else 1,
+                      rt.options(W, H, P * k, profile=wavefront, **render_kw))
+            if wavefront:
+                profiles.append(dict(rt.last_profile(), passes=P * k))
+            done += k
 
-    for i in range(args.warmup):
-        step(i)
+    steps(0, args.warmup)
     profiles.clear()
     rt.check(rt.lib().rt_synchronize())
     cnt_before = int(gb.download()[2].sum(dtype=np.int64))  # accumulated samples (adaptive: actual)
@@ -438,8 +453,7 @@ def main(argv=None):
     if dist:
         dist.barrier()
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(args.warmup + k)
+    steps(args.warmup, args.steps)
     if comm:  # ONE RCCL reduce over xGMI of fb/sq/count into rank 0 (rt_reduce_shards)
         comm.reduce(gb.g, W, H, root=0, stream=None)
     if rank == 0:
@@ -487,6 +501,7 @@ def main(argv=None):
             "finish_ms_per_call": round(float(np.mean([p["finish_ms"] for p in profiles])), 3),
             "call_ms": round(float(np.mean([p["call_ms"] for p in profiles])), 3),
             "iterations_per_call": round(float(np.mean([p["iterations"] for p in profiles])), 1),
+            "passes_per_call": round(float(np.mean([p["passes"] for p in profiles])), 1),
         }
     else:
         kernel_detail = {"kernel": "rt_path_kernel<false,20>"}
@@ -546,7 +561,7 @@ def main(argv=None):
                          f"{'on (min ' + str(args.min_samples) + ')' if args.adaptive else 'off'}, "
                          f"max depth {args.max_depth or 'unbounded'}"),
             "adaptive": args.adaptive, "max_depth": args.max_depth,
-            "scene": args.scene, "width": W, "height": H, "spp_per_step": P,
+            "scene": args.scene, "width": W, "height": H, "spp_per_step": P, "steps_per_call": spc,
             "triangles": info["triangles"], "kd_nodes": info["nodes"], "kd_indices": info["indices"],
             "parallelism": parallelism,
         },

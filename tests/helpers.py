@@ -41,8 +41,9 @@ class GpuRun:
                num_shards=1, wf_pipelines=0, wf_long_depth=0):
         g = rt.GBuffer(W, H, seed_skip)
         cnt = rt.DeviceCounters() if count else None
-        for c in range(calls):
-            opt = rt.options(W, H, passes, adaptive, min_samples, tolerance, max_depth,
+        per_call = list(passes) if isinstance(passes, (list, tuple)) else [passes] * calls  # passes of each call
+        for c, pc in enumerate(per_call):
+            opt = rt.options(W, H, pc, adaptive, min_samples, tolerance, max_depth,
                              counters=cnt.p if cnt else None, kernel=kernel, wf_tail=wf_tail,
                              wf_finish_waves=wf_finish_waves, wf_wide=wf_wide, shard_id=shard_id,
                              num_shards=num_shards, wf_pipelines=wf_pipelines, wf_long_depth=wf_long_depth)
@@ -62,8 +63,9 @@ def oracle_render(path, W, H, passes, calls=1, adaptive=False, min_samples=100, 
     rng = oracle.mt19937(n, seed_skip)
     cam = sc.camera if camera is None else camera
     total = {}
-    for c in range(calls):
-        k = sc.render(cam, fb, sq, cnt, rng, W, H, passes, sample_count_arg=0 if c == 0 else 1, pixels=pixels,
+    per_call = list(passes) if isinstance(passes, (list, tuple)) else [passes] * calls  # passes of each call
+    for c, pc in enumerate(per_call):
+        k = sc.render(cam, fb, sq, cnt, rng, W, H, pc, sample_count_arg=0 if c == 0 else 1, pixels=pixels,
                       adaptive=adaptive, min_samples=min_samples, tolerance=tolerance, max_depth=max_depth)
         for key, v in k.items():
             total[key] = max(total.get(key, 0), v) if key == "maxdepth" else total.get(key, 0) + v

@@ -270,19 +270,21 @@ def test_room2m_every_pixel_bench_options():
 
 @pytest.mark.timeout(240)
 def test_room2m_bench_configuration_sparse_pixels():
-    """bench.py's timed configuration exactly: room2m at 1920x1080, two
-    rt_render calls of 64 passes (sample_count 0 then 1), wavefront kernel with
-    its defaults (3 pipelines, long-path hand-off at depth 64, wide tails,
-    cooperative finisher), no counters (the bench's kernels).  Every 1031st
-    pixel re-rendered by the oracle over the same 128 spp.  A counted call of
-    the same options must not fire the 65,536-bounce watchdog."""
+    """bench.py's configuration exactly: room2m at 1920x1080, its warm-up
+    call of 64 passes (sample_count 0) then a timed call of 4 steps = 256
+    passes (sample_count 1), wavefront kernel with its defaults (3 pipelines,
+    long-path hand-off at depth 64, wide tails, cooperative finisher), no
+    counters (the bench's kernels).  Every 1031st pixel re-rendered by the
+    oracle over the same 320 spp.  A counted call of the same options must not
+    fire the 65,536-bounce watchdog."""
     run = helpers.GpuRun("room2m")
     W, H, P = 1920, 1080, 64
-    gpu, _, g = run.render(W, H, P, calls=2, kernel=rt.KERNEL_WAVEFRONT)
+    calls = [P, 4 * P]
+    gpu, _, g = run.render(W, H, calls, kernel=rt.KERNEL_WAVEFRONT)
     pixels = np.arange(0, W * H, 1031, dtype=np.int32)
-    ref, rcnt = helpers.oracle_render(run.path, W, H, P, calls=2, pixels=pixels)
+    ref, rcnt = helpers.oracle_render(run.path, W, H, calls, pixels=pixels)
     helpers.assert_bitwise(gpu, ref, pixels=pixels, what="room2m bench configuration")
-    assert np.all(gpu[2] == 2 * P)
+    assert np.all(gpu[2] == sum(calls))
     assert helpers.rel_linf(gpu[0][pixels], gpu[2][pixels], ref[0][pixels], ref[2][pixels]) < 1e-4
     assert rcnt["watchdog"] == 0
     cnt = rt.DeviceCounters()
