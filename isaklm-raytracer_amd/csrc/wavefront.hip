@@ -39,6 +39,14 @@ using namespace rtk;
 #ifndef WF_SHADE_PRIO
 #define WF_SHADE_PRIO 3
 #endif
+// wf_shade runs in the slots its pipeline's trace launch just left, beside
+// the other pipelines' trace waves (80 VGPRs each): at the same footprint
+// (6 waves/SIMD, the rest of its ~126 VGPRs spilled) its waves fit those
+// holes.  Measured (room2m 1080p, 256 passes/call, 3 rounds): 13.60 s at 126
+// VGPRs, 13.58 at 96, 13.21 at 80, 13.21 at 72, 13.31 at 64
+#ifndef WF_SHADE_WAVES
+#define WF_SHADE_WAVES 6
+#endif
 #ifndef WF_TAIL_PRIO
 #define WF_TAIL_PRIO 2
 #endif
@@ -490,6 +498,13 @@ __global__ void __launch_bounds__(WF_TBLOCK, WF_TRACE_WAVES) wf_trace_coop(RtDev
 
 namespace {
 
+// a ? x : y of two Vec3D values (a conditional of two lvalues selects their
+// ADDRESSES, which keeps the path state in scratch memory)
+__device__ __forceinline__ Vec3D pick(bool a, Vec3D x, Vec3D y)
+{
+    return rt_v3(a ? x.x : y.x, a ? x.y : y.y, a ? x.z : y.z);
+}
+
 // the state of one pixel's path between two ray queries
 struct PathRegs {
     uint32_t slot;
@@ -674,7 +689,7 @@ __device__ __forceinline__ bool shade_step(const RtDevScene &sc, const RtDevFram
 } // namespace
 
 template <bool COUNT>
-__global__ void __launch_bounds__(WF_TBLOCK) wf_shade(RtDevScene sc, RtDevFrame fr, RtDevCamera cam, WfState st, int q)
+__global__ void __launch_bounds__(WF_TBLOCK, WF_SHADE_WAVES) wf_shade(RtDevScene sc, RtDevFrame fr, RtDevCamera cam, WfState st, int q)
 {
     if (WF_SHADE_PRIO > 0) __builtin_amdgcn_s_setprio(WF_SHADE_PRIO); // ahead of co-resident trace waves
     Cnt c;
@@ -712,14 +727,14 @@ __global__ void __launch_bounds__(WF_TBLOCK) wf_shade(RtDevScene sc, RtDevFrame 
             store_regs(st, fr, p);
             if (want) { // the pending ray(s): extension = (ro, cont)
                 st.ro[slot] = p.ro;
-                st.cont[slot] = p.shadow ? p.cont : p.rd;
+                st.cont[slot] = pick(p.shadow, p.cont, p.rd);
             }
         }
         const bool to_long = want && st.long_depth > 0 && p.depth > st.long_depth;
         const bool go = want && !to_long;
         const bool sh = go && p.shadow, ex = go && (!p.shadow || p.ext_live);
         const uint32_t es = enqueue_ray(st, qn, sh, p.ro, p.rd);
-        const uint32_t ee = enqueue_ray(st, qn, ex, p.ro, p.shadow ? p.cont : p.rd);
+        const uint32_t ee = enqueue_ray(st, qn, ex, p.ro, pick(p.shadow, p.cont, p.rd));
         if (sh) st.e_sh[p.slot] = es;
         if (ex) st.e_ext[p.slot] = ee;
         enqueue_path(st, qn, go, p.slot);
