@@ -47,6 +47,16 @@ using namespace rtk;
 #ifndef WF_SHADE_WAVES
 #define WF_SHADE_WAVES 6
 #endif
+// wf_long, too, runs beside the pipelines' trace waves: at their footprint
+// (80 VGPRs, ~85 spilled) its waves fit the slots a trace block leaves.
+// Measured (as WF_SHADE_WAVES): 13.16 s at 126 VGPRs, 13.16 at 128 (4
+// waves), 12.87 at 80, 12.86 at 72, 12.92 at 64
+#ifndef WF_LONG_WAVES
+#define WF_LONG_WAVES 6
+#endif
+#ifndef WF_FIN_OCC
+#define WF_FIN_OCC 1 // wf_finish_coop occupancy floor (1: the compiler's choice, 2 waves/SIMD)
+#endif
 #ifndef WF_TAIL_PRIO
 #define WF_TAIL_PRIO 2
 #endif
@@ -787,7 +797,7 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_finish(RtDevScene sc, RtDevFrame 
 // counts[4]).  With ppw = 1 a lone long glass path gets its leaves tested 64
 // entries at a time instead of one.
 template <bool COUNT>
-__global__ void __launch_bounds__(WF_BLOCK) wf_finish_coop(RtDevScene sc, RtDevFrame fr, RtDevCamera cam, WfState st,
+__global__ void __launch_bounds__(WF_BLOCK, WF_FIN_OCC) wf_finish_coop(RtDevScene sc, RtDevFrame fr, RtDevCamera cam, WfState st,
                                                            int q, int ppw, int cap, int postpone, int wide)
 {
     __shared__ uint32_t s_node[WF_LDS_STACK * WF_BLOCK];
@@ -913,7 +923,7 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_finish_coop(RtDevScene sc, RtDevF
 // hardware queue.  The final slice (every producer done, all entries
 // published) drains what is left.
 template <bool COUNT>
-__global__ void __launch_bounds__(WF_BLOCK) wf_long(RtDevScene sc, RtDevFrame fr, RtDevCamera cam, WfState st,
+__global__ void __launch_bounds__(WF_BLOCK, WF_LONG_WAVES) wf_long(RtDevScene sc, RtDevFrame fr, RtDevCamera cam, WfState st,
                                                     int final_slice)
 {
     __shared__ WideItem s_wide[(WF_BLOCK / 64) * WIDE_CAP];
