@@ -49,6 +49,7 @@ def main():
             t = time.perf_counter()
             rt.render(run.dev, g, run.camera, 0, opt)
             times[v].append(time.perf_counter() - t)
+            print(f"round {r} {v} {times[v][-1]:.3f} s", file=sys.stderr, flush=True)  # progress (gpurun: silence kills)
             if v.split(":")[0] != "0":
                 profs[v].append(rt.last_profile())
     out = {}
