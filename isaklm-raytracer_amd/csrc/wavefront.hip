@@ -1186,6 +1186,12 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
     // 33.1 Msamples/s on room2m 1080p (tools/gpu_sweep.sh, profiles/r02).
     const int grid = grid_env >= 64 && grid_env <= 16384 ? grid_env : 512;
     const int tgrid = grid * (WF_BLOCK / WF_TBLOCK); // the same waves in WF_TBLOCK-thread blocks
+    // wf_shade: half the trace grid (~2 paths per lane per launch).  Measured
+    // per 256-pass room2m call (2 rounds each): 64 / 128 / 256 / 384 / 512 /
+    // 1,024 / 2,048 blocks: 13.27 / 12.82 / 12.78 / 12.78 / 12.87 / 13.01 /
+    // 13.21 s.  RT_WF_SHADE_GRID overrides (experiments)
+    static const int sgrid_env = getenv("RT_WF_SHADE_GRID") ? atoi(getenv("RT_WF_SHADE_GRID")) : 0;
+    const int sgrid = sgrid_env >= 16 && sgrid_env <= 16384 ? sgrid_env : (tgrid / 2 > 16 ? tgrid / 2 : 16);
     const size_t slots = (size_t)fr.width * fr.height;
     const bool count = fr.counters != nullptr;
     const bool prof = profile != 0;
@@ -1346,8 +1352,8 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
                     else hipLaunchKernelGGL(wf_trace<false>, dim3(grid), dim3(WF_BLOCK), 0, s, sc, st, q, fr.counters);
                 }
                 if (!mark(5)) return -1;
-                if (count) hipLaunchKernelGGL(wf_shade<true>, dim3(tgrid), dim3(WF_TBLOCK), 0, s, sc, fr, cam, st, q);
-                else hipLaunchKernelGGL(wf_shade<false>, dim3(tgrid), dim3(WF_TBLOCK), 0, s, sc, fr, cam, st, q);
+                if (count) hipLaunchKernelGGL(wf_shade<true>, dim3(sgrid), dim3(WF_TBLOCK), 0, s, sc, fr, cam, st, q);
+                else hipLaunchKernelGGL(wf_shade<false>, dim3(sgrid), dim3(WF_TBLOCK), 0, s, sc, fr, cam, st, q);
                 if (hipGetLastError() != hipSuccess) return -1;
                 if (!mark(2)) return -1;
                 if (hipMemcpyAsync(pp.host_count, st.counts, 32, hipMemcpyDeviceToHost, s) != hipSuccess)
