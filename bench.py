@@ -77,6 +77,18 @@ def algorithmic_bytes(c):
             20 * c["skip"])
 
 
+def call_plan(first, count, per_call):
+    """(first step, steps) of each rt_render call rendering steps
+    [first, first + count) in calls of up to per_call steps; the call that
+    renders step 0 resets the G-buffer (sample_count 0)"""
+    plan, done = [], 0
+    while done < count:
+        k = min(per_call, count - done)
+        plan.append((first + done, k))
+        done += k
+    return plan
+
+
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -428,14 +440,11 @@ def main(argv=None):
 
     def steps(first, count):
         """render steps [first, first + count) in calls of up to spc steps"""
-        done = 0
-        while done < count:
-            k = min(spc, count - done)
-            rt.render(dscene, gb, host.camera, 0 if first + done == 0 else 1,
+        for start, k in call_plan(first, count, spc):
+            rt.render(dscene, gb, host.camera, 0 if start == 0 else 1,
                       rt.options(W, H, P * k, profile=wavefront, **render_kw))
             if wavefront:
                 profiles.append(dict(rt.last_profile(), passes=P * k))
-            done += k
 
     steps(0, args.warmup)
     profiles.clear()

@@ -80,3 +80,17 @@ def test_roofline_from_counters(tmp_path):
 
 def test_metric_names_the_rendered_frame():
     assert "1920×1080" in bench.METRIC
+
+
+def test_call_plan_groups_steps_into_calls():
+    # the driver's --steps 20 --warmup 5 with the default 4 steps per call
+    assert bench.call_plan(0, 5, 4) == [(0, 4), (4, 1)]
+    assert bench.call_plan(5, 20, 4) == [(5, 4), (9, 4), (13, 4), (17, 4), (21, 4)]
+    # every step rendered exactly once, only the first call starts at step 0
+    for first, count, per in ((0, 1, 4), (1, 4, 4), (0, 7, 3), (3, 0, 4), (2, 9, 1)):
+        plan = bench.call_plan(first, count, per)
+        covered = [s for start, k in plan for s in range(start, start + k)]
+        assert covered == list(range(first, first + count))
+        assert all(1 <= k <= per for _, k in plan)
+    args = bench.parse_args([])
+    assert args.passes * args.steps_per_call == 256
