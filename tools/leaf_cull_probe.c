@@ -74,8 +74,11 @@ int main(int argc, char **argv)
                 b[3 + c] = fmaxf(b[3 + c], tbox[t][3 + c]);
             }
         }
+        float m = 1.0f;
+        for (int c = 0; c < 6; ++c) m = fmaxf(m, fabsf(b[c]));
         for (int c = 0; c < 3; ++c) {
-            const float g = margin * (b[3 + c] - b[c]) + 1e-4f;
+            /* margin < 0: the product's growth (scene_prepare.cpp), 1e-4 of the largest coordinate magnitude */
+            const float g = margin < 0 ? 1e-4f * m : margin * (b[3 + c] - b[c]) + 1e-4f;
             lbox[i][c] = b[c] - g;
             lbox[i][3 + c] = b[3 + c] + g;
         }
@@ -121,7 +124,19 @@ int main(int argc, char **argv)
                 if (a > t0) t0 = a;
                 if (b < t1) t1 = b;
             }
-            const int miss = t0 > t1;
+            int miss = t0 > t1;
+            if (margin < 0) { /* the product's test (coop_trace.h leaf_box_maybe), in float */
+                const float y[3] = {1.0f / d[0], 1.0f / d[1], 1.0f / d[2]};
+                int guarded = 0;
+                for (int c = 0; c < 3; ++c) guarded |= !(fabsf(d[c]) >= 0x1p-60f && fabsf(d[c]) <= 0x1p40f);
+                float lo = 0.0f, hi = exit_;
+                for (int c = 0; c < 3; ++c) {
+                    const float a = (lbox[node][c] - o[c]) * y[c], b = (lbox[node][3 + c] - o[c]) * y[c];
+                    lo = fmaxf(lo, fminf(a, b));
+                    hi = fminf(hi, fmaxf(a, b));
+                }
+                miss = !guarded && lo > hi + 0x1p-16f * (fabsf(lo) + fabsf(hi));
+            }
             /* mailbox probe: triangles of this leaf already tested earlier along this ray */
             for (int k = 0; k < L->b; ++k) {
                 const int tt = idx[L->a + k];

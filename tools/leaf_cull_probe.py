@@ -1,7 +1,8 @@
 """Driver for tools/leaf_cull_probe.c: dumps a scene's reference-layout KD
 tree / indices / triangles and a ray list (rays from the camera position in
 random directions, plus diffuse-like bounce rays from their hit points), then
-runs the probe.  usage: python tools/leaf_cull_probe.py SCENE [MARGIN] [N]"""
+runs the probe.  usage: python tools/leaf_cull_probe.py SCENE [MARGIN] [N]
+(MARGIN < 0: the product's leaf-box growth and float slab test, coop_trace.h leaf_box_maybe)"""
 import os
 import subprocess
 import sys
@@ -41,7 +42,7 @@ def main():
         for pth, data in zip(paths, (nodes, idx.astype(np.int32).tobytes(), tris, rays.tobytes())):
             open(pth, "wb").write(data)
         exe = os.path.join(t, "probe")
-        subprocess.run(["gcc", "-O2", "-fopenmp", os.path.join(ROOT, "tools", "leaf_cull_probe.c"), "-o", exe, "-lm"],
+        subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-fopenmp", os.path.join(ROOT, "tools", "leaf_cull_probe.c"), "-o", exe, "-lm"],
                        check=True)
         print(subprocess.run([exe, *paths, margin], check=True, capture_output=True, text=True).stdout.strip())
 
