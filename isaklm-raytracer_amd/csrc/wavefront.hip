@@ -42,8 +42,9 @@ using namespace rtk;
 // wf_shade runs in the slots its pipeline's trace launch just left, beside
 // the other pipelines' trace waves (80 VGPRs each): at the same footprint
 // (6 waves/SIMD, the rest of its ~126 VGPRs spilled) its waves fit those
-// holes.  Measured (room2m 1080p, 256 passes/call, 3 rounds): 13.60 s at 126
-// VGPRs, 13.58 at 96, 13.21 at 80, 13.21 at 72, 13.31 at 64
+// holes.  Measured (room2m 1080p, 256 passes/call, 3 rounds, s per call):
+// 13.83 at 126 VGPRs, 13.58 at 96, 13.21 at 80, 13.21 at 72, 13.31 at 64
+// (and 13.60 for the earlier 102-VGPR build that kept its path state in scratch)
 #ifndef WF_SHADE_WAVES
 #define WF_SHADE_WAVES 6
 #endif
@@ -55,7 +56,7 @@ using namespace rtk;
 #define WF_LONG_WAVES 6
 #endif
 #ifndef WF_FIN_OCC
-#define WF_FIN_OCC 1 // wf_finish_coop occupancy floor (1: the compiler's choice, 2 waves/SIMD)
+#define WF_FIN_OCC 1 // wf_finish_coop occupancy floor (1: the compiler's choice, 2 waves/SIMD; 3: no change)
 #endif
 #ifndef WF_TAIL_PRIO
 #define WF_TAIL_PRIO 2
