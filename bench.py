@@ -35,9 +35,14 @@ bytes per sample x the timed samples/s: chip-wide, call-level, <= peak by
 construction of the counters.  The SURVEY §8d algorithmic bytes (which the
 caches serve, mostly) are reported separately as `algorithmic_GBps`.
 
-cpu_baseline: the C oracle (OpenMP) on the host cores of the GPU box on a
-bounded pixel sample of the same frame, beside the reference's own
-single-core rate measured in the survey container.
+cpu_baseline: the C oracle (OpenMP) on the host cores of the GPU box on
+BASELINE.md's budget (the full frame x 1 spp; the whole job for the Cornell
+config), beside the reference's own single-core rate measured in the survey
+container.
+
+deviations: the always-on statistics of the timed kernels over the whole
+timed region (rt_deviation_stats): watchdog / depth-limit cuts, longest path,
+histogram of paths deeper than 64 bounces.
 """
 import argparse
 import csv
@@ -89,6 +94,11 @@ def call_plan(first, count, per_call):
     return plan
 
 
+def call_steps(args):
+    """steps per timed rt_render call (the first, largest call of the plan)"""
+    return max(1, min(args.steps_per_call, args.steps))
+
+
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -100,7 +110,8 @@ def parse_args(argv=None):
     ap.add_argument("--scene", default="room2m")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-seconds", type=float, default=240.0,
+                    help="cap on the CPU baseline (full frame x 1 spp unless predicted above this)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 counter passes (roofline traffic)")
     ap.add_argument("--pmc-save", default=None, help="directory to keep the parsed counter summaries in")
@@ -195,7 +206,9 @@ def _window_sums(cc_csv, trace_csv):
 def measure_pmc(args, save_dir):
     """rocprofv3 counter passes over one render call (child processes, run
     before this process initialises the GPU).  Returns a dict or an error."""
-    child = ["--pmc-child", "1", "--passes", str(args.passes), "--scene", args.scene, "--width", str(args.width),
+    # the profiled call has the timed calls' shape: passes x steps-per-call
+    child = ["--pmc-child", "1", "--passes", str(args.passes * call_steps(args)), "--scene", args.scene,
+             "--width", str(args.width),
              "--height", str(args.height), "--scene-dir", args.scene_dir, "--kernel", args.kernel,
              "--max-depth", str(args.max_depth), "--min-samples", str(args.min_samples)]
     if args.adaptive:
@@ -228,13 +241,12 @@ def measure_pmc(args, save_dir):
     return res
 
 
-def pmc_child(args):
-    """The profiled render: warm-up call, marker, ONE call of the bench's
-    passes, marker.  Prints the call's sample count."""
-    import rt
-
+def pmc_child(args, rt):
+    """The profiled render: warm-up call, marker, ONE call of the timed calls'
+    passes (the parent passes passes x steps-per-call), marker.  Prints the
+    call's sample count."""
     rt.check(rt.lib().rt_set_device(0))
-    scene_file = ensure_scene(args)
+    scene_file = ensure_scene(args, rt)
     host = rt.HostScene(scene_file)
     dscene = rt.DeviceScene(host)
     W, H = args.width, args.height
@@ -308,9 +320,7 @@ def roofline_from_pmc(pmc, samples_per_s):
 
 
 # ------------------------------------------------------------------ helpers
-def ensure_scene(args):
-    import rt
-
+def ensure_scene(args, rt):
     scene_dir = os.path.join(args.scene_dir, args.scene)
     scene_file = os.path.join(scene_dir, "scene.txt")
     if not os.path.exists(scene_file):
@@ -335,10 +345,13 @@ def cpu_info():
     return model, os.cpu_count() or 1, usable
 
 
-def cpu_baseline(scene_path, W, H, seconds):
-    """The C oracle (OpenMP) on a bounded sample of the same frame.  Threads:
-    the CPU share this job was given (OMP_NUM_THREADS on the GPU box, which
-    sets it to the box's share), else every usable core."""
+def cpu_baseline(scene_path, W, H, cap_seconds, passes=1):
+    """The C oracle (OpenMP) on BASELINE.md's CPU budget: the full frame x
+    `passes` spp (1 for configs 2-5; the whole job for the Cornell config).
+    Threads: the CPU share this job was given (OMP_NUM_THREADS on the GPU box,
+    which sets it to the box's share), else every usable core.  If a probe
+    predicts more than cap_seconds, a bounded pixel sample is timed instead
+    (and the line says so)."""
     import oracle
 
     model, nproc, usable = cpu_info()
@@ -347,36 +360,47 @@ def cpu_baseline(scene_path, W, H, seconds):
     sc = oracle.OracleScene(scene_path)
     n = W * H
 
-    def run(pixels):
+    def run(pixels, p):
         fb = np.zeros(n * 3, np.float32)
         sq = np.zeros(n, np.float32)
         cnt = np.zeros(n, np.int32)
         rng = oracle.mt19937(n)
         t = time.perf_counter()
-        sc.render(sc.camera, fb, sq, cnt, rng, W, H, 1, sample_count_arg=0, pixels=pixels, adaptive=False,
+        sc.render(sc.camera, fb, sq, cnt, rng, W, H, p, sample_count_arg=0, pixels=pixels, adaptive=False,
                   threads=threads)
         return time.perf_counter() - t
 
-    probe = np.arange(0, n, max(1, n // 2048), dtype=np.int32)
-    dt = run(probe)
-    rate = len(probe) / max(dt, 1e-6)
-    count = int(min(n, max(len(probe), rate * seconds)))
-    pixels = np.linspace(0, n - 1, count).astype(np.int32)
-    dt = run(pixels)
+    probe = np.arange(0, n, max(1, n // 4096), dtype=np.int32)
+    dt = run(probe, 1)
+    predicted = dt * n * passes / len(probe)
+    if predicted <= cap_seconds:
+        dt = run(None, passes)
+        count, what = n * passes, f"the full {W}x{H} frame x {passes} spp"
+    else:
+        count = int(max(len(probe), len(probe) * cap_seconds / max(dt, 1e-6)))
+        count = min(n, count)
+        pixels = np.linspace(0, n - 1, count).astype(np.int32)
+        dt = run(pixels, 1)
+        what = (f"{count} pixels spread over the {W}x{H} frame x 1 spp (the full-frame budget was predicted at "
+                f"{predicted:.0f} s > --cpu-seconds {cap_seconds:.0f})")
     value = count / dt / 1e6
     return {"value": round(value, 6), "unit": "Msamples/s", "cores": threads, "kind": "port",
             "per_core": round(value / threads, 6), "cpu_model": model, "nproc": nproc, "usable_cpus": usable,
-            "sample": f"{count} pixels spread over the {W}x{H} frame x 1 spp ({dt:.1f} s, OpenMP {threads} threads "
-                      f"= the job's CPU share, oracle/rt_oracle.c)",
+            "sample": f"{what} ({dt:.1f} s, OpenMP {threads} threads = the job's CPU share, oracle/rt_oracle.c)",
             "reference_single_core": REF_SINGLE_CORE}
 
 
 # ------------------------------------------------------------------ main
-def main(argv=None):
+def main(argv=None, binding=None):
+    """`binding`: the ctypes binding module (default: isaklm-raytracer_amd/rt.py,
+    the HIP library).  Tests pass a CPU stand-in to exercise the multi-rank
+    accounting without a GPU (tests/test_bench_ranks.py)."""
     argv = list(sys.argv[1:] if argv is None else argv)
     args = parse_args(argv)
     if args.pmc_child:
-        return pmc_child(args)
+        import rt
+
+        return pmc_child(args, rt)
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         return launch_ranks(args.gpus, argv)
     world = int(os.environ.get("WORLD_SIZE", 1))
@@ -400,11 +424,16 @@ def main(argv=None):
     # counter passes first: the children must own the GPU alone, and this
     # process must not have initialised it yet
     pmc = None
-    if rank == 0 and world == 1 and not args.no_pmc:
-        ensure_scene(args)  # host-only scene generation, once, outside the profiled children
+    if rank == 0 and world == 1 and not args.no_pmc and binding is None:
+        import rt as rt_host_only
+
+        ensure_scene(args, rt_host_only)  # host-only scene generation, once, outside the profiled children
         pmc = measure_pmc(args, args.pmc_save)
 
-    import rt
+    if binding is None:
+        import rt
+    else:
+        rt = binding
 
     ndev = ctypes.c_int(0)
     rt.check(rt.lib().rt_device_count(ctypes.byref(ndev)))
@@ -419,10 +448,10 @@ def main(argv=None):
         comm = rt.Comm(world, rank, uid[0])
 
     if local == 0:
-        ensure_scene(args)
+        ensure_scene(args, rt)
     if dist:
         dist.barrier()
-    scene_file = ensure_scene(args)
+    scene_file = ensure_scene(args, rt)
     t = time.perf_counter()
     host = rt.HostScene(scene_file)
     dscene = rt.DeviceScene(host)
@@ -459,6 +488,7 @@ def main(argv=None):
     rgba = ctypes.c_void_p()
     rt.check(rt.lib().rt_device_alloc(ctypes.byref(rgba), n * 4))
     rt.check(rt.lib().rt_synchronize())
+    rt.deviation_stats(reset=True)  # always-on deviation statistics: the timed region only
     if dist:
         dist.barrier()
     t0 = time.perf_counter()
@@ -477,6 +507,18 @@ def main(argv=None):
         e = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
+    dev = rt.deviation_stats(reset=False)
+    if dist:  # every rank's statistics (sums; max of the longest path)
+        import torch
+
+        dv = torch.tensor([dev["watchdog_paths"], dev["cut_paths"], dev["deep_paths"]] + dev["deep_hist"],
+                          dtype=torch.int64)
+        dist.all_reduce(dv)
+        mx = torch.tensor([dev["max_deep_depth"]], dtype=torch.int64)
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        v = [int(x) for x in dv.tolist()]
+        dev = {"watchdog_paths": v[0], "cut_paths": v[1], "deep_paths": v[2], "deep_hist": v[3:],
+               "max_deep_depth": int(mx.item())}
     total_samples = world * n * P * args.steps
     value = total_samples / elapsed / 1e6
     acc = gb.download()[2]
@@ -528,7 +570,8 @@ def main(argv=None):
         achieved, detail = roofline_from_pmc(pmc, samples_per_s)
         roof.update(achieved=round(achieved, 1), frac=round(achieved / HBM_PEAK_GBPS, 4),
                     traffic=round(detail["hbm_bytes_per_sample"] * n * P), **detail)
-        roof["traffic_unit"] = f"HBM bytes per call of {P} passes (whole frame, every kernel)"
+        roof["traffic_unit"] = (f"HBM bytes per step of {P} passes (whole frame, every kernel), from one profiled "
+                                f"call of {P * call_steps(args)} passes = the timed calls' shape")
         dk = detail["per_kernel"].get(detail["dominant_kernel"] or "", {})
         if wavefront and dk.get("dispatches") and "wf_trace_coop" in (detail["dominant_kernel"] or ""):
             # the dominant kernel alone: its counter bytes per launch / its live
@@ -576,19 +619,28 @@ def main(argv=None):
         },
         "roofline": roof,
         "per_sample": {k: round(c[k] / max(c["sample"], 1), 3) for k in ("ray", "node", "tri", "hit", "nee")},
-        "deviations": {"watchdog_paths": c["watchdog"], "max_path_depth": c["maxdepth"],
-                       "deep_pushes": c["deep_push"],
-                       "note": "counted over one extra call of the same options: paths cut by the 65,536-bounce "
-                               "watchdog (SURVEY H8; the reference loops unbounded), the longest path in bounces, "
-                               "traversal pushes at stack index >= 19 (past the reference's 19-entry arrays, "
-                               "SURVEY H16)"},
+        "deviations": {
+            "scope": f"timed region: every path of the {args.steps} timed steps on all ranks "
+                     "(always-on statistics of the non-counting bench kernels, rt_deviation_stats)",
+            "watchdog_paths": dev["watchdog_paths"], "cut_paths": dev["cut_paths"],
+            "max_path_depth": dev["max_deep_depth"] if dev["deep_paths"] else c["maxdepth"],
+            "deep_paths": dev["deep_paths"],
+            "deep_path_hist": {f"{64 << k}-{(64 << (k + 1)) - 1}": h for k, h in enumerate(dev["deep_hist"]) if h},
+            "watchdog_limit": 16777215,
+            "deep_pushes": c["deep_push"], "deep_pushes_scope": "one extra counted call of the same options",
+            "note": "paths cut by the 2^24-1-bounce watchdog (SURVEY H8; the reference loops unbounded), paths cut "
+                    "by max_depth, the longest path in bounces and the histogram of paths that ended at depth >= 64; "
+                    "deep_pushes = traversal pushes at stack index >= 19 (past the reference's 19-entry arrays, "
+                    "SURVEY H16)"},
         "samples_check": {"accumulated": got, "expected": None if args.adaptive else expect * n},
         "actual_samples": actual_samples,
         "value_actual": round(actual_samples / elapsed / 1e6, 3) if actual_samples is not None else None,
         "setup_s": round(setup_s, 2),
     }
     if world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(scene_file, W, H, args.cpu_seconds)
+        # the whole job for the Cornell config, full frame x 1 spp otherwise
+        job = P * args.steps if args.scene == "cornell" else 1
+        line["cpu_baseline"] = cpu_baseline(scene_file, W, H, args.cpu_seconds, passes=job)
     else:
         line["cpu_baseline"] = None
     print(json.dumps(line), flush=True)

@@ -48,14 +48,51 @@
 extern "C" {
 #endif
 
-/* ---------------- reference-layout types (byte-identical) ---------------- */
+/* ABI version: 3 = rt_scene_prepare(const Scene *, rt_scene_t *) without
+ * counts (the counted form is rt_scene_prepare_counts), RtDeviations and
+ * rt_deviation_stats, rt_abi_version.  An integrator checks
+ * rt_abi_version() == RT_ABI_VERSION at start-up: a binary built against an
+ * older header would otherwise link (C linkage) and mis-pass arguments. */
+#define RT_ABI_VERSION 3
+
+/* CUDA uchar4, used for texels (rt/scene.cuh:18) */
+typedef struct RtUChar4 { uint8_t x, y, z, w; } RtUChar4;
+
+/* ---------------- reference-layout types (byte-identical) ----------------
+ * A C++ caller that brings the reference's own types — the reference is one
+ * translation unit (rt/main.cu:8-14) whose headers define Vec2D, Vec3D
+ * (rt/math_library.cuh:55,99), Texture, Material, Triangle, KD_Tree_Node,
+ * Bounding_Box, KD_Tree, Scene (rt/scene.cuh:16-121), G_Buffer
+ * (rt/screen.cuh:15) and Camera (rt/camera.cuh:15) — defines
+ * ISAKLM_RT_CALLER_TYPES before including this header.  The definitions
+ * below are then replaced by forward declarations, so the header can come
+ * BEFORE those types (G_Buffer's constructor, rt/screen.cuh:22-46, already
+ * calls the allocation functions) or after them; the functions take the
+ * caller's types (C linkage: type names do not enter the symbols).  Once all
+ * of them are defined, the caller writes ISAKLM_RT_CHECK_LAYOUT(); at
+ * namespace scope: the static_asserts of the byte layout this library
+ * assumes.  See INTEGRATION.md and tests/native/ref_main_shape.cpp. */
+#ifdef ISAKLM_RT_CALLER_TYPES
+#ifndef __cplusplus
+#error "ISAKLM_RT_CALLER_TYPES: the reference's types are C++ (anonymous unions, constructors)"
+#endif
+struct Vec2D;
+struct Vec3D;
+struct Texture;
+struct Material;
+struct Triangle;
+struct KD_Tree_Node;
+struct Bounding_Box;
+struct KD_Tree;
+struct Scene;
+struct G_Buffer;
+struct Camera;
+#else
 
 /* rt/math_library.cuh:71-82 (union {x,u},{y,v}) */
 typedef struct Vec2D { float x, y; } Vec2D;
 /* rt/math_library.cuh:115-131 (union {x,r},{y,g},{z,b}) */
 typedef struct Vec3D { float x, y, z; } Vec3D;
-/* CUDA uchar4, used for texels (rt/scene.cuh:18) */
-typedef struct RtUChar4 { uint8_t x, y, z, w; } RtUChar4;
 
 /* rt/scene.cuh:16-21 */
 typedef struct Texture {
@@ -127,23 +164,30 @@ typedef struct Camera {
     float aperture_radius;
 } Camera;
 
+#endif /* ISAKLM_RT_CALLER_TYPES */
+
 #ifdef __cplusplus
-static_assert(sizeof(Vec2D) == 8, "Vec2D");
-static_assert(sizeof(Vec3D) == 12, "Vec3D");
-static_assert(sizeof(Texture) == 16, "Texture");
-static_assert(sizeof(Material) == 56 && offsetof(Material, roughness) == 24 &&
-              offsetof(Material, transparent) == 36 && offsetof(Material, texture) == 40, "Material");
-static_assert(sizeof(Triangle) == 152 && offsetof(Triangle, n1) == 36 && offsetof(Triangle, uv1) == 72 &&
-              offsetof(Triangle, material) == 96, "Triangle");
-static_assert(sizeof(KD_Tree_Node) == 20 && offsetof(KD_Tree_Node, plane_axis) == 8 &&
-              offsetof(KD_Tree_Node, plane_offset) == 12 && offsetof(KD_Tree_Node, is_leaf_node) == 16,
-              "KD_Tree_Node");
-static_assert(sizeof(Bounding_Box) == 24, "Bounding_Box");
-static_assert(sizeof(KD_Tree) == 40, "KD_Tree");
-static_assert(sizeof(Scene) == 72 && offsetof(Scene, light_indicies) == 16 && offsetof(Scene, kd_tree) == 32,
-              "Scene");
-static_assert(sizeof(G_Buffer) == 32, "G_Buffer");
+/* the reference's byte layout */
+#define ISAKLM_RT_CHECK_LAYOUT()                                                                              \
+static_assert(sizeof(Vec2D) == 8, "Vec2D"); \
+static_assert(sizeof(Vec3D) == 12, "Vec3D"); \
+static_assert(sizeof(Texture) == 16, "Texture"); \
+static_assert(sizeof(Material) == 56 && offsetof(Material, roughness) == 24 && \
+              offsetof(Material, transparent) == 36 && offsetof(Material, texture) == 40, "Material"); \
+static_assert(sizeof(Triangle) == 152 && offsetof(Triangle, n1) == 36 && offsetof(Triangle, uv1) == 72 && \
+              offsetof(Triangle, material) == 96, "Triangle"); \
+static_assert(sizeof(KD_Tree_Node) == 20 && offsetof(KD_Tree_Node, plane_axis) == 8 && \
+              offsetof(KD_Tree_Node, plane_offset) == 12 && offsetof(KD_Tree_Node, is_leaf_node) == 16, \
+              "KD_Tree_Node"); \
+static_assert(sizeof(Bounding_Box) == 24, "Bounding_Box"); \
+static_assert(sizeof(KD_Tree) == 40, "KD_Tree"); \
+static_assert(sizeof(Scene) == 72 && offsetof(Scene, light_indicies) == 16 && offsetof(Scene, kd_tree) == 32, \
+              "Scene"); \
+static_assert(sizeof(G_Buffer) == 32, "G_Buffer"); \
 static_assert(sizeof(Camera) == 28 && offsetof(Camera, FOV) == 20, "Camera");
+#ifndef ISAKLM_RT_CALLER_TYPES
+ISAKLM_RT_CHECK_LAYOUT()
+#endif
 #endif
 
 /* ---------------- status codes ---------------- */
@@ -157,6 +201,7 @@ static_assert(sizeof(Camera) == 28 && offsetof(Camera, FOV) == 20, "Camera");
 
 const char *rt_last_error(void);
 const char *rt_version(void);
+int rt_abi_version(void); /* RT_ABI_VERSION of the built library */
 
 /* ---------------- texture decoding ----------------
  * stbi_load(path, &w, &h, &n, 4) as make_texture (rt/scene.cuh:25-63) calls
@@ -375,6 +420,25 @@ typedef struct RtProfile {
     int pipelines;
 } RtProfile;
 int rt_last_profile(RtProfile *out);
+
+/* Always-on deviation statistics of every rt_render on the current device
+ * since the last reset (recorded by every kernel, counting or not, at one
+ * device-scope atomic per rare event).  The reference's bounce loop is
+ * unbounded (rt/path_tracing.cuh:279-319); the build stops a path only at a
+ * watchdog of 2^24 - 1 extension rays or at RtOptions.max_depth.
+ * deep_hist[k] counts paths that ended at depth d (extension rays, as
+ * RT_CNT_MAXDEPTH) with 64 * 2^k <= d < 64 * 2^(k+1); max_deep_depth is the
+ * longest of them (0 if no path reached depth 64).  reset != 0 zeroes the
+ * statistics after reading them.  Synchronises the device. */
+#define RT_DEV_HIST_BINS 18
+typedef struct RtDeviations {
+    unsigned long long watchdog_paths; /* cut by the watchdog (max_depth 0): a deviation from the reference */
+    unsigned long long cut_paths;      /* cut at the depth limit (watchdog or max_depth) */
+    unsigned long long max_deep_depth; /* longest path that reached depth 64 */
+    unsigned long long deep_paths;     /* paths that reached depth 64 (sum of deep_hist) */
+    unsigned long long deep_hist[RT_DEV_HIST_BINS];
+} RtDeviations;
+int rt_deviation_stats(RtDeviations *out, int reset);
 
 void rt_default_options(RtOptions *opt);
 /* render(): if sample_count == 0 the frame's fb/sq/count are reset first

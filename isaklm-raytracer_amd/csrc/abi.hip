@@ -111,12 +111,54 @@ int upload_prepared(const rt_host::PreparedHost &h, int ntris, int nindices, rt_
     return RT_OK;
 }
 
+// always-on deviation statistics (RT_DEV_*), one zeroed block per device
+std::mutex g_dev_mu;
+std::map<int, unsigned long long *> g_dev_stats;
+
+unsigned long long *dev_stats_block()
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> g(g_dev_mu);
+    auto it = g_dev_stats.find(dev);
+    if (it != g_dev_stats.end()) return it->second;
+    void *p = nullptr;
+    if (hipMalloc(&p, RT_DEV_WORDS * 8) != hipSuccess) return nullptr;
+    if (hipMemset(p, 0, RT_DEV_WORDS * 8) != hipSuccess) {
+        (void)hipFree(p);
+        return nullptr;
+    }
+    g_dev_stats[dev] = (unsigned long long *)p;
+    return (unsigned long long *)p;
+}
+
 } // namespace
 
 extern "C" {
 
 const char *rt_last_error(void) { return g_error.c_str(); }
-const char *rt_version(void) { return "isaklm-raytracer_amd 0.1 (gfx950)"; }
+const char *rt_version(void) { return "isaklm-raytracer_amd 0.3 (gfx950)"; }
+int rt_abi_version(void) { return RT_ABI_VERSION; }
+
+int rt_deviation_stats(RtDeviations *out, int reset)
+{
+    if (!out) { rt_set_error("rt_deviation_stats: null out"); return RT_E_INVALID; }
+    unsigned long long *d = dev_stats_block();
+    if (!d) { rt_set_error("rt_deviation_stats: no device block"); return RT_E_HIP; }
+    unsigned long long w[RT_DEV_WORDS];
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpy(w, d, sizeof w, hipMemcpyDeviceToHost));
+    memset(out, 0, sizeof *out);
+    out->watchdog_paths = w[RT_DEV_WATCHDOG];
+    out->cut_paths = w[RT_DEV_CUT];
+    out->max_deep_depth = w[RT_DEV_MAXDEPTH];
+    for (int k = 0; k < RT_DEV_HIST_BINS; ++k) {
+        out->deep_hist[k] = w[RT_DEV_HIST + k];
+        out->deep_paths += w[RT_DEV_HIST + k];
+    }
+    if (reset) HIPCHK(hipMemset(d, 0, RT_DEV_WORDS * 8));
+    return RT_OK;
+}
 
 // ---------------- device memory ----------------
 int rt_device_alloc(void **ptr, size_t bytes)
@@ -631,6 +673,11 @@ int rt_render(rt_scene_t scene, G_Buffer g, Camera cam, int sample_count, const 
     fr.num_shards = o.num_shards > 1 ? o.num_shards : 1;
     fr.counters = o.counters_device;
     fr.wave_times = o.wave_times_device;
+    fr.dev_stats = dev_stats_block();
+    if (!fr.dev_stats) {
+        rt_set_error("rt_render: deviation statistics block: %s", hipGetErrorString(hipGetLastError()));
+        return RT_E_HIP;
+    }
 
     // Camera::rotation() and tanf(FOV / 2) are frame constants (rt/camera.cuh:22-25, :381)
     RtDevCamera dc;

@@ -100,6 +100,7 @@ __global__ void __launch_bounds__(RT_BLOCK, STACK <= RT_STACK_SMALL ? 4 : 2) rt_
         bool finish = false;
         if (!shadow && depth == limit) { // max_depth / watchdog
             if (COUNT && fr.max_depth <= 0) c.v[RT_CNT_WATCHDOG]++;
+            dev_record_cut(fr);
             finish = true;
         } else {
             if (!shadow) ++depth;
@@ -154,6 +155,7 @@ __global__ void __launch_bounds__(RT_BLOCK, STACK <= RT_STACK_SMALL ? 4 : 2) rt_
         }
         if (finish) { // accumulation (:322-324)
             if (COUNT) c.path_end(depth);
+            dev_record_end(fr, depth);
             fb = fb + L;
             sq = sq + rt_square(rt_luminance(L));
             ++count;

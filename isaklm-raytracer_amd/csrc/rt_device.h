@@ -35,7 +35,22 @@
 #define RT_STACK_DEPTH 32
 #define RT_REF_STACK 19 // KD_TREE_DEPTH (rt/macros.h): the reference's stack arrays' length
 #define RT_LEAF_TAG 3u
-#define RT_WATCHDOG_BOUNCES 65536 // SURVEY H8; never reached by a parity config
+// the reference's bounce loop is unbounded (rt/path_tracing.cuh:
+// 279-319).  The watchdog cuts a path only at 2^24 - 1 extension rays (the
+// largest depth the wavefront path flags hold, flags >> 8): far above the
+// longest path measured on any test or bench scene (RtDeviations, bench line).
+#define RT_WATCHDOG_BOUNCES ((1 << 24) - 1)
+// always-on deviation statistics (rt_deviation_stats): a path that ends at
+// this depth or deeper is recorded (max depth, log2 histogram) with one
+// device-scope atomic — rare (total internal reflection in glass)
+#define RT_DEEP_PATH 64
+#define RT_DEV_WATCHDOG 0   // paths cut by the watchdog (max_depth == 0)
+#define RT_DEV_MAXDEPTH 1   // longest path that ended at depth >= RT_DEEP_PATH (atomic max)
+#define RT_DEV_CUT 2        // paths cut at the depth limit (watchdog or RtOptions.max_depth)
+#define RT_DEV_HIST 3       // + k: paths ending at depth in [64 * 2^k, 64 * 2^(k+1)), k < RT_DEV_HIST_BINS
+                            // (isaklm_rt.h: 18 bins, 64 * 2^18 = 2^24 > RT_WATCHDOG_BOUNCES)
+#define RT_DEV_WORDS 32
+static_assert(RT_DEV_HIST + RT_DEV_HIST_BINS <= RT_DEV_WORDS, "deviation block");
 
 struct RtDevMaterial {          // 64 B
     float albedo[3];
@@ -98,4 +113,5 @@ struct RtDevFrame {
     unsigned long long *counters;
     unsigned long long *wave_times; // debug: per-wave s_memrealtime [start, end] (counting variant)
     int shard_id, num_shards;   // row-interleaved sharding: render rows y % num_shards == shard_id
+    unsigned long long *dev_stats; // RT_DEV_WORDS always-on deviation statistics (every kernel, counting or not)
 };

@@ -29,6 +29,24 @@ struct Cnt {
 
 __device__ __forceinline__ float as_float(uint32_t u) { return __uint_as_float(u); }
 
+// Always-on deviation statistics, counting build or not: a path
+// cut at the depth limit (rare: never, at the watchdog's 2^24 - 1) and a path
+// that ends at depth >= RT_DEEP_PATH (total internal reflection in glass; ~1
+// in 10^4 paths on room2m) each cost one or three device-scope atomics.
+__device__ __forceinline__ void dev_record_cut(const RtDevFrame &fr)
+{
+    atomicAdd(fr.dev_stats + RT_DEV_CUT, 1ull);
+    if (fr.max_depth <= 0) atomicAdd(fr.dev_stats + RT_DEV_WATCHDOG, 1ull);
+}
+__device__ __forceinline__ void dev_record_end(const RtDevFrame &fr, int depth)
+{
+    if (depth < RT_DEEP_PATH) return;
+    atomicMax(fr.dev_stats + RT_DEV_MAXDEPTH, (unsigned long long)depth);
+    int k = 31 - __clz(depth / RT_DEEP_PATH); // floor(log2(depth / 64))
+    k = k < RT_DEV_HIST_BINS - 1 ? k : RT_DEV_HIST_BINS - 1;
+    atomicAdd(fr.dev_stats + RT_DEV_HIST + k, 1ull);
+}
+
 // the pixel rows this call renders (RtOptions.num_shards > 1: row-interleaved shards)
 __device__ __forceinline__ bool rt_row_owned(const RtDevFrame &fr, int y)
 {

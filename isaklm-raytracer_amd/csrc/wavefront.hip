@@ -33,6 +33,9 @@ using namespace rtk;
 #ifndef WF_TBLOCK
 #define WF_TBLOCK 256 // threads per block of the queue kernels (wf_trace_coop, wf_shade)
 #endif
+// tgrid * WF_TBLOCK == grid * WF_BLOCK threads: the spill area (sized for
+// grid * WF_BLOCK threads, indexed by the global thread id) must cover them
+static_assert(WF_BLOCK % WF_TBLOCK == 0 && WF_TBLOCK % 64 == 0, "WF_TBLOCK must divide WF_BLOCK in whole waves");
 // wave priorities beside the other pipelines' trace waves (A/B, 4 rounds:
 // -1 % call time together): a pipeline's shade launch and the tail of its
 // trace launch are on its critical path, the other launches' bulk is not
@@ -628,6 +631,7 @@ __device__ __forceinline__ bool shade_step(const RtDevScene &sc, const RtDevFram
                         if (!(r > pr)) {
                             if (p.depth == limit) { // max_depth / watchdog before the next extension ray
                                 if (COUNT && fr.max_depth <= 0) c.v[RT_CNT_WATCHDOG]++;
+                                dev_record_cut(fr);
                             } else {
                                 ++p.depth;
                                 p.ext_live = true;
@@ -666,6 +670,7 @@ __device__ __forceinline__ bool shade_step(const RtDevScene &sc, const RtDevFram
             p.T = p.T * (1.0f / pr);
             if (p.depth == limit) { // max_depth / watchdog before the next extension ray
                 if (COUNT && fr.max_depth <= 0) c.v[RT_CNT_WATCHDOG]++;
+                dev_record_cut(fr);
                 finish = true;
             } else {
                 ++p.depth;
@@ -675,6 +680,7 @@ __device__ __forceinline__ bool shade_step(const RtDevScene &sc, const RtDevFram
     }
     if (finish) { // accumulation (:322-324), then the pixel's next pass
         if (COUNT) c.path_end(p.depth);
+        dev_record_end(fr, p.depth);
         const uint32_t slot = p.slot;
         Vec3D fb = fr.fb[slot] + p.L;
         float sq = fr.sq[slot] + rt_square(rt_luminance(p.L));
@@ -1231,11 +1237,13 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
     // the workspace (per-pixel path state, long-path hand-off) is shared by every
     // call on this device: a call on another stream than the previous one must
     // not start before that call's last wf_long slice and pipelines are done
-    if (w.recorded) {
-        if (hipStreamWaitEvent(stream, w.long_ev, 0) != hipSuccess) return -1;
-        for (int pi = 0; pi < WF_MAX_PIPES; ++pi)
-            if (w.pipe[pi].joined && hipStreamWaitEvent(stream, w.pipe[pi].join, 0) != hipSuccess) return -1;
-    }
+    // (every pipeline the previous call used, whatever this call's pipeline
+    // count: pixels may move to another pipeline while the previous call's
+    // finisher still writes their path state; the wf_long wait only if a
+    // slice was ever launched)
+    if (w.recorded && hipStreamWaitEvent(stream, w.long_ev, 0) != hipSuccess) return -1;
+    for (int pi = 0; pi < WF_MAX_PIPES; ++pi)
+        if (w.pipe[pi].joined && hipStreamWaitEvent(stream, w.pipe[pi].join, 0) != hipSuccess) return -1;
     if (long_depth > 0) {
         if (hipMemsetAsync(lst.long_flag, 0, slots * 4, stream) != hipSuccess) return -1;
         if (hipMemsetAsync(lst.long_ctr, 0, 256, stream) != hipSuccess) return -1;

@@ -73,6 +73,26 @@ def last_profile():
     return {k: getattr(p, k) for k, _ in RtProfile._fields_}
 
 
+DEV_HIST_BINS = 18
+
+
+class RtDeviations(ctypes.Structure):
+    _fields_ = [("watchdog_paths", ctypes.c_ulonglong), ("cut_paths", ctypes.c_ulonglong),
+                ("max_deep_depth", ctypes.c_ulonglong), ("deep_paths", ctypes.c_ulonglong),
+                ("deep_hist", ctypes.c_ulonglong * DEV_HIST_BINS)]
+
+
+def deviation_stats(reset=False):
+    """Always-on deviation statistics of every rt_render on this device since
+    the last reset (rt_deviation_stats): watchdog / depth-limit cuts and the
+    histogram of paths that ended at depth >= 64 (bin k: [64*2^k, 64*2^(k+1)))."""
+    d = RtDeviations()
+    check(lib().rt_deviation_stats(ctypes.byref(d), int(reset)))
+    return {"watchdog_paths": d.watchdog_paths, "cut_paths": d.cut_paths, "max_deep_depth": d.max_deep_depth,
+            "deep_paths": d.deep_paths, "deep_hist": [int(v) for v in d.deep_hist]}
+
+
+ABI_VERSION = 3  # RT_ABI_VERSION of include/isaklm_rt.h
 TRIANGLE_BYTES = 152
 NODE_BYTES = 20
 COUNTER_NAMES = ["node", "tri", "hit", "texel", "nee", "sample", "skip", "ray", "watchdog", "maxdepth"]
@@ -134,6 +154,11 @@ def lib():
         L.rt_render.argtypes = [vp, G_Buffer, Camera, i, ctypes.POINTER(RtOptions)]
         L.rt_tonemap.argtypes = [G_Buffer, vp, i, i, vp]
         L.rt_save_render.argtypes = [G_Buffer, i, i, ctypes.c_char_p]
+        L.rt_deviation_stats.argtypes = [ctypes.POINTER(RtDeviations), i]
+        L.rt_abi_version.restype = i
+        if L.rt_abi_version() != ABI_VERSION:
+            raise RtError(f"{LIB_PATH}: ABI version {L.rt_abi_version()}, this binding expects {ABI_VERSION} "
+                          "(rebuild with __graft_entry__.build())")
         _lib = L
     return _lib
 

@@ -13,9 +13,14 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liboracle.so")
-N_COUNTERS = 16
+N_COUNTERS = 40
 COUNTER_NAMES = ["node", "tri", "hit", "texel", "nee", "sample", "skip", "ray", "watchdog", "maxdepth"]
 DEEP_PUSH = 15  # CNT_DEEP_PUSH / RT_CNT_DEEP_PUSH
+CUT = 16  # CNT_CUT: paths cut at the depth limit (watchdog or max_depth)
+DEEP_HIST = 17  # CNT_DEEP_HIST: 18 bins of paths ending at depth in [64*2^k, 64*2^(k+1))
+DEEP_HIST_BINS = 18
+# hazard instrumentation: inputs that triggered each quirk
+HAZARDS = {"xi_one": 35, "exit_tie": 36, "on_split": 37, "axis_parallel": 38, "degenerate": 39}
 
 _lib = None
 
@@ -147,6 +152,9 @@ class OracleScene:
                         0 if px is None else len(px), sample_count_arg, ctypes.byref(o), _p(counters))
         out = {k: int(counters[i]) for i, k in enumerate(COUNTER_NAMES)}
         out["deep_push"] = int(counters[DEEP_PUSH])
+        out["cut"] = int(counters[CUT])
+        out["deep_hist"] = [int(v) for v in counters[DEEP_HIST:DEEP_HIST + DEEP_HIST_BINS]]
+        out["hazards"] = {k: int(counters[i]) for k, i in HAZARDS.items()}
         return out
 
     def __del__(self):

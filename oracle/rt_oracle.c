@@ -45,10 +45,23 @@ const char *or_last_error(void) { return g_err; }
 #define MAX_COLOR_CHANNEL 255            /* rt/macros.h:9 */
 #define PIF 3.1415926536f                /* rt/math_library.cuh:9 */
 #define TAUF (PIF * 2)                   /* rt/math_library.cuh:10 */
-#define WATCHDOG_BOUNCES 65536           /* never fires in parity configs */
+#define WATCHDOG_BOUNCES ((1 << 24) - 1) /* as the product (rt_device.h); never fires in parity configs */
+#define DEEP_PATH 64                     /* deviation histogram: paths ending at depth >= 64 */
+#define DEEP_HIST_BINS 18
 
 enum { CNT_NODE = 0, CNT_TRI, CNT_HIT, CNT_TEXEL, CNT_NEE, CNT_SAMPLE, CNT_SKIP, CNT_RAY, CNT_WATCHDOG, CNT_MAXDEPTH,
-       CNT_DEEP_PUSH = 15 /* pushes at stack index >= KD_TREE_DEPTH: past the reference's arrays */ };
+       CNT_DEEP_PUSH = 15 /* pushes at stack index >= KD_TREE_DEPTH: past the reference's arrays */,
+       CNT_CUT = 16       /* paths cut at the depth limit (watchdog or max_depth) */,
+       CNT_DEEP_HIST = 17 /* + k: paths ending at depth in [64 * 2^k, 64 * 2^(k+1)), k < DEEP_HIST_BINS
+                             (the product's always-on RtDeviations, rt_deviation_stats) */,
+       /* hazard instrumentation: how often an input
+        * triggered each quirk the build reproduces, so a test can show it
+        * was exercised */
+       CNT_XI_ONE = 35,        /* H4: NEE light pick with xi == 1.0 (reads the padded entry) */
+       CNT_EXIT_TIE = 36,      /* H6: an inside hit with t == the leaf's exit (deferred to a later leaf) */
+       CNT_ON_SPLIT = 37,      /* H5: inner node visited with the ray origin exactly on its split */
+       CNT_AXIS_PARALLEL = 38, /* H7: inner node visited with direction[axis] == 0 (t = +-inf / NaN) */
+       CNT_DEGENERATE = 39     /* H7: triangle test with a NaN plane normal (zero-area triangle) */ };
 
 /* ------------------------------------------------ types (rt/scene.cuh etc.) */
 typedef struct { float x, y; } V2;                     /* rt/math_library.cuh:55-66 */
@@ -92,6 +105,7 @@ struct OrScene {
     int *indices;
     int nindices, indexcap;
     BBox bounds;
+    unsigned char *degenerate; /* per triangle: NaN plane normal (test instrumentation, CNT_DEGENERATE) */
 };
 
 /* -------------------------------------------- math (rt/math_library.cuh) */
@@ -282,7 +296,10 @@ static bool trace_leaf(const OrScene *sc, Ray ray, float max_t, int off, int cou
         V3 b = {0.0f, 0.0f, 0.0f};
         float tt = FLT_MAX;
         cnt[CNT_TRI] += 1;
-        if (intersect_triangle(ray, t, &b, &tt) && (tt < smallest)) {
+        const bool inside = intersect_triangle(ray, t, &b, &tt);
+        if (inside && tt == max_t) cnt[CNT_EXIT_TIE] += 1;
+        if (sc->degenerate[index]) cnt[CNT_DEGENERATE] += 1;
+        if (inside && (tt < smallest)) {
             hit = true;
             smallest = tt;
             ti = index;
@@ -364,6 +381,8 @@ static bool trace_ray(const OrScene *sc, Ray ray, Sample *sm, unsigned long long
         float exit_ = exit_d[sp];
         while (!node.is_leaf_node) {
             int near_i = node.a, far_i = node.b;
+            if (axis_of(ray.position, node.plane_axis) == node.plane_offset) cnt[CNT_ON_SPLIT] += 1;
+            if (axis_of(ray.direction, node.plane_axis) == 0.0f) cnt[CNT_AXIS_PARALLEL] += 1;
             if (axis_of(ray.position, node.plane_axis) >= node.plane_offset) {
                 near_i = node.b;
                 far_i = node.a;
@@ -655,6 +674,7 @@ static V3 sample_direct_light(const OrScene *sc, V3 pos, V3 normal, uint32_t *rn
         rng_next(rng);
         return v3(0.0f, 0.0f, 0.0f);
     }
+    if (xi == 1.0f) cnt[CNT_XI_ONE] += 1;
     int li = sc->lights[(int)(xi * (float)sc->nlights)];
     const Triangle *light = &sc->tris[li];
     V3 rp = random_point_in_triangle(light, rng);
@@ -695,6 +715,7 @@ static V3 trace_path(const OrScene *sc, Ray primary, uint32_t *rng, int max_dept
     while (1) {
         if (depth == limit) {
             if (max_depth <= 0) cnt[CNT_WATCHDOG] += 1;
+            cnt[CNT_CUT] += 1;
             break;
         }
         ++depth;
@@ -716,6 +737,11 @@ static V3 trace_path(const OrScene *sc, Ray primary, uint32_t *rng, int max_dept
         T = mulvs(T, 1.0f / p);
     }
     if ((unsigned long long)depth > cnt[CNT_MAXDEPTH]) cnt[CNT_MAXDEPTH] = (unsigned long long)depth;
+    if (depth >= DEEP_PATH) {
+        int k = 0;
+        while (k < DEEP_HIST_BINS - 1 && depth >= (DEEP_PATH << (k + 1))) ++k;
+        cnt[CNT_DEEP_HIST + k] += 1;
+    }
     return L;
 }
 
@@ -944,6 +970,12 @@ static void finish_scene(OrScene *sc)
         if (e.x > 0 || e.y > 0 || e.z > 0) sc->lights[sc->nlights++] = i;
     }
     sc->lights[sc->nlights] = sc->nlights > 0 ? sc->lights[sc->nlights - 1] : 0; /* H4 padding */
+    sc->degenerate = (unsigned char *)calloc((size_t)sc->ntris + 1, 1);
+    for (int i = 0; i < sc->ntris; ++i) {
+        const Triangle *t = &sc->tris[i];
+        V3 n = normalize(cross(sub(t->p2, t->p1), sub(t->p3, t->p1)));
+        sc->degenerate[i] = n.x != n.x || n.y != n.y || n.z != n.z;
+    }
 }
 
 /* ------------------------------------------ loader (rt/mesh_loading.cuh) */
@@ -1342,7 +1374,7 @@ OrScene *or_scene_from_triangles(const void *tris, int count)
 void or_scene_free(OrScene *s)
 {
     if (!s) return;
-    free(s->tris); free(s->lights); free(s->nodes); free(s->indices);
+    free(s->tris); free(s->lights); free(s->nodes); free(s->indices); free(s->degenerate);
     free(s);
 }
 

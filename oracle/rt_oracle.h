@@ -28,7 +28,7 @@ extern "C" {
 typedef struct OrScene OrScene;
 
 /* counters, same meaning as RT_CNT_* in include/isaklm_rt.h */
-#define OR_CNT_COUNT 16
+#define OR_CNT_COUNT 40 /* [16] depth-limit cuts, [17..34] deep-path histogram, [35..39] hazard triggers */
 
 typedef struct OrOptions {
     int width, height;

@@ -54,7 +54,11 @@ class GpuRun:
 
 
 def oracle_render(path, W, H, passes, calls=1, adaptive=False, min_samples=100, tolerance=0.05, max_depth=0,
-                  seed_skip=0, pixels=None, scene=None, camera=None):
+                  seed_skip=0, pixels=None, scene=None, camera=None, deviations=None):
+    """The oracle over the same calls as GpuRun.render.  Returns the G_Buffer
+    arrays and the counters comparable with the GPU's counting build; the
+    deviation statistics (depth-limit cuts, deep-path histogram: the GPU's
+    always-on rt_deviation_stats) go into the `deviations` dict if given."""
     sc = scene or oracle.OracleScene(path)
     n = W * H
     fb = np.zeros(n * 3, np.float32)
@@ -67,6 +71,14 @@ def oracle_render(path, W, H, passes, calls=1, adaptive=False, min_samples=100, 
     for c, pc in enumerate(per_call):
         k = sc.render(cam, fb, sq, cnt, rng, W, H, pc, sample_count_arg=0 if c == 0 else 1, pixels=pixels,
                       adaptive=adaptive, min_samples=min_samples, tolerance=tolerance, max_depth=max_depth)
+        cut, hist, haz = k.pop("cut"), k.pop("deep_hist"), k.pop("hazards")
+        if deviations is not None:
+            deviations["cut"] = deviations.get("cut", 0) + cut
+            old = deviations.get("deep_hist", [0] * len(hist))
+            deviations["deep_hist"] = [a + b for a, b in zip(old, hist)]
+            h = deviations.setdefault("hazards", {})
+            for key, v in haz.items():
+                h[key] = h.get(key, 0) + v
         for key, v in k.items():
             total[key] = max(total.get(key, 0), v) if key == "maxdepth" else total.get(key, 0) + v
     return (fb.reshape(n, 3), sq, cnt, rng), total
@@ -90,6 +102,42 @@ def rel_linf(gpu_fb, gpu_cnt, ref_fb, ref_cnt):
     b = ref_fb / np.maximum(ref_cnt, 1)[:, None]
     den = np.maximum(np.abs(b), 1e-30)
     return float(np.max(np.abs(a - b) / den)) if len(a) else 0.0
+
+
+# ------------------------------------------------------------ deep-path trap
+def make_trap_scene(d, length=60.0):
+    """Deep paths on demand: a light guide.  The camera looks
+    obliquely into the end face of a long, thin glass rod (glass.mat: n 1.51,
+    roughness 0.001).  A camera ray refracted through the end face meets the
+    side faces beyond the critical angle, so it is guided down the rod by
+    total internal reflection; inside the medium the reference's specular
+    weight is exactly 1 (rt/path_tracing.cuh:194-197) and the roulette
+    survives with p = max(T) = 1, so the path runs ~100-1,000 bounces to the
+    far end.  Rod 0.2 x 0.2 x `length` (the loader re-centres it: z in
+    [-length/2, length/2]), a floor and a lamp beside it."""
+    os.makedirs(d, exist_ok=True)
+    with open(os.path.join(d, "trap.mat"), "w") as f:
+        f.write("material glass\nalbedo 0.995 0.995 0.995\nroughness 0.001\nn 1.51\ntransparent\n\n"
+                "material floor\nalbedo 0.7 0.7 0.7\nroughness 0.5\nn 1.5\n\n"
+                "material lamp\nalbedo 0.8 0.8 0.8\nemittance 6.0 5.5 5.0\nroughness 0.5\nn 1.5\n")
+    h, L = 0.1, length
+    v = [(-h, -h, 0), (h, -h, 0), (h, h, 0), (-h, h, 0), (-h, -h, L), (h, -h, L), (h, h, L), (-h, h, L)]
+    rod = ["# glass rod"] + [f"v {x} {y} {z}" for x, y, z in v]
+    rod += ["usemtl glass", "f 1 4 3 2", "f 5 6 7 8", "f 1 2 6 5", "f 4 8 7 3", "f 1 5 8 4", "f 2 3 7 6"]
+    with open(os.path.join(d, "rod.obj"), "w") as fh:
+        fh.write("\n".join(rod) + "\n")
+    room = ["# floor and lamp", "v -4 0 -4", "v 4 0 -4", "v 4 0 4", "v -4 0 4",
+            "v -0.5 3 -0.5", "v 0.5 3 -0.5", "v 0.5 3 0.5", "v -0.5 3 0.5",
+            "usemtl floor", "f 1 2 3 4", "usemtl lamp", "f 5 8 7 6"]
+    with open(os.path.join(d, "room.obj"), "w") as fh:
+        fh.write("\n".join(room) + "\n")
+    scene = os.path.join(d, "scene.txt")
+    with open(scene, "w") as fh:
+        # the camera 0.43 in front of the end face (z = -length/2), 35 degrees off its axis
+        fh.write("mesh rod.obj trap.mat 0 0 0 0 0 1 0\n"
+                 f"mesh room.obj trap.mat 0 0.5 {-L / 2:.1f} 0 0 1 0\n"
+                 f"camera -0.25 0.02 {-L / 2 - 0.35:.2f} 0.6202 -0.0465 0.3 0.002\n")
+    return scene
 
 
 # ------------------------------------------------------------ textured scene

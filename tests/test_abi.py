@@ -116,3 +116,47 @@ def test_gbuffer_checkpoint_errors(tmp_path):
     assert L.rt_gbuffer_load(str(tmp_path / "junk.gbuf").encode(), g, 4, 4, ctypes.byref(sc)) == -4
     (tmp_path / "other.gbuf").write_bytes(b"RTGBUF01" + struct.pack("<4i", 5, 5, 7, 0) + bytes(25 * 24))
     assert L.rt_gbuffer_load(str(tmp_path / "other.gbuf").encode(), g, 4, 4, ctypes.byref(sc)) == -1  # RT_E_INVALID
+
+
+MAIN_SHAPE = os.path.join(ROOT, "tests", "native", "ref_main_shape.cpp")
+
+
+def build_main_shape(out_dir):
+    """Compile + link the reference-main-shaped TU (its own reference-layout
+    types, then isaklm_rt.h with ISAKLM_RT_CALLER_TYPES) against the library."""
+    exe = os.path.join(str(out_dir), "ref_main_shape")
+    lib_dir = os.path.dirname(rt.LIB_PATH)
+    subprocess.run(["g++", "-std=c++17", "-O1", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), MAIN_SHAPE,
+                    "-o", exe, "-L", lib_dir, "-lisaklm_rt", "-Wl,-rpath," + lib_dir,
+                    "-Wl,-rpath,/opt/rocm/lib"], check=True, capture_output=True, text=True)
+    return exe
+
+
+def test_reference_shaped_main_compiles_and_links(tmp_path):
+    """INTEGRATION.md's drop-in: a TU that already defines the reference's
+    Vec2D / Vec3D / Texture / Material / Triangle / KD_Tree_Node /
+    Bounding_Box / KD_Tree / Scene / G_Buffer / Camera (anonymous unions,
+    constructors, member functions as in rt/*.cuh) includes isaklm_rt.h after
+    them with ISAKLM_RT_CALLER_TYPES: it compiles (the header's static_asserts
+    check the caller's layouts), links, and runs up to its usage check."""
+    exe = build_main_shape(tmp_path)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 2 and "usage: ref_main_shape" in r.stderr
+
+
+def test_caller_types_layout_mismatch_is_a_compile_error(tmp_path):
+    """A caller type with another layout (Camera without aperture_radius)
+    fails the header's static_asserts instead of corrupting rt_render's
+    arguments at run time."""
+    src = tmp_path / "bad.cpp"
+    src.write_text(open(MAIN_SHAPE).read().replace("    float FOV;\n    float aperture_radius;\n", "    float FOV;\n"))
+    r = subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-I", os.path.join(ROOT, "include"), str(src)],
+                       capture_output=True, text=True)
+    assert r.returncode != 0 and "Camera" in r.stderr
+
+
+def test_abi_version_matches_header():
+    import re as _re
+
+    text = open(HEADER).read()
+    assert rt.lib().rt_abi_version() == int(_re.search(r"#define RT_ABI_VERSION (\d+)", text).group(1)) == rt.ABI_VERSION

@@ -68,3 +68,32 @@ def test_driver_checkpoint_resume(tmp_path):
     assert ck.stat().st_size == 8 + 16 + W * H * 24 and not os.path.exists(str(ck) + ".tmp")
     np.testing.assert_array_equal(rt.decode_image(str(resumed)), rt.decode_image(str(straight)))
     assert not np.array_equal(rt.decode_image(str(tmp_path / "half.png")), rt.decode_image(str(straight)))
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(180)
+def test_reference_shaped_main_renders_like_the_oracle(tmp_path):
+    """The reference-main-shaped program (tests/native/ref_main_shape.cpp: the
+    caller's own reference types, cudaMalloc/cudaMemcpy -> rt_device_alloc /
+    rt_upload, G_Buffer(), create_scene(), rt_scene_prepare on the Scene
+    alone, the pass loop over rt_render, save_render) writes the oracle's
+    tonemapped frame bit for bit."""
+    import test_abi
+
+    exe = test_abi.build_main_shape(tmp_path)
+    W, H, SPP, P = 48, 40, 7, 3
+    scene = helpers.scene_path("cornell")
+    out = tmp_path / "main_shape.png"
+    r = subprocess.run([exe, scene, str(W), str(H), str(SPP), str(P), str(out)], capture_output=True, text=True,
+                       timeout=150)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+    osc = oracle.OracleScene(scene)
+    n = W * H
+    fb, sq, cnt = np.zeros(n * 3, np.float32), np.zeros(n, np.float32), np.zeros(n, np.int32)
+    seeds = oracle.mt19937(n)
+    done = 0
+    while done < SPP:
+        k = min(P, SPP - done)
+        osc.render(osc.camera, fb, sq, cnt, seeds, W, H, k, sample_count_arg=done, adaptive=False)
+        done += k
+    np.testing.assert_array_equal(rt.decode_image(str(out)), oracle.tonemap(fb, cnt).reshape(H, W, 4)[::-1])
