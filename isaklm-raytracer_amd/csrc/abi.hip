@@ -61,9 +61,13 @@ int upload_vec(RtPreparedScene &s, const std::vector<T> &v, const T **out)
 {
     void *p = nullptr;
     size_t n = v.size() * sizeof(T);
-    HIPCHK(hipMalloc(&p, n > 0 ? n : 16));
+    // 64 zero bytes of slack after every array: the traversal's 16-B node-pair
+    // loads read one node past the last (never used: the last node in
+    // pre-order is a leaf)
+    HIPCHK(hipMalloc(&p, n + 64));
     s.allocs.push_back(p);
     s.bytes += n;
+    HIPCHK(hipMemset(p, 0, n + 64));
     if (n) HIPCHK(hipMemcpy(p, v.data(), n, hipMemcpyHostToDevice));
     *out = (const T *)p;
     return RT_OK;

@@ -18,6 +18,9 @@
 #pragma once
 
 #define WF_COOP_LIST 128 // per-wave LDS list of plane-test candidates
+#ifndef WF_NODE_PAIRS
+#define WF_NODE_PAIRS 0 // descent: 16-B node-pair loads (child1 arrives with its parent)
+#endif
 
 namespace rtk {
 
@@ -145,9 +148,31 @@ __device__ __forceinline__ bool coop_descend(const RtDevScene &sc, CoopRay &r, S
     // one flag per lane instead of early returns: the loop has a single
     // (wave-uniform) exit, which keeps the exec-mask bookkeeping small
     bool act = r.live && !r.pend, ended = false;
+#if WF_NODE_PAIRS
+    // Node pairs: child1 is always node + 1 (pre-order), so one 16-B load at
+    // node i brings node i + 1 along; a step into child1 right after a load
+    // needs no load of its own (one dependent memory round trip fewer).  The
+    // node array carries one padding node (upload_vec's slack).
+    bool have = false;    // nx = the nodes word pair of r.node, already loaded
+    uint2 nx = make_uint2(0u, 0u);
+#endif
     for (int k = 0; k < cap && __any(act); ++k) {
         if (!act) continue;
+#if WF_NODE_PAIRS
+        uint2 nd, n1 = make_uint2(0u, 0u);
+        const bool loaded = !have;
+        if (have) {
+            nd = nx;
+        } else {
+            const uint2 *np = reinterpret_cast<const uint2 *>(sc.nodes + 2 * (size_t)r.node);
+            nd = np[0];
+            n1 = np[1];
+        }
+        have = false;
+        const uint32_t at = r.node;
+#else
         const uint2 nd = *reinterpret_cast<const uint2 *>(sc.nodes + 2 * (size_t)r.node);
+#endif
         if (COUNT) c.v[RT_CNT_NODE]++;
         if ((nd.y & 3u) == RT_LEAF_TAG) {
             const int cnt = (int)(nd.y >> 2);
@@ -188,6 +213,12 @@ __device__ __forceinline__ bool coop_descend(const RtDevScene &sc, CoopRay &r, S
             r.node = near_c;
             r.exit_ = t;
         }
+#if WF_NODE_PAIRS
+        if (loaded && r.node == at + 1) {
+            have = true;
+            nx = n1;
+        }
+#endif
     }
     return ended;
 }

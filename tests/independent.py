@@ -178,9 +178,12 @@ def random_point_in_triangle(p1, p2, p3, rng):  # :222-233
 def direct_light(tris, lights, trace, pos, normal, rng):
     """sample_direct_light (:235-265) at N points.  `tris` = (n, 152) uint8
     reference-layout triangles, `lights` = light_indicies, `trace(rays6)` a
-    trace_ray returning (hit, triangle_index, surface normal) per ray.  The
-    reference reads light_indicies[light_count] when the draw is exactly 1.0
-    (SURVEY H4): taken here as the last light."""
+    trace_ray returning (hit, triangle_index, surface normal, emittance) per
+    ray — the emittance of the hit Sample, i.e. texture-modulated
+    (sample_texture, rt/trace_ray.cuh:155), which is what the reference
+    scales (:259), not the light's material emittance.  The reference reads
+    light_indicies[light_count] when the draw is exactly 1.0:
+    taken here as the last light."""
     xi, rng = rng_next(rng)
     nl = len(lights)
     if nl == 0:
@@ -190,11 +193,9 @@ def direct_light(tris, lights, trace, pos, normal, rng):
     k = (xi * f32(nl)).astype(np.int64)
     li = np.asarray(lights, np.int64)[np.minimum(k, nl - 1)]
     P = tris[li, :36].copy().view(f32).reshape(-1, 3, 3)
-    mat = tris[li, 96:120].copy().view(f32)
-    emit = mat[:, 3:6]
     rp, rng = random_point_in_triangle(P[:, 0], P[:, 1], P[:, 2], rng)
     d = normalize(rp - pos)
-    hit, tri, snorm = trace(np.concatenate([pos, d], axis=1).astype(f32))
+    hit, tri, snorm, emit = trace(np.concatenate([pos, d], axis=1).astype(f32))
     e1, e2 = P[:, 1] - P[:, 0], P[:, 2] - P[:, 0]
     cr = cross(e1, e2)
     area = (0.5 * np.sqrt(dot(cr, cr)).astype(np.float64)).astype(f32)  # 0.5 is a double

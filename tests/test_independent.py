@@ -116,9 +116,11 @@ def test_direct_light_matches_independent_restatement():
     assert n > 2000  # the box is open at the front
     state = g.integers(0, 2 ** 32, n, dtype=np.uint64).astype(np.uint32)
 
-    def trace(rays6):
+    def trace(rays6):  # the Cornell box is untextured: a hit's emittance is its material's
         o = osc.trace_rays(rays6)
-        return o[:, 0] == 1, o[:, 1].astype(np.int64), o[:, 5:8].astype(f32)
+        tri = o[:, 1].astype(np.int64)
+        emit = tris[np.maximum(tri, 0), 108:120].copy().view(f32).reshape(-1, 3)
+        return o[:, 0] == 1, tri, o[:, 5:8].astype(f32), emit
 
     mine, mine_rng = ind.direct_light(tris, lights, trace, pos, nrm, state)
     got = np.zeros((n, 3), f32)
