@@ -50,10 +50,11 @@ extern "C" {
 
 /* ABI version: 3 = rt_scene_prepare(const Scene *, rt_scene_t *) without
  * counts (the counted form is rt_scene_prepare_counts), RtDeviations and
- * rt_deviation_stats, rt_abi_version.  An integrator checks
+ * rt_deviation_stats, rt_abi_version; 4 = RT_CNT_COUNT 40 (the optional
+ * counters buffer grew).  An integrator checks
  * rt_abi_version() == RT_ABI_VERSION at start-up: a binary built against an
  * older header would otherwise link (C linkage) and mis-pass arguments. */
-#define RT_ABI_VERSION 3
+#define RT_ABI_VERSION 4
 
 /* CUDA uchar4, used for texels (rt/scene.cuh:18) */
 typedef struct RtUChar4 { uint8_t x, y, z, w; } RtUChar4;
@@ -346,7 +347,23 @@ enum {
     RT_CNT_T_WIDE_LOAD = 25,   /* wide_trace phases: frontier + node load, */
     RT_CNT_T_WIDE_LEAF = 26,   /* leaf batch, */
     RT_CNT_T_WIDE_EXPAND = 27, /* expansion */
-    RT_CNT_COUNT = 32
+    /* cooperative leaf test, counting build only: wave-time in the chunk
+     * loop's plane-load wait, chunk set-up (owner scan, next load issue),
+     * plane test + candidate append, and the barycentric stages */
+    RT_CNT_T_LEAF_WAIT = 28,
+    RT_CNT_T_LEAF_SETUP = 29,
+    RT_CNT_T_LEAF_TEST = 30,
+    RT_CNT_T_LEAF_BARY = 31,
+    /* cooperative trace, counting build only: traversal-stack pushes and
+     * pops beyond the LDS part of the stack (HBM spill), pending lanes summed
+     * over the wave's leaf tests and the number of those tests, and the
+     * descent's wave-time waiting for node loads */
+    RT_CNT_SPILL_PUSH = 32,
+    RT_CNT_SPILL_POP = 33,
+    RT_CNT_PEND_LANES = 34,
+    RT_CNT_LEAF_TESTS = 35,
+    RT_CNT_T_DESC_WAIT = 36,
+    RT_CNT_COUNT = 40
 };
 
 #define RT_KERNEL_MEGA 0

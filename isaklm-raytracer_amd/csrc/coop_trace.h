@@ -21,6 +21,9 @@
 #ifndef WF_NODE_PAIRS
 #define WF_NODE_PAIRS 0 // descent: 16-B node-pair loads (child1 arrives with its parent)
 #endif
+#ifndef WF_CHUNK_UNROLL
+#define WF_CHUNK_UNROLL 1 // leaf chunk loop unrolled over two register sets
+#endif
 
 namespace rtk {
 
@@ -173,6 +176,13 @@ __device__ __forceinline__ bool coop_descend(const RtDevScene &sc, CoopRay &r, S
 #else
         const uint2 nd = *reinterpret_cast<const uint2 *>(sc.nodes + 2 * (size_t)r.node);
 #endif
+        if (COUNT) {
+            // counting build: the wave-time spent waiting for this node load
+            const unsigned long long tq = __builtin_amdgcn_s_memtime();
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (__lane_id() == (__ffsll((long long)__ballot(1)) - 1))
+                c.v[RT_CNT_T_DESC_WAIT] += __builtin_amdgcn_s_memtime() - tq;
+        }
         if (COUNT) c.v[RT_CNT_NODE]++;
         if ((nd.y & 3u) == RT_LEAF_TAG) {
             const int cnt = (int)(nd.y >> 2);
@@ -187,6 +197,7 @@ __device__ __forceinline__ bool coop_descend(const RtDevScene &sc, CoopRay &r, S
                 ended = true;
                 act = false;
             } else {
+                if (COUNT && r.sp - 1 >= WF_LDS_STACK) c.v[RT_CNT_SPILL_POP]++;
                 coop_pop(r, stk);
             }
             continue;
@@ -208,6 +219,7 @@ __device__ __forceinline__ bool coop_descend(const RtDevScene &sc, CoopRay &r, S
             r.node = far_c;
         } else {
             if (COUNT && r.sp >= RT_REF_STACK) c.v[RT_CNT_DEEP_PUSH]++;
+            if (COUNT && r.sp >= WF_LDS_STACK) c.v[RT_CNT_SPILL_PUSH]++;
             stk.put(r.sp, far_c, t);
             ++r.sp;
             r.node = near_c;
@@ -268,29 +280,38 @@ __device__ __forceinline__ bool coop_leaves(const RtDevScene &sc, CoopRay &r, ST
         if (lane < rest) list[lane] = mv;
         list_n = rest;
     };
-    // Software pipeline: the owner, entry and plane load of chunk c + 1 are
-    // issued before chunk c's plane test, so its load latency overlaps it.
-    int nj = 0;
-    uint32_t nk = 0;
-    RtF4 nA = RtF4{0.0f, 0.0f, 0.0f, 0.0f};
-    auto setup = [&](int b) {
+    // counting build: wave-time split of the chunk loop (lane 0's clock; the
+    // explicit waits make the split observable and perturb it a little)
+    unsigned long long tw = 0;
+    auto tick = [&](int slot) {
+        if (COUNT) {
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            if (lane == 0 && slot >= 0) c.v[slot] += t - tw;
+            tw = t;
+        }
+    };
+    // one 64-pair chunk: its owner lanes, leaf entries and plane records
+    struct Chunk {
+        int j;
+        uint32_t k;
+        RtF4 A;
+    };
+    auto setup = [&](int b, Chunk &ch) {
         const int p = b + lane;
-        nj = chunk_owner(w.mark, start, leaf_count, b, carry);
-        carry = lane63(nj);
+        ch.j = chunk_owner(w.mark, start, leaf_count, b, carry);
+        carry = lane63(ch.j);
         // the shuffle runs on every lane: behind a `p < total` branch it would
         // read 0 from owners whose own position is past the end of the chunk
-        const uint32_t k = (uint32_t)__shfl((int)kbase, nj) + (uint32_t)p;
-        nk = p < total ? k : 0u; // past the last pair: entry 0, a valid address
-        nA = ldf4(sc.isect_a + nk);
+        const uint32_t k = (uint32_t)__shfl((int)kbase, ch.j) + (uint32_t)p;
+        ch.k = p < total ? k : 0u; // past the last pair: entry 0, a valid address
+        ch.A = ldf4(sc.isect_a + ch.k);
     };
-    if (total > 0) setup(0);
-    for (int base = 0; base < total; base += 64) {
+    // plane test of a chunk and append of its candidates
+    auto test = [&](int base, const Chunk &ch) {
         if (COUNT && lane == 0) c.v[RT_CNT_CHUNKS]++;
-        const int j = nj;
-        const uint32_t k = nk;
-        const RtF4 A = nA;
+        const int j = ch.j;
+        const RtF4 A = ch.A;
         const bool valid = base + lane < total;
-        if (base + 64 < total) setup(base + 64);
         const Vec3D oo = rt_v3(__shfl(r.o.x, j), __shfl(r.o.y, j), __shfl(r.o.z, j));
         const Vec3D dd = rt_v3(__shfl(r.d.x, j), __shfl(r.d.y, j), __shfl(r.d.z, j));
         const float ex = __shfl(r.exit_, j);
@@ -304,12 +325,57 @@ __device__ __forceinline__ bool coop_leaves(const RtDevScene &sc, CoopRay &r, ST
         const int below = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)pm, 0u));
         const int npm = __popcll(pm);
         const int slot = list_n + (cand ? below : npm + lane - below);
-        list[slot] = CoopCand{(k << 6) | (uint32_t)j, __float_as_uint(num), __float_as_uint(dn)};
+        list[slot] = CoopCand{(ch.k << 6) | (uint32_t)j, __float_as_uint(num), __float_as_uint(dn)};
         if (COUNT && cand) c.v[RT_CNT_CAND]++;
         list_n += npm;
-        if (list_n >= 64) bary_stage();
+        tick(RT_CNT_T_LEAF_TEST);
+        if (list_n >= 64) {
+            bary_stage();
+            tick(RT_CNT_T_LEAF_BARY);
+        }
+    };
+    // Software pipeline, unrolled twice over two chunk register sets: chunk
+    // c + 1's owner scan, entry and plane load are issued before chunk c's
+    // test, and each set is reloaded only after its test, so the loaded
+    // planes never have to be moved between registers (a loop-carried copy
+    // would wait for the load at the end of every iteration and undo the
+    // pipelining).
+    // The set-ups run unconditionally (a chunk past the end owns entry 0 of
+    // lane `carry`: a valid address, never tested): a conditional set-up
+    // would merge its registers with the old ones at the join, i.e. copy
+    // them, and wait for the load right there.
+    tick(-1);
+#if !WF_CHUNK_UNROLL
+    // (A/B reference: one register set, the loaded planes copied into the
+    // next iteration's set at the loop's end)
+    if (total > 0) {
+        Chunk cur, nxt;
+        setup(0, nxt);
+        for (int base = 0; base < total; base += 64) {
+            cur = nxt;
+            if (base + 64 < total) setup(base + 64, nxt);
+            test(base, cur);
+        }
     }
+#else
+    if (total > 0) {
+        Chunk c0, c1;
+        setup(0, c0);
+        tick(RT_CNT_T_LEAF_SETUP);
+        for (int base = 0;; base += 128) {
+            setup(base + 64, c1);
+            tick(RT_CNT_T_LEAF_SETUP);
+            test(base, c0);
+            if (base + 64 >= total) break;
+            setup(base + 128, c0);
+            tick(RT_CNT_T_LEAF_SETUP);
+            test(base + 64, c1);
+            if (base + 128 >= total) break;
+        }
+    }
+#endif
     if (list_n > 0) bary_stage();
+    tick(RT_CNT_T_LEAF_BARY);
     // ---- per-lane result: winner, or pop, or miss
     const unsigned long long key = vkey[lane];
     bool done = false;
@@ -326,6 +392,7 @@ __device__ __forceinline__ bool coop_leaves(const RtDevScene &sc, CoopRay &r, ST
             r.live = false;
             done = true;
         } else {
+            if (COUNT && r.sp - 1 >= WF_LDS_STACK) c.v[RT_CNT_SPILL_POP]++;
             coop_pop(r, stk);
         }
     }
@@ -346,8 +413,13 @@ __device__ __forceinline__ bool coop_round(const RtDevScene &sc, CoopRay &r, STK
     if (r.live && !r.pend) done = coop_descend<COUNT>(sc, r, stk, cap, c);
     const unsigned long long pm = __ballot(r.pend), lm = __ballot(r.live);
     const unsigned long long t1 = COUNT ? __builtin_amdgcn_s_memtime() : 0ull;
-    if (pm && (__popcll(pm) >= postpone || pm == lm))
+    if (pm && (__popcll(pm) >= postpone || pm == lm)) {
+        if (COUNT && __lane_id() == 0) {
+            c.v[RT_CNT_PEND_LANES] += (unsigned long long)__popcll(pm);
+            c.v[RT_CNT_LEAF_TESTS]++;
+        }
         if (coop_leaves<COUNT>(sc, r, stk, w, tri, hbx, hby, hbz, c)) done = true;
+    }
     if (COUNT && __lane_id() == 0) {
         const unsigned long long t2 = __builtin_amdgcn_s_memtime();
         c.v[RT_CNT_T_DESCEND] += t1 - t0;

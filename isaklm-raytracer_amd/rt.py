@@ -92,13 +92,15 @@ def deviation_stats(reset=False):
             "deep_paths": d.deep_paths, "deep_hist": [int(v) for v in d.deep_hist]}
 
 
-ABI_VERSION = 3  # RT_ABI_VERSION of include/isaklm_rt.h
+ABI_VERSION = 4  # RT_ABI_VERSION of include/isaklm_rt.h
 TRIANGLE_BYTES = 152
 NODE_BYTES = 20
 COUNTER_NAMES = ["node", "tri", "hit", "texel", "nee", "sample", "skip", "ray", "watchdog", "maxdepth"]
 FINISH_COUNTER_NAMES = ["finish_node", "finish_tri", "finish_ray", "cand", "plane", "deep_push", "t_descend", "t_leaves",
-                        "t_fetch", "rounds", "chunks", "bary", "wide_calls", "wide_rounds", "t_wide", "t_wide_load", "t_wide_leaf", "t_wide_expand"]
-N_COUNTERS = 32
+                        "t_fetch", "rounds", "chunks", "bary", "wide_calls", "wide_rounds", "t_wide", "t_wide_load", "t_wide_leaf", "t_wide_expand",
+                       "t_leaf_wait", "t_leaf_setup", "t_leaf_test", "t_leaf_bary", "spill_push", "spill_pop",
+                        "pend_lanes", "leaf_tests", "t_desc_wait"]
+N_COUNTERS = 40
 
 _lib = None
 

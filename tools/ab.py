@@ -73,7 +73,10 @@ def main():
                   "shade_ms": [round(p["shade_ms"]) for p in profs[v]],
                   "finish_ms": [round(p["finish_ms"]) for p in profs[v]],
                   "iterations": [p["iterations"] for p in profs[v]],
-                  "per_sample": {k: round(c[k] / max(c["sample"], 1), 2) for k in ("ray", "node", "tri", "cand", "plane", "rounds", "chunks", "bary")},
+                  "per_sample": {k: round(c[k] / max(c["sample"], 1), 2) for k in ("ray", "node", "tri", "cand", "plane", "rounds", "chunks", "bary", "t_descend", "t_leaves", "t_fetch", "finish_node", "finish_tri", "finish_ray",
+                                                                                          "t_leaf_wait", "t_leaf_setup", "t_leaf_test", "t_leaf_bary",
+                                                                                          "spill_push", "spill_pop", "pend_lanes", "leaf_tests",
+                                                                                          "t_desc_wait")},
                   "wide": {"calls": c["wide_calls"], "rounds_per_call": round(c["wide_rounds"] / max(c["wide_calls"], 1), 2),
                            "clk_per_call": round(c["t_wide"] / max(c["wide_calls"], 1)),
                            "clk_per_round": {k: round(c[k] / max(c["wide_rounds"], 1))
