@@ -51,10 +51,10 @@ extern "C" {
 /* ABI version: 3 = rt_scene_prepare(const Scene *, rt_scene_t *) without
  * counts (the counted form is rt_scene_prepare_counts), RtDeviations and
  * rt_deviation_stats, rt_abi_version; 4 = RT_CNT_COUNT 40 (the optional
- * counters buffer grew).  An integrator checks
+ * counters buffer grew); 5 = RtOptions.traversal.  An integrator checks
  * rt_abi_version() == RT_ABI_VERSION at start-up: a binary built against an
  * older header would otherwise link (C linkage) and mis-pass arguments. */
-#define RT_ABI_VERSION 4
+#define RT_ABI_VERSION 5
 
 /* CUDA uchar4, used for texels (rt/scene.cuh:18) */
 typedef struct RtUChar4 { uint8_t x, y, z, w; } RtUChar4;
@@ -419,7 +419,17 @@ typedef struct RtOptions {
      * running beside the pipelines, which finishes it one ray per wave with
      * all 64 lanes (0 = default 64, < 0 = off) */
     int wf_long_depth;
+    /* ray queries (identical results either way): RT_TRAVERSAL_BOUNDED
+     * (default) first finds a lower bound of the ray's first hit distance in
+     * a conservative BVH built by rt_scene_prepare and skips the KD subtrees
+     * the reference would test for nothing; RT_TRAVERSAL_KD runs the KD
+     * traversal alone.  Calls with counters_device always run the KD
+     * traversal (its counters are the reference's) */
+    int traversal;
 } RtOptions;
+
+#define RT_TRAVERSAL_BOUNDED 0
+#define RT_TRAVERSAL_KD 1
 
 /* Per-call kernel timing of the last rt_render on this device with
  * RtOptions.profile = 1 (wavefront kernels; HIP events on the call's stream,

@@ -21,7 +21,7 @@ INCLUDE = os.path.join(ROOT, "include")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
 HOST_SOURCES = ["host/mesh_loading.cpp", "host/kd_build.cpp", "host/scene_prepare.cpp", "host/misc.cpp", "host/image_decode.cpp",
-                "host/scenes.cpp"]
+                "host/scenes.cpp", "host/bvh_build.cpp"]
 HIP_SOURCES = ["path_kernel.hip", "wavefront.hip", "abi.hip", "shards.hip"]
 # every header under csrc/ (a header missing here would not trigger a rebuild)
 HEADERS = sorted(os.path.relpath(f, os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc"))

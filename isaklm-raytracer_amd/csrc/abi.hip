@@ -22,7 +22,7 @@ int rt_launch_path(const RtDevScene &sc, const RtDevFrame &fr, const RtDevCamera
 int rt_launch_tonemap(const Vec3D *fb, const int *count, RtUChar4 *out, int n, hipStream_t stream);
 int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevCamera &cam, hipStream_t stream,
                         int variant, int tail, int finish_waves, int profile, int cap, int postpone, int wide,
-                        int pipes, int long_depth);
+                        int pipes, int long_depth, int traversal);
 
 int rt_wavefront_device_init();
 
@@ -96,6 +96,16 @@ int upload_prepared(const rt_host::PreparedHost &h, int ntris, int nindices, rt_
         return rc;
     }
     RtDevScene &dv = s->dev;
+    dv.bvh_nodes = nullptr;
+    dv.bvh_a = nullptr;
+    dv.bvh_bary = nullptr;
+    dv.bvh_scale = h.bvh_scale;
+    if (h.bvh_depth >= 0 && ((rc = upload_vec(*s, h.bvh_nodes, &dv.bvh_nodes)) ||
+                             (rc = upload_vec(*s, h.bvh_a, &dv.bvh_a)) ||
+                             (rc = upload_vec(*s, h.bvh_bary, &dv.bvh_bary)))) {
+        release(s);
+        return rc;
+    }
     dv.nodes = nodes;
     dv.isect_a = a;
     dv.isect_bary = bary;
@@ -697,7 +707,8 @@ int rt_render(rt_scene_t scene, G_Buffer g, Camera cam, int sample_count, const 
     if (o.kernel >= RT_KERNEL_WAVEFRONT && o.kernel <= 3) {
         if (scene->max_depth > RT_STACK_DEPTH ||
             rt_launch_wavefront(scene->dev, fr, dc, stream, o.kernel, o.wf_tail, o.wf_finish_waves, o.profile,
-                                o.wf_descent_cap, o.wf_postpone, o.wf_wide, o.wf_pipelines, o.wf_long_depth) != 0) {
+                                o.wf_descent_cap, o.wf_postpone, o.wf_wide, o.wf_pipelines, o.wf_long_depth,
+                                o.traversal) != 0) {
             rt_set_error("rt_render: wavefront launch failed: %s", hipGetErrorString(hipGetLastError()));
             return RT_E_HIP;
         }

@@ -1,0 +1,55 @@
+// bvh_common.h — arithmetic shared by the BVH-bounded traversal
+// (bvh_trace.h, device), its builder (host/bvh_build.*) and the margin
+// stress test (tests/native/bvh_margin_check.cpp), so that all three run
+// exactly the same float operations (-ffp-contract=off everywhere).
+#pragma once
+#include "rt_device.h"
+#include "rt_vecmath.h"
+
+// Per-ray part of the conservative margin (host/bvh_build.h): the origin's
+// share of a passing test's plane-distance error, the rounding of o + d*s
+// and of the slab test; `scale` = the scene's largest |vertex|_1.
+RT_HD float rt_ray_margin(float ox, float oy, float oz, float scale)
+{
+    return 0x1p-16f * (fabsf(ox) + fabsf(oy) + fabsf(oz) + 2.0f * scale);
+}
+
+// Slab test of a box grown by the ray's margin: om = o + margin, op = o -
+// margin, inv = 1 / d.  True when the ray's [0, best] may meet the box.  An
+// axis-parallel ray (inv = inf) whose origin lies exactly on a grown face
+// makes a NaN there; culling or not is then both correct (no hit point can
+// lie on a grown face: the margins are generous).
+RT_HD bool rt_bvh_box(float lx, float ly, float lz, float hx, float hy, float hz, Vec3D om, Vec3D op, Vec3D inv,
+                      float best, float &tn)
+{
+    const float ax = (lx - om.x) * inv.x, bx = (hx - op.x) * inv.x;
+    const float ay = (ly - om.y) * inv.y, by = (hy - op.y) * inv.y;
+    const float az = (lz - om.z) * inv.z, bz = (hz - op.z) * inv.z;
+    tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+    const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+    return tn <= tf && tf >= 0.0f && tn <= best;
+}
+
+// intersect_triangle's plane part (rt/trace_ray.cuh:73-96) on the
+// precomputed plane A = {n, dot(n, p1)}: s, and whether the test goes on
+// (dn != 0, s >= 1e-5, s < closest)
+RT_HD bool rt_tri_plane(RtF4 A, Vec3D o, Vec3D d, float closest, float &s)
+{
+    const float dn = d.x * A.x + d.y * A.y + d.z * A.z;
+    s = (A.w - (o.x * A.x + o.y * A.y + o.z * A.z)) / dn;
+    return dn != 0 && s >= 0.00001f && s < closest;
+}
+
+// calculate_barycentric_coordinates + the range test (rt/trace_ray.cuh:48-71,
+// :97-110) on the precomputed record {p1, d00}, {v0, d01}, {v1, d11}, 1/den
+RT_HD bool rt_tri_bary(RtF4 B, RtF4 C, RtF4 D, float rd, Vec3D o, Vec3D d, float s, float &cx, float &cy, float &cz)
+{
+    const float px = o.x + d.x * s, py = o.y + d.y * s, pz = o.z + d.z * s;
+    const float v2x = px - B.x, v2y = py - B.y, v2z = pz - B.z;
+    const float d20 = v2x * C.x + v2y * C.y + v2z * C.z;
+    const float d21 = v2x * D.x + v2y * D.y + v2z * D.z;
+    cy = (D.w * d20 - C.w * d21) * rd;
+    cz = (B.w * d21 - C.w * d20) * rd;
+    cx = 1.0f - cy - cz;
+    return cx >= 0.0f && cx <= 1.0f && cy >= 0.0f && cy <= 1.0f && cz >= 0.0f && cz <= 1.0f;
+}

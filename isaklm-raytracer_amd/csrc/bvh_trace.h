@@ -1,0 +1,166 @@
+// bvh_trace.h — trace_ray (rt/trace_ray.cuh:244-318) bounded by the
+// conservative BVH (host/bvh_build.h): same result, bit for bit, with a
+// fraction of the KD traversal's work.
+//
+//  1. the reference's scene-box test gives [entry, exit] (no box: miss);
+//  2. the BVH query computes s_min = the smallest s of any triangle test
+//     that passes with s < exit, with the reference's own per-triangle
+//     arithmetic (intersect_triangle + barycentrics, rt/trace_ray.cuh:48-113);
+//     the BVH's boxes are grown so that no passing test is culled.  None:
+//     every leaf test of the reference fails too (a hit needs s < the leaf's
+//     exit <= the root's exit) — a miss;
+//  3. the reference's KD traversal, unchanged (split distance, near / far
+//     order, the implied-exit stack), except that a split crossing at
+//     t <= s_min goes straight to the far side with entry = t: every leaf
+//     under the near side has exit <= t <= s_min, and a test there can only
+//     pass with s >= s_min >= exit — the reference finds nothing in it and
+//     continues at the far side with exactly that entry.  Leaves with exit
+//     <= s_min are skipped for the same reason; the others get the
+//     reference's leaf test (closest starts at the leaf's exit, strict <,
+//     first wins).
+// Any lower bound of the smallest passing s would do (a smaller one only
+// skips less), so the query may cull with any best-so-far it has proven.
+#pragma once
+#include "bvh_common.h"
+#include "rt_kernels.h"
+
+namespace rtk {
+
+// one triangle test of intersect_triangle + calculate_barycentric_coordinates
+// (rt/trace_ray.cuh:48-113) on precomputed records: the same operations as
+// trace()'s leaf loop; true and s when it passes with s < closest
+__device__ __forceinline__ bool tri_test(const RtF4 *plane, const RtIsectBary *bary, uint32_t e, Vec3D o, Vec3D d,
+                                         float closest, float &s, float &cx, float &cy, float &cz)
+{
+    if (!rt_tri_plane(ldf4(plane + e), o, d, closest, s)) return false;
+    return rt_tri_bary(ldf4(&bary[e].b), ldf4(&bary[e].c), ldf4(&bary[e].d), as_float(bary[e].rd), o, d, s, cx, cy,
+                       cz);
+}
+
+// s_min of step 2: the smallest s < best of any passing test (best if none)
+template <typename STACK>
+__device__ __forceinline__ float bvh_bound(const RtDevScene &sc, Vec3D o, Vec3D d, float best, STACK &stk)
+{
+    const float m = rt_ray_margin(o.x, o.y, o.z, sc.bvh_scale);
+    const Vec3D om = rt_v3(o.x + m, o.y + m, o.z + m), op = rt_v3(o.x - m, o.y - m, o.z - m);
+    const Vec3D inv = rt_v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    int sp = 0;
+    uint32_t cur = 0; // the root (always an inner node)
+    while (true) {
+        if (!(cur & RT_BVH_LEAF)) {
+            const RtF4 *nd = sc.bvh_nodes + 4 * (size_t)cur;
+            const RtF4 a = ldf4(nd), b = ldf4(nd + 1), c = ldf4(nd + 2);
+            const uint2 ch = *reinterpret_cast<const uint2 *>(nd + 3);
+            float tn0, tn1;
+            const bool h0 = rt_bvh_box(a.x, a.y, a.z, a.w, b.x, b.y, om, op, inv, best, tn0) && ch.x != RT_BVH_EMPTY;
+            const bool h1 = rt_bvh_box(b.z, b.w, c.x, c.y, c.z, c.w, om, op, inv, best, tn1) && ch.y != RT_BVH_EMPTY;
+            if (h0 && h1) {
+                const bool second_first = tn1 < tn0;
+                stk.put(sp, second_first ? ch.x : ch.y, second_first ? tn0 : tn1);
+                ++sp;
+                cur = second_first ? ch.y : ch.x;
+                continue;
+            }
+            if (h0 || h1) {
+                cur = h0 ? ch.x : ch.y;
+                continue;
+            }
+        } else {
+            const uint32_t first = (cur & ~RT_BVH_LEAF) >> 3, end = first + (cur & 7u) + 1u;
+            for (uint32_t e = first; e < end; ++e) {
+                float s, cx, cy, cz;
+                if (tri_test(sc.bvh_a, sc.bvh_bary, e, o, d, best, s, cx, cy, cz)) best = s;
+            }
+        }
+        // pop the next subtree that may still hold a smaller s
+        bool more = false;
+        while (sp > 0) {
+            --sp;
+            uint32_t n;
+            float tn;
+            stk.get(sp, n, tn);
+            if (tn <= best) {
+                cur = n;
+                more = true;
+                break;
+            }
+        }
+        if (!more) return best;
+    }
+}
+
+// trace_ray with the bound: returns the triangle index or -1 and the hit's
+// barycentric coordinates, bit-identical to trace()
+template <typename STACK>
+__device__ __forceinline__ int trace_bvh(const RtDevScene &sc, const Vec3D o, const Vec3D d, float &hbx, float &hby,
+                                         float &hbz, STACK &stk)
+{
+    float entry, exit_;
+    if (!bbox_hit(sc, o, d, entry, exit_)) return -1;
+    const float root_exit = exit_;
+    const float s_min = bvh_bound(sc, o, d, exit_, stk);
+    if (!(s_min < root_exit)) return -1;
+    const float yx = rt_recip_guard(d.x), yy = rt_recip_guard(d.y), yz = rt_recip_guard(d.z);
+    int sp = 0;
+    uint32_t node = 0;
+    while (true) {
+        uint2 nd = *reinterpret_cast<const uint2 *>(sc.nodes + 2 * (size_t)node);
+        while ((nd.y & 3u) != RT_LEAF_TAG) {
+            const uint32_t axis = nd.y & 3u;
+            const float split = as_float(nd.x);
+            const float oax = axis == 0 ? o.x : (axis == 1 ? o.y : o.z);
+            const float dax = axis == 0 ? d.x : (axis == 1 ? d.y : d.z);
+            const float yax = axis == 0 ? yx : (axis == 1 ? yy : yz);
+            uint32_t near_c = node + 1, far_c = nd.y >> 2;
+            if (oax >= split) { // ray_behind_plane (:174-188)
+                near_c = nd.y >> 2;
+                far_c = node + 1;
+            }
+            const float t = rt_div_by(split - oax, dax, yax); // intersect_plane (:190-210)
+            if (t >= exit_ || t < 0) {
+                node = near_c;
+            } else if (t <= entry) {
+                node = far_c;
+            } else if (t <= s_min) { // the near side holds no hit: its leaves' exits are <= t
+                node = far_c;
+                entry = t;
+            } else {
+                stk.put(sp, far_c, t);
+                ++sp;
+                node = near_c;
+                exit_ = t;
+            }
+            nd = *reinterpret_cast<const uint2 *>(sc.nodes + 2 * (size_t)node);
+        }
+        const uint32_t count = nd.y >> 2;
+        if (count > 0 && exit_ > s_min) {
+            // trace_leaf_node (:115-172): closest starts at the leaf's exit
+            float smallest = exit_;
+            int best = -1;
+            float bx = 0.0f, by = 0.0f, bz = 0.0f;
+            for (uint32_t e = nd.x; e < nd.x + count; ++e) {
+                float s, cx, cy, cz;
+                if (tri_test(sc.isect_a, sc.isect_bary, e, o, d, smallest, s, cx, cy, cz)) {
+                    smallest = s;
+                    best = (int)sc.isect_bary[e].tri;
+                    bx = cx;
+                    by = cy;
+                    bz = cz;
+                }
+            }
+            if (best >= 0) {
+                hbx = bx;
+                hby = by;
+                hbz = bz;
+                return best;
+            }
+        }
+        if (sp == 0) return -1;
+        --sp;
+        node = stk.node_at(sp);
+        entry = stk.entry_at(sp);
+        exit_ = sp > 0 ? stk.entry_at(sp - 1) : root_exit;
+    }
+}
+
+} // namespace rtk

@@ -56,6 +56,13 @@ struct PreparedHost {
     int light_count = 0;
     int max_depth = 0;
     Bounding_Box bounds;
+    // the conservative BVH that bounds each ray's first hit (bvh_build.h);
+    // bvh_depth < 0: not built (the KD-only traversal runs)
+    std::vector<RtF4> bvh_nodes;          // 4 per node
+    std::vector<RtF4> bvh_a;              // BVH leaf-slot order
+    std::vector<RtIsectBary> bvh_bary;    // BVH leaf-slot order
+    float bvh_scale = 0.0f;
+    int bvh_depth = -1, bvh_always = 0, bvh_dropped = 0;
 };
 int prepare_host(const Triangle *tris, int ntris, const KD_Tree_Node *nodes, int nnodes, const int *indices,
                  int nindices, const int *lights, int nlights, Bounding_Box bounds, PreparedHost &out);

@@ -7,12 +7,16 @@
 // renumbered into pre-order with child1 == node + 1, which is the identity
 // for trees from create_kd_tree (rt/create_kd_tree.cuh:225-258) and keeps
 // traversal order for any other tree.
+#include <omp.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <map>
 #include <string>
 #include <vector>
 
+#include "bvh_build.h"
 #include "rt_host.h"
 
 namespace rt_host {
@@ -128,8 +132,8 @@ int prepare_host(const Triangle *tris, int ntris, const KD_Tree_Node *nodes, int
     }
 
     // --- intersection constants (rt/trace_ray.cuh:48-113), per triangle ---
-    std::vector<RtF4> ta((size_t)ntris), tb((size_t)ntris), tc((size_t)ntris), td((size_t)ntris);
-    std::vector<float> tr((size_t)ntris);
+    std::vector<RtF4> ta((size_t)ntris);
+    std::vector<RtIsectBary> tbary((size_t)ntris);
     out.shade.resize(7 * (size_t)ntris);
 #pragma omp parallel for schedule(static)
     for (int i = 0; i < ntris; ++i) {
@@ -141,10 +145,13 @@ int prepare_host(const Triangle *tris, int ntris, const KD_Tree_Node *nodes, int
         float d00 = rt_dot(v0, v0), d01 = rt_dot(v0, v1), d11 = rt_dot(v1, v1);
         float rd = 1.0f / (d00 * d11 - d01 * d01);
         ta[i] = f4(n.x, n.y, n.z, d);
-        tb[i] = f4(t.p1.x, t.p1.y, t.p1.z, d00);
-        tc[i] = f4(v0.x, v0.y, v0.z, d01);
-        td[i] = f4(v1.x, v1.y, v1.z, d11);
-        tr[i] = rd;
+        RtIsectBary &r = tbary[i];
+        r.b = f4(t.p1.x, t.p1.y, t.p1.z, d00);
+        r.c = f4(v0.x, v0.y, v0.z, d01);
+        r.d = f4(v1.x, v1.y, v1.z, d11);
+        r.rd = fbits(rd);
+        r.tri = (uint32_t)i;
+        r.pad[0] = r.pad[1] = 0;
         RtF4 *s = &out.shade[7 * (size_t)i];
         s[0] = f4(t.p1.x, t.p1.y, t.p1.z, bitsf((uint32_t)tri_mat[i]));
         s[1] = f4(t.p2.x, t.p2.y, t.p2.z, t.uv1.x);
@@ -162,13 +169,32 @@ int prepare_host(const Triangle *tris, int ntris, const KD_Tree_Node *nodes, int
     for (long long e = 0; e < (long long)ne; ++e) {
         const int t = indices[e];
         out.isect_a[e] = ta[t];
-        RtIsectBary &r = out.isect_bary[e];
-        r.b = tb[t];
-        r.c = tc[t];
-        r.d = td[t];
-        r.rd = fbits(tr[t]);
-        r.tri = (uint32_t)t;
-        r.pad[0] = r.pad[1] = 0;
+        out.isect_bary[e] = tbary[t];
+    }
+
+    // --- the conservative BVH (bvh_build.h), records in its leaf order ----
+    BvhHost bvh;
+    out.bvh_depth = -1;
+    const double t0 = omp_get_wtime();
+    const int brc = build_bvh(tris, ntris, ta.data(), tbary.data(), bvh);
+    if (getenv("RT_BVH_STATS"))
+        fprintf(stderr, "[bvh] rc %d tris %d nodes %zu depth %d always %d dropped %d scale %g build %.3f s\n", brc,
+                ntris, bvh.nodes.size() / 4, bvh.depth, bvh.always, bvh.dropped, bvh.scale, omp_get_wtime() - t0);
+    if (brc == RT_OK && bvh.depth < RT_BVH_STACK) {
+        out.bvh_nodes = std::move(bvh.nodes);
+        out.bvh_a.resize(bvh.order.size());
+        out.bvh_bary.resize(bvh.order.size());
+#pragma omp parallel for schedule(static)
+        for (long long k = 0; k < (long long)bvh.order.size(); ++k) {
+            out.bvh_a[k] = ta[bvh.order[k]];
+            out.bvh_bary[k] = tbary[bvh.order[k]];
+        }
+        out.bvh_scale = bvh.scale;
+        out.bvh_depth = bvh.depth;
+        out.bvh_always = bvh.always;
+        out.bvh_dropped = bvh.dropped;
+    } else if (brc != RT_OK && brc != RT_E_UNSUPPORTED) {
+        return brc;
     }
 
     // --- lights: one padding entry for the xi == 1.0 draw -----

@@ -88,7 +88,20 @@ struct RtDevScene {
     int triangle_count;
     int index_count;            // KD leaf entries
     float bmin[3], bmax[3];
+    // conservative BVH bounding each ray's first hit (host/bvh_build.h,
+    // bvh_trace.h); bvh_nodes == nullptr: none (KD-only traversal)
+    const RtF4 *bvh_nodes;      // 4 per node: child boxes {lo0, hi0.x}, {hi0.yz, lo1.xy}, {lo1.z, hi1}, {ref0, ref1, -, -}
+    const RtF4 *bvh_a;          // per BVH leaf slot: plane (as isect_a)
+    const RtIsectBary *bvh_bary; // per BVH leaf slot: barycentric-test record (as isect_bary)
+    float bvh_scale;            // largest |vertex|_1 (rt_ray_margin)
 };
+
+// BVH child reference: an inner node's index, or RT_BVH_LEAF | first << 3 |
+// (count - 1) for the leaf of slots [first, first + count), or RT_BVH_EMPTY
+#define RT_BVH_LEAF 0x80000000u
+#define RT_BVH_EMPTY 0xFFFFFFFFu
+#define RT_BVH_LEAF_MAX 8
+#define RT_BVH_STACK 64 // traversal stack entries: trees deeper than this are not used
 
 struct RtDevCamera {            // Camera precomputed once per call (same ops as the reference)
     float R[9];                 // rotation_matrix(yaw, pitch): i, j, k

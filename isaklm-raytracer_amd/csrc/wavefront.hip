@@ -25,6 +25,7 @@
 #include <thread>
 #include <vector>
 
+#include "bvh_trace.h"
 #include "rt_kernels.h"
 
 using namespace rtk;
@@ -70,6 +71,16 @@ static_assert(WF_BLOCK % WF_TBLOCK == 0 && WF_TBLOCK % 64 == 0, "WF_TBLOCK must 
 #ifndef WF_TRACE_WAVES
 #define WF_TRACE_WAVES 6 // wf_trace_coop occupancy target (blocks of 4 waves per CU = waves per SIMD)
 #endif
+#ifndef WF_BVH_LDS
+#define WF_BVH_LDS 12   // wf_trace_bvh: stack entries in LDS (BVH query and KD descent share the stack)
+#endif
+#ifndef WF_BVH_WAVES
+#define WF_BVH_WAVES 6  // wf_trace_bvh occupancy target
+#endif
+// per-thread spill entries: the deeper of the KD stack (past WF_LDS_STACK) and the BVH stack (past WF_BVH_LDS)
+#define WF_SPILL_ENTRIES \
+    ((RT_STACK_DEPTH - WF_LDS_STACK) > (RT_BVH_STACK - WF_BVH_LDS) ? (RT_STACK_DEPTH - WF_LDS_STACK) \
+                                                                    : (RT_BVH_STACK - WF_BVH_LDS))
 #define WF_TAIL_DEFAULT 65536u       // RtOptions.wf_tail
 #define WF_FINISH_WAVES_DEFAULT 2048u // RtOptions.wf_finish_waves
 #define WF_FINISH_WAVES_SMALL 512u    // ... for trees below WF_FIN_WIDE_MIN_ENTRIES leaf entries
@@ -252,6 +263,35 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_trace(RtDevScene sc, WfState st, 
         }
     }
     if (COUNT) flush_counters(c, counters);
+}
+
+// trace_ray bounded by the conservative BVH (bvh_trace.h): one ray per lane,
+// lanes refill from the queue (one wave-aggregated atomic per refill round)
+// so a wave is not held by its slowest ray's successors
+__global__ void __launch_bounds__(WF_BLOCK, WF_BVH_WAVES) wf_trace_bvh(RtDevScene sc, WfState st, int q)
+{
+    __shared__ uint32_t s_node[WF_BVH_LDS * WF_BLOCK];
+    __shared__ float s_entry[WF_BVH_LDS * WF_BLOCK];
+    const int tid = threadIdx.x;
+    const int gtid = blockIdx.x * WF_BLOCK + tid;
+    Stack<WF_BVH_LDS> stk{s_node + tid, s_entry + tid, WF_BLOCK, st.spill + gtid, st.spill_threads};
+    const uint32_t n = st.counts[q];
+    const RtF4 *rays = st.q_ray[q];
+    uint32_t *fetch = st.counts + 2 + q;
+    const int lane = __lane_id();
+    while (true) {
+        const unsigned long long m = __ballot(true);
+        const int leader = __ffsll((long long)m) - 1;
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(fetch, (uint32_t)__popcll(m));
+        base = __shfl(base, leader);
+        const uint32_t e = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        if (e >= n) break;
+        const RtF4 o4 = ldf4(rays + 2 * (size_t)e), d4 = ldf4(rays + 2 * (size_t)e + 1);
+        float bx = 0.0f, by = 0.0f, bz = 0.0f;
+        const int hit = trace_bvh(sc, ld3(o4), ld3(d4), bx, by, bz, stk);
+        *reinterpret_cast<float4 *>(st.hits + e) = make_float4(__int_as_float(hit), bx, by, bz);
+    }
 }
 
 // Persistent trace with dynamic ray fetch: every lane runs rays one leaf at a
@@ -1108,7 +1148,7 @@ int ensure(Workspace &w, size_t slots, int grid, int npipes)
         o_qr1[i] = take(2 * slots * 32);
         o_h[i] = take(2 * slots * 16);
         o_cnt[i] = take(256);
-        o_sp[i] = take(spill_threads * 8 * (RT_STACK_DEPTH - WF_LDS_STACK));
+        o_sp[i] = take(spill_threads * 8 * WF_SPILL_ENTRIES);
     }
     if (hipMalloc(&w.blob, off) != hipSuccess) {
         w.blob = nullptr;
@@ -1175,7 +1215,7 @@ extern "C" int rt_last_profile(RtProfile *out)
 
 int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevCamera &cam, hipStream_t stream,
                         int variant, int tail_opt, int finish_waves_opt, int profile, int cap_opt, int postpone_opt,
-                        int wide_opt, int pipes_opt, int long_opt)
+                        int wide_opt, int pipes_opt, int long_opt, int traversal)
 {
     // 1: wave-cooperative leaves (entries packed as k << 6 | lane: needs < 2^26 entries), 2: static, 3: per-lane fetch
     int trace_kind = variant;
@@ -1202,6 +1242,8 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
     const size_t slots = (size_t)fr.width * fr.height;
     const bool count = fr.counters != nullptr;
     const bool prof = profile != 0;
+    // the queue trace launches run the BVH-bounded traversal (counting calls: the KD one, whose counters are the reference's)
+    const bool bounded = !count && traversal == RT_TRAVERSAL_BOUNDED && sc.bvh_nodes != nullptr;
     const int tiles = ((fr.width + 15) / 16) * ((fr.height + 15) / 16);
     int npipes = pipes_opt > 0 ? pipes_opt : WF_PIPES_DEFAULT;
     npipes = npipes > WF_MAX_PIPES ? WF_MAX_PIPES : npipes;
@@ -1344,7 +1386,9 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
                 if (hipMemsetAsync(st.counts + 6 + (q ^ 1), 0, 4, s) != hipSuccess) return -1; // next path list
                 if (hipMemsetAsync(st.counts + 2 + q, 0, 4, s) != hipSuccess) return -1; // fetch cursor
                 if (!mark(4)) return -1;
-                if (trace_kind == 1) {
+                if (bounded) {
+                    hipLaunchKernelGGL(wf_trace_bvh, dim3(grid), dim3(WF_BLOCK), 0, s, sc, st, q);
+                } else if (trace_kind == 1) {
                     const int li = it * npipes + pi;
                     unsigned long long *tl = fr.wave_times && li < WF_TIMELINE_LAUNCHES ? fr.wave_times + 3 * li : nullptr;
                     if (count)

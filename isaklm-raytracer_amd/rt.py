@@ -56,7 +56,7 @@ class RtOptions(ctypes.Structure):
                 ("wf_tail", ctypes.c_int), ("wf_finish_waves", ctypes.c_int), ("profile", ctypes.c_int),
                 ("wf_descent_cap", ctypes.c_int), ("wf_postpone", ctypes.c_int), ("wf_wide", ctypes.c_int),
                 ("shard_id", ctypes.c_int), ("num_shards", ctypes.c_int), ("wf_pipelines", ctypes.c_int),
-                ("wf_long_depth", ctypes.c_int)]
+                ("wf_long_depth", ctypes.c_int), ("traversal", ctypes.c_int)]
 
 
 class RtProfile(ctypes.Structure):
@@ -92,7 +92,7 @@ def deviation_stats(reset=False):
             "deep_paths": d.deep_paths, "deep_hist": [int(v) for v in d.deep_hist]}
 
 
-ABI_VERSION = 4  # RT_ABI_VERSION of include/isaklm_rt.h
+ABI_VERSION = 5  # RT_ABI_VERSION of include/isaklm_rt.h
 TRIANGLE_BYTES = 152
 NODE_BYTES = 20
 COUNTER_NAMES = ["node", "tri", "hit", "texel", "nee", "sample", "skip", "ray", "watchdog", "maxdepth"]
@@ -347,11 +347,16 @@ class GBuffer:
 
 KERNEL_MEGA = 0
 KERNEL_WAVEFRONT = 1
+TRAVERSAL_BOUNDED = 0
+TRAVERSAL_KD = 1
 
 
 def options(width, height, passes=1, adaptive=True, min_samples=100, tolerance=0.05, max_depth=0, stream=None,
             counters=None, kernel=KERNEL_MEGA, wf_tail=0, wf_finish_waves=0, profile=False, wf_descent_cap=0,
-            wf_postpone=0, wf_wide=0, shard_id=0, num_shards=1, wave_times=None, wf_pipelines=0, wf_long_depth=0):
+            wf_postpone=0, wf_wide=0, shard_id=0, num_shards=1, wave_times=None, wf_pipelines=0, wf_long_depth=0,
+            traversal=None):
+    """RtOptions; traversal: TRAVERSAL_BOUNDED / TRAVERSAL_KD (None: the
+    library default, or RT_TRAVERSAL from the environment)."""
     o = RtOptions()
     lib().rt_default_options(ctypes.byref(o))
     o.width, o.height, o.passes = width, height, passes
@@ -365,6 +370,10 @@ def options(width, height, passes=1, adaptive=True, min_samples=100, tolerance=0
     o.wave_times_device = wave_times
     o.wf_pipelines = wf_pipelines
     o.wf_long_depth = wf_long_depth
+    if traversal is None and os.environ.get("RT_TRAVERSAL"):
+        traversal = {"bounded": TRAVERSAL_BOUNDED, "kd": TRAVERSAL_KD}[os.environ["RT_TRAVERSAL"]]
+    if traversal is not None:
+        o.traversal = traversal
     return o
 
 

@@ -1,0 +1,304 @@
+// bvh_trace_check.cpp — host restatement of the BVH-bounded trace_ray
+// (csrc/bvh_trace.h) checked against the plain KD traversal (trace_ray,
+// rt/trace_ray.cuh:244-318, as csrc/rt_kernels.h trace()) on a real scene:
+// camera rays and bounce-like rays (from random points on the triangles, in
+// random directions, some grazing), every result compared bit for bit
+// (triangle, barycentrics).  Also reports the work per ray of both
+// traversals (nodes, triangle tests) — the reason for the bounded one.
+//
+// Links the library's host code (rt_host::*): the scene loader, the KD
+// build and prepare_host, i.e. the very arrays the GPU gets.
+//
+// Usage: bvh_trace_check scene.txt [rays] [seed]; exit 0 = all identical.
+#include <math.h>
+#include <omp.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <random>
+#include <vector>
+
+#include "host/bvh_build.h"
+#include "host/rt_host.h"
+
+namespace {
+
+float bitsf(uint32_t u)
+{
+    float f;
+    memcpy(&f, &u, 4);
+    return f;
+}
+
+struct Work {
+    long long nodes = 0, tests = 0, bvh_nodes = 0, bvh_tests = 0, leaves = 0;
+};
+
+struct Hit {
+    int tri = -1;
+    float b[3] = {0, 0, 0};
+};
+
+bool scene_box(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, float &t1, float &t2)
+{
+    const Bounding_Box &b = h.bounds;
+    float tminx = (b.min.x - o.x) / d.x, tminy = (b.min.y - o.y) / d.y, tminz = (b.min.z - o.z) / d.z;
+    float tmaxx = (b.max.x - o.x) / d.x, tmaxy = (b.max.y - o.y) / d.y, tmaxz = (b.max.z - o.z) / d.z;
+    t1 = fmaxf(fmaxf(fminf(tminx, tmaxx), fminf(tminy, tmaxy)), fminf(tminz, tmaxz));
+    t2 = fminf(fminf(fmaxf(tminx, tmaxx), fmaxf(tminy, tmaxy)), fmaxf(tminz, tmaxz));
+    return t1 <= t2;
+}
+
+bool test(const RtF4 *A, const RtIsectBary *R, uint32_t e, Vec3D o, Vec3D d, float closest, float &s, float *b)
+{
+    if (!rt_tri_plane(A[e], o, d, closest, s)) return false;
+    return rt_tri_bary(R[e].b, R[e].c, R[e].d, bitsf(R[e].rd), o, d, s, b[0], b[1], b[2]);
+}
+
+// the KD traversal with s_min = -inf is trace_ray itself; with the bound it
+// is bvh_trace.h's step 3
+Hit kd_trace(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, float entry, float exit_, float s_min, Work &w)
+{
+    Hit hit;
+    struct E { uint32_t node; float entry; };
+    E stk[64];
+    int sp = 0;
+    const float root_exit = exit_;
+    uint32_t node = 0;
+    while (true) {
+        uint32_t nx = h.nodes[2 * node], ny = h.nodes[2 * node + 1];
+        ++w.nodes;
+        while ((ny & 3u) != RT_LEAF_TAG) {
+            const uint32_t axis = ny & 3u;
+            const float split = bitsf(nx);
+            const float oax = axis == 0 ? o.x : (axis == 1 ? o.y : o.z);
+            const float dax = axis == 0 ? d.x : (axis == 1 ? d.y : d.z);
+            uint32_t near_c = node + 1, far_c = ny >> 2;
+            if (oax >= split) {
+                near_c = ny >> 2;
+                far_c = node + 1;
+            }
+            const float t = (split - oax) / dax;
+            if (t >= exit_ || t < 0) {
+                node = near_c;
+            } else if (t <= entry) {
+                node = far_c;
+            } else if (t <= s_min) {
+                node = far_c;
+                entry = t;
+            } else {
+                stk[sp++] = E{far_c, t};
+                node = near_c;
+                exit_ = t;
+            }
+            nx = h.nodes[2 * node];
+            ny = h.nodes[2 * node + 1];
+            ++w.nodes;
+        }
+        const uint32_t count = ny >> 2;
+        if (count > 0 && exit_ > s_min) {
+            ++w.leaves;
+            float smallest = exit_;
+            for (uint32_t e = nx; e < nx + count; ++e) {
+                float s, b[3];
+                ++w.tests;
+                if (test(h.isect_a.data(), h.isect_bary.data(), e, o, d, smallest, s, b)) {
+                    smallest = s;
+                    hit.tri = (int)h.isect_bary[e].tri;
+                    memcpy(hit.b, b, sizeof b);
+                }
+            }
+            if (hit.tri >= 0) return hit;
+        }
+        if (sp == 0) return hit;
+        --sp;
+        node = stk[sp].node;
+        entry = stk[sp].entry;
+        exit_ = sp > 0 ? stk[sp - 1].entry : root_exit;
+    }
+}
+
+float bvh_bound(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, float best, Work &w)
+{
+    const float m = rt_ray_margin(o.x, o.y, o.z, h.bvh_scale);
+    const Vec3D om = rt_v3(o.x + m, o.y + m, o.z + m), op = rt_v3(o.x - m, o.y - m, o.z - m);
+    const Vec3D inv = rt_v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    struct E { uint32_t ref; float tn; };
+    E stk[RT_BVH_STACK];
+    int sp = 0;
+    uint32_t cur = 0;
+    while (true) {
+        if (!(cur & RT_BVH_LEAF)) {
+            ++w.bvh_nodes;
+            const RtF4 *nd = &h.bvh_nodes[4 * (size_t)cur];
+            uint32_t c0, c1;
+            memcpy(&c0, &nd[3].x, 4);
+            memcpy(&c1, &nd[3].y, 4);
+            float tn0, tn1;
+            const bool h0 = rt_bvh_box(nd[0].x, nd[0].y, nd[0].z, nd[0].w, nd[1].x, nd[1].y, om, op, inv, best, tn0) &&
+                            c0 != RT_BVH_EMPTY;
+            const bool h1 = rt_bvh_box(nd[1].z, nd[1].w, nd[2].x, nd[2].y, nd[2].z, nd[2].w, om, op, inv, best, tn1) &&
+                            c1 != RT_BVH_EMPTY;
+            if (h0 && h1) {
+                const bool sf = tn1 < tn0;
+                stk[sp++] = E{sf ? c0 : c1, sf ? tn0 : tn1};
+                cur = sf ? c1 : c0;
+                continue;
+            }
+            if (h0 || h1) {
+                cur = h0 ? c0 : c1;
+                continue;
+            }
+        } else {
+            const uint32_t first = (cur & ~RT_BVH_LEAF) >> 3, end = first + (cur & 7u) + 1u;
+            for (uint32_t e = first; e < end; ++e) {
+                float s, b[3];
+                ++w.bvh_tests;
+                if (test(h.bvh_a.data(), h.bvh_bary.data(), e, o, d, best, s, b)) best = s;
+            }
+        }
+        bool more = false;
+        while (sp > 0) {
+            --sp;
+            if (stk[sp].tn <= best) {
+                cur = stk[sp].ref;
+                more = true;
+                break;
+            }
+        }
+        if (!more) return best;
+    }
+}
+
+Hit bounded_trace(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, Work &w)
+{
+    float t1, t2;
+    if (!scene_box(h, o, d, t1, t2)) return Hit{};
+    const float s_min = bvh_bound(h, o, d, t2, w);
+    if (!(s_min < t2)) return Hit{};
+    return kd_trace(h, o, d, t1, t2, s_min, w);
+}
+
+Hit plain_trace(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, Work &w)
+{
+    float t1, t2;
+    if (!scene_box(h, o, d, t1, t2)) return Hit{};
+    return kd_trace(h, o, d, t1, t2, -INFINITY, w);
+}
+
+} // namespace
+
+int main(int argc, char **argv)
+{
+    if (argc < 2) {
+        fprintf(stderr, "usage: %s scene.txt [rays] [seed]\n", argv[0]);
+        return 2;
+    }
+    const long long rays = argc > 2 ? atoll(argv[2]) : 200000;
+    std::mt19937_64 rng(argc > 3 ? strtoull(argv[3], nullptr, 10) : 7);
+    RtHostScene scene;
+    Camera cam;
+    if (rt_host::load_scene_file(scene, argv[1], &cam) != RT_OK) {
+        fprintf(stderr, "scene load failed\n");
+        return 2;
+    }
+    const int n = (int)scene.tris.size();
+    std::vector<KD_Tree_Node> nodes;
+    std::vector<int> indices;
+    Bounding_Box bounds;
+    if (rt_host::build_kd_tree(scene.tris.data(), n, nodes, indices, bounds) != RT_OK) return 2;
+    std::vector<int> lights = rt_host::light_list(scene.tris.data(), n);
+    rt_host::PreparedHost h;
+    if (rt_host::prepare_host(scene.tris.data(), n, nodes.data(), (int)nodes.size(), indices.data(),
+                              (int)indices.size(), lights.data(), (int)lights.size(), bounds, h) != RT_OK) {
+        fprintf(stderr, "prepare failed\n");
+        return 2;
+    }
+    if (h.bvh_depth < 0) {
+        fprintf(stderr, "no BVH built\n");
+        return 2;
+    }
+    printf("tris %d kd_nodes %zu bvh_nodes %zu bvh_depth %d always %d dropped %d\n", n, nodes.size(),
+           h.bvh_nodes.size() / 4, h.bvh_depth, h.bvh_always, h.bvh_dropped);
+    std::uniform_real_distribution<float> U(0.0f, 1.0f);
+    auto unit = [&]() {
+        while (true) {
+            Vec3D v = rt_v3(2 * U(rng) - 1, 2 * U(rng) - 1, 2 * U(rng) - 1);
+            float l = rt_dot(v, v);
+            if (l > 1e-6f && l <= 1.0f) return rt_normalize(v);
+        }
+    };
+    Work wp, wb;
+    long long mism = 0, hits = 0;
+#pragma omp parallel
+    {
+        Work lp, lb;
+        long long lm = 0, lh = 0;
+        std::mt19937_64 r2(rng() + 0x9e3779b97f4a7c15ull * (unsigned)omp_get_thread_num());
+        std::uniform_real_distribution<float> V(0.0f, 1.0f);
+        auto unit2 = [&]() {
+            while (true) {
+                Vec3D v = rt_v3(2 * V(r2) - 1, 2 * V(r2) - 1, 2 * V(r2) - 1);
+                float l = rt_dot(v, v);
+                if (l > 1e-6f && l <= 1.0f) return rt_normalize(v);
+            }
+        };
+#pragma omp for schedule(dynamic, 1024)
+        for (long long k = 0; k < rays; ++k) {
+            Vec3D o, d;
+            const int mode = (int)(k % 4);
+            if (mode == 0) { // from the camera
+                o = cam.position;
+                d = unit2();
+            } else { // from a point on a random triangle (a bounce), some grazing / axis-parallel
+                const Triangle &t = scene.tris[(size_t)(V(r2) * n) % n];
+                float b1 = V(r2), b2 = V(r2);
+                if (b1 + b2 > 1) {
+                    b1 = 1 - b1;
+                    b2 = 1 - b2;
+                }
+                o = t.p1 + b1 * (t.p2 - t.p1) + b2 * (t.p3 - t.p1);
+                d = unit2();
+                if (mode == 2) {
+                    Vec3D nn = rt_normalize(rt_cross(t.p2 - t.p1, t.p3 - t.p1));
+                    if (nn.x == nn.x) d = rt_normalize(d - rt_dot(d, nn) * nn + 1e-4f * (V(r2) - 0.5f) * nn);
+                } else if (mode == 3 && (k & 4)) {
+                    const int a = (int)(k >> 3) % 3;
+                    if (a == 0) d.x = 0; else if (a == 1) d.y = 0; else d.z = 0;
+                    d = rt_normalize(d);
+                }
+                if (d.x != d.x) continue;
+            }
+            const Hit a = plain_trace(h, o, d, lp), b = bounded_trace(h, o, d, lb);
+            if (a.tri >= 0) ++lh;
+            if (a.tri != b.tri || memcmp(a.b, b.b, sizeof a.b) != 0) {
+                if (++lm <= 5) {
+#pragma omp critical
+                    fprintf(stderr, "MISMATCH o (%a %a %a) d (%a %a %a): kd %d, bounded %d\n", o.x, o.y, o.z, d.x,
+                            d.y, d.z, a.tri, b.tri);
+                }
+            }
+        }
+#pragma omp critical
+        {
+            mism += lm;
+            hits += lh;
+            wp.nodes += lp.nodes;
+            wp.tests += lp.tests;
+            wp.leaves += lp.leaves;
+            wb.nodes += lb.nodes;
+            wb.tests += lb.tests;
+            wb.leaves += lb.leaves;
+            wb.bvh_nodes += lb.bvh_nodes;
+            wb.bvh_tests += lb.bvh_tests;
+        }
+    }
+    (void)unit;
+    const double R = (double)rays;
+    printf("rays %lld hits %lld mismatches %lld\n", rays, hits, mism);
+    printf("kd-only per ray: nodes %.1f leaves %.1f tests %.1f\n", wp.nodes / R, wp.leaves / R, wp.tests / R);
+    printf("bounded per ray: bvh nodes %.1f bvh tests %.1f kd nodes %.1f leaves %.2f tests %.1f\n", wb.bvh_nodes / R,
+           wb.bvh_tests / R, wb.nodes / R, wb.leaves / R, wb.tests / R);
+    return mism == 0 ? 0 : 1;
+}

@@ -33,18 +33,29 @@ def _camera(run, arr):
     return c
 
 
-def _render_both(run, osc, W, H, P, rng0, cam_arr, kernel, calls=1):
-    """GPU render with the G-buffer seeds rng0 and camera cam_arr against the
-    oracle on the same inputs; returns the oracle's hazard counts"""
+def _gpu(run, W, H, P, rng0, cam_arr, kernel, calls, cnt, traversal=None):
     n = W * H
     g = rt.GBuffer(W, H)
     g.upload(np.zeros((n, 3), np.float32), np.zeros(n, np.float32), np.zeros(n, np.int32), rng0)
-    cnt = rt.DeviceCounters()
     cam = _camera(run, cam_arr)
     for c in range(calls):
         rt.render(run.dev, g, cam, 0 if c == 0 else 1,
-                  rt.options(W, H, P, adaptive=False, counters=cnt.p, kernel=kernel))
-    gpu = g.download()
+                  rt.options(W, H, P, adaptive=False, counters=cnt.p if cnt else None, kernel=kernel,
+                             traversal=traversal))
+    return g.download()
+
+
+def _render_both(run, osc, W, H, P, rng0, cam_arr, kernel, calls=1):
+    """GPU render with the G-buffer seeds rng0 and camera cam_arr against the
+    oracle on the same inputs, three ways: the counting build (KD traversal,
+    counters compared too) and the product build with each traversal
+    (RT_TRAVERSAL_BOUNDED: the BVH-bounded one on the wavefront kernel);
+    returns the oracle's hazard counts"""
+    n = W * H
+    cnt = rt.DeviceCounters()
+    gpu = _gpu(run, W, H, P, rng0, cam_arr, kernel, calls, cnt)
+    products = [(t, _gpu(run, W, H, P, rng0, cam_arr, kernel, calls, None, traversal=t))
+                for t in (rt.TRAVERSAL_BOUNDED, rt.TRAVERSAL_KD)]
     fb = np.zeros(n * 3, np.float32)
     sq = np.zeros(n, np.float32)
     ct = np.zeros(n, np.int32)
@@ -60,6 +71,8 @@ def _render_both(run, osc, W, H, P, rng0, cam_arr, kernel, calls=1):
             total[key] = max(total.get(key, 0), v) if key == "maxdepth" else total.get(key, 0) + v
     helpers.assert_bitwise(gpu, (fb.reshape(n, 3), sq, ct, rng))
     assert cnt.read() == total, (cnt.read(), total)
+    for t, out in products:
+        helpers.assert_bitwise(out, (fb.reshape(n, 3), sq, ct, rng), what=f"traversal {t}")
     return haz
 
 
