@@ -94,6 +94,20 @@ def call_plan(first, count, per_call):
     return plan
 
 
+def traversal_of(args, rt):
+    return rt.TRAVERSAL_BOUNDED if args.traversal == "bounded" else rt.TRAVERSAL_KD
+
+
+def bounded_trace_bytes(c):
+    """Bytes the bounded queue trace kernel's algorithm reads / writes
+    (counters of a RT_TRAVERSAL_BOUNDED_COUNTED call; DESIGN.md "Roofline"):
+    per ray its 32-B ray and 16-B hit record, 64 B per BVH node (both child
+    boxes), 16 B per plane test (BVH or KD), 56 B per barycentric record
+    read, 8 B per KD node."""
+    return (48 * c["ray"] + 64 * c["b_bvh_node"] + 16 * (c["b_bvh_tri"] + c["tri"]) + 56 * c["b_bary"] +
+            8 * c["node"])
+
+
 def call_steps(args):
     """steps per timed rt_render call (the first, largest call of the plan)"""
     return max(1, min(args.steps_per_call, args.steps))
@@ -119,6 +133,9 @@ def parse_args(argv=None):
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher/rank wiring only (no GPU): ranks meet over gloo, rank 0 prints the line")
     ap.add_argument("--kernel", choices=["mega", "wavefront"], default="wavefront")
+    ap.add_argument("--traversal", choices=["bounded", "kd"], default="bounded",
+                    help="ray queries: the BVH-bounded KD traversal (default) or the KD traversal alone "
+                         "(RtOptions.traversal; identical images)")
     ap.add_argument("--adaptive", action="store_true", help="adaptive sampling (configs[4]); value stays nominal "
                     "W*H*spp/s, value_actual = accumulated samples/s")
     ap.add_argument("--min-samples", type=int, default=100)
@@ -210,7 +227,7 @@ def measure_pmc(args, save_dir):
     child = ["--pmc-child", "1", "--passes", str(args.passes * call_steps(args)), "--scene", args.scene,
              "--width", str(args.width),
              "--height", str(args.height), "--scene-dir", args.scene_dir, "--kernel", args.kernel,
-             "--max-depth", str(args.max_depth), "--min-samples", str(args.min_samples)]
+             "--traversal", args.traversal, "--max-depth", str(args.max_depth), "--min-samples", str(args.min_samples)]
     if args.adaptive:
         child.append("--adaptive")
     res = {"passes": {}}
@@ -252,7 +269,8 @@ def pmc_child(args, rt):
     W, H = args.width, args.height
     g = rt.GBuffer(W, H)
     kernel = rt.KERNEL_WAVEFRONT if args.kernel == "wavefront" else rt.KERNEL_MEGA
-    kw = dict(adaptive=args.adaptive, min_samples=args.min_samples, max_depth=args.max_depth, kernel=kernel)
+    kw = dict(adaptive=args.adaptive, min_samples=args.min_samples, max_depth=args.max_depth, kernel=kernel,
+              traversal=traversal_of(args, rt))
     rt.render(dscene, g, host.camera, 0, rt.options(W, H, 8, **kw))
     rgba = ctypes.c_void_p()
     rt.check(rt.lib().rt_device_alloc(ctypes.byref(rgba), W * H * 4))
@@ -463,7 +481,9 @@ def main(argv=None, binding=None):
     gb = rt.GBuffer(W, H, rank * n)  # spp slice r: mt19937 outputs [r*W*H, (r+1)*W*H) (shard.seed_skip)
     kernel = rt.KERNEL_WAVEFRONT if args.kernel == "wavefront" else rt.KERNEL_MEGA
     wavefront = kernel == rt.KERNEL_WAVEFRONT
-    render_kw = dict(adaptive=args.adaptive, min_samples=args.min_samples, max_depth=args.max_depth, kernel=kernel)
+    render_kw = dict(adaptive=args.adaptive, min_samples=args.min_samples, max_depth=args.max_depth, kernel=kernel,
+                     traversal=traversal_of(args, rt))
+    bounded = wavefront and args.traversal == "bounded"
     spc = max(1, args.steps_per_call)
     profiles = []
 
@@ -528,23 +548,45 @@ def main(argv=None, binding=None):
     expect = world * P * (args.warmup + args.steps)
 
     # work counters of one extra (untimed) call -> algorithmic bytes and the
-    # reference deviations (watchdog, longest path, pushes past the 19-entry stack)
+    # reference deviations (watchdog, longest path, pushes past the 19-entry
+    # stack): the KD traversal, whose counters are the reference's
     counters = rt.DeviceCounters()
-    copt = rt.options(W, H, P, counters=counters.p, profile=wavefront, **render_kw)
+    copt = rt.options(W, H, P, counters=counters.p, profile=wavefront, **dict(render_kw, traversal=rt.TRAVERSAL_KD))
     rt.render(dscene, gb, host.camera, 1, copt)
     c = counters.read(finisher=True)
     bytes_per_call = algorithmic_bytes(c)
     if wavefront:
-        cprof = rt.last_profile()
-        trace_bytes = 8 * (c["node"] - c["finish_node"]) + 40 * (c["tri"] - c["finish_tri"])
         launches = sum(p["trace_launches"] for p in profiles)
         avg_launch_ms = sum(p["trace_ms"] for p in profiles) / max(launches, 1)
+        if bounded:
+            # the dominant kernel's own work: one more call, the bounded queue
+            # trace kernel counting (RT_TRAVERSAL_BOUNDED_COUNTED)
+            bcnt = rt.DeviceCounters()
+            rt.render(dscene, gb, host.camera, 1, rt.options(W, H, P, counters=bcnt.p, profile=True,
+                                                             **dict(render_kw, traversal=rt.TRAVERSAL_BOUNDED_COUNTED)))
+            bc = bcnt.read(finisher=True)
+            cprof = rt.last_profile()
+            trace_bytes = bounded_trace_bytes(bc)
+            kname = "wf_trace_bvh<false>"
+            work = {"rays": bc["ray"], "bvh_nodes_per_ray": round(bc["b_bvh_node"] / max(bc["ray"], 1), 2),
+                    "bvh_tests_per_ray": round(bc["b_bvh_tri"] / max(bc["ray"], 1), 2),
+                    "kd_nodes_per_ray": round(bc["node"] / max(bc["ray"], 1), 2),
+                    "kd_tests_per_ray": round(bc["tri"] / max(bc["ray"], 1), 2),
+                    "bary_per_ray": round(bc["b_bary"] / max(bc["ray"], 1), 2),
+                    "bytes_per_ray": round(trace_bytes / max(bc["ray"], 1), 1),
+                    "counted_call_passes": P}
+        else:
+            cprof = rt.last_profile()
+            trace_bytes = 8 * (c["node"] - c["finish_node"]) + 40 * (c["tri"] - c["finish_tri"])
+            kname = "wf_trace_coop<false>"
+            work = {}
         bytes_per_launch = trace_bytes / max(cprof["trace_launches"], 1)
         kernel_detail = {
-            "kernel": "wf_trace_coop<false>",
+            "kernel": kname,
             "pipelines": cprof["pipelines"],
             "trace_launches_per_call": launches / max(len(profiles), 1),
             "avg_launch_ms": round(avg_launch_ms, 4),
+            "algorithmic_bytes_per_launch": round(bytes_per_launch),
             "algorithmic_GBps_per_launch": round(bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9, 1),
             "trace_union_ms_per_call": round(float(np.mean([p["trace_union_ms"] for p in profiles])), 3),
             "trace_ms_per_call": round(float(np.mean([p["trace_ms"] for p in profiles])), 3),
@@ -554,6 +596,8 @@ def main(argv=None, binding=None):
             "iterations_per_call": round(float(np.mean([p["iterations"] for p in profiles])), 1),
             "passes_per_call": round(float(np.mean([p["passes"] for p in profiles])), 1),
         }
+        if work:
+            kernel_detail["kernel_work"] = work
     else:
         kernel_detail = {"kernel": "rt_path_kernel<false,20>"}
 
@@ -573,7 +617,7 @@ def main(argv=None, binding=None):
         roof["traffic_unit"] = (f"HBM bytes per step of {P} passes (whole frame, every kernel), from one profiled "
                                 f"call of {P * call_steps(args)} passes = the timed calls' shape")
         dk = detail["per_kernel"].get(detail["dominant_kernel"] or "", {})
-        if wavefront and dk.get("dispatches") and "wf_trace_coop" in (detail["dominant_kernel"] or ""):
+        if wavefront and dk.get("dispatches") and kernel_detail["kernel"].split("<")[0] in (detail["dominant_kernel"] or ""):
             # the dominant kernel alone: its counter bytes per launch / its live
             # average launch time (HIP events on its pipeline's stream, timed steps)
             per_launch = 1e9 * (dk.get("fetch_GB", 0.0) + dk.get("write_GB", 0.0)) / dk["dispatches"]

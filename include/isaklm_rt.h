@@ -363,6 +363,13 @@ enum {
     RT_CNT_PEND_LANES = 34,
     RT_CNT_LEAF_TESTS = 35,
     RT_CNT_T_DESC_WAIT = 36,
+    /* RtOptions.traversal = RT_TRAVERSAL_BOUNDED_COUNTED only: the bounded
+     * queue trace kernel's own work (RT_CNT_NODE / _TRI then count its KD
+     * nodes / plane tests): BVH nodes, BVH plane tests, and the barycentric
+     * records read by both phases */
+    RT_CNT_B_BVH_NODE = 37,
+    RT_CNT_B_BVH_TRI = 38,
+    RT_CNT_B_BARY = 39,
     RT_CNT_COUNT = 40
 };
 
@@ -423,13 +430,18 @@ typedef struct RtOptions {
      * (default) first finds a lower bound of the ray's first hit distance in
      * a conservative BVH built by rt_scene_prepare and skips the KD subtrees
      * the reference would test for nothing; RT_TRAVERSAL_KD runs the KD
-     * traversal alone.  Calls with counters_device always run the KD
-     * traversal (its counters are the reference's) */
+     * traversal alone.  Calls with counters_device run the KD traversal (its
+     * counters are the reference's) unless traversal is
+     * RT_TRAVERSAL_BOUNDED_COUNTED: the wavefront queue trace launches then
+     * run the bounded traversal and count its own work (RT_CNT_RAY, _NODE,
+     * _TRI, _HIT, RT_CNT_B_*; measurement: the finisher and the long-path
+     * kernel are not counted).  The megakernel always runs the KD traversal. */
     int traversal;
 } RtOptions;
 
 #define RT_TRAVERSAL_BOUNDED 0
 #define RT_TRAVERSAL_KD 1
+#define RT_TRAVERSAL_BOUNDED_COUNTED 2
 
 /* Per-call kernel timing of the last rt_render on this device with
  * RtOptions.profile = 1 (wavefront kernels; HIP events on the call's stream,

@@ -14,6 +14,20 @@ RT_HD float rt_ray_margin(float ox, float oy, float oz, float scale)
     return 0x1p-16f * (fabsf(ox) + fabsf(oy) + fabsf(oz) + 2.0f * scale);
 }
 
+// Whether the bound applies to this ray.  The skip rule needs every KD
+// split distance t = (split - o) / d to be a number (+-inf allowed): then
+// the exits inside a near subtree never exceed its split distance.  A
+// direction component of exactly 0 makes t = 0 / 0 = NaN for a ray lying in a
+// split plane; the reference then pushes with NaN, and later pushes inside
+// that subtree can carry exits beyond the split (its leaf order is no longer
+// front to back).  Such rays (and non-finite ones) take the plain KD
+// traversal.
+RT_HD bool rt_bounded_ray(Vec3D o, Vec3D d)
+{
+    return fabsf(d.x) > 0.0f && fabsf(d.y) > 0.0f && fabsf(d.z) > 0.0f && o.x - o.x == 0.0f && o.y - o.y == 0.0f &&
+           o.z - o.z == 0.0f && d.x - d.x == 0.0f && d.y - d.y == 0.0f && d.z - d.z == 0.0f;
+}
+
 // Slab test of a box grown by the ray's margin: om = o + margin, op = o -
 // margin, inv = 1 / d.  True when the ray's [0, best] may meet the box.  An
 // axis-parallel ray (inv = inf) whose origin lies exactly on a grown face

@@ -29,17 +29,19 @@ namespace rtk {
 // one triangle test of intersect_triangle + calculate_barycentric_coordinates
 // (rt/trace_ray.cuh:48-113) on precomputed records: the same operations as
 // trace()'s leaf loop; true and s when it passes with s < closest
+template <bool COUNT>
 __device__ __forceinline__ bool tri_test(const RtF4 *plane, const RtIsectBary *bary, uint32_t e, Vec3D o, Vec3D d,
-                                         float closest, float &s, float &cx, float &cy, float &cz)
+                                         float closest, float &s, float &cx, float &cy, float &cz, Cnt &c)
 {
     if (!rt_tri_plane(ldf4(plane + e), o, d, closest, s)) return false;
+    if (COUNT) c.v[RT_CNT_B_BARY]++;
     return rt_tri_bary(ldf4(&bary[e].b), ldf4(&bary[e].c), ldf4(&bary[e].d), as_float(bary[e].rd), o, d, s, cx, cy,
                        cz);
 }
 
 // s_min of step 2: the smallest s < best of any passing test (best if none)
-template <typename STACK>
-__device__ __forceinline__ float bvh_bound(const RtDevScene &sc, Vec3D o, Vec3D d, float best, STACK &stk)
+template <bool COUNT, typename STACK>
+__device__ __forceinline__ float bvh_bound(const RtDevScene &sc, Vec3D o, Vec3D d, float best, STACK &stk, Cnt &cn)
 {
     const float m = rt_ray_margin(o.x, o.y, o.z, sc.bvh_scale);
     const Vec3D om = rt_v3(o.x + m, o.y + m, o.z + m), op = rt_v3(o.x - m, o.y - m, o.z - m);
@@ -49,6 +51,7 @@ __device__ __forceinline__ float bvh_bound(const RtDevScene &sc, Vec3D o, Vec3D 
     while (true) {
         if (!(cur & RT_BVH_LEAF)) {
             const RtF4 *nd = sc.bvh_nodes + 4 * (size_t)cur;
+            if (COUNT) cn.v[RT_CNT_B_BVH_NODE]++;
             const RtF4 a = ldf4(nd), b = ldf4(nd + 1), c = ldf4(nd + 2);
             const uint2 ch = *reinterpret_cast<const uint2 *>(nd + 3);
             float tn0, tn1;
@@ -69,7 +72,8 @@ __device__ __forceinline__ float bvh_bound(const RtDevScene &sc, Vec3D o, Vec3D 
             const uint32_t first = (cur & ~RT_BVH_LEAF) >> 3, end = first + (cur & 7u) + 1u;
             for (uint32_t e = first; e < end; ++e) {
                 float s, cx, cy, cz;
-                if (tri_test(sc.bvh_a, sc.bvh_bary, e, o, d, best, s, cx, cy, cz)) best = s;
+                if (COUNT) cn.v[RT_CNT_B_BVH_TRI]++;
+                if (tri_test<COUNT>(sc.bvh_a, sc.bvh_bary, e, o, d, best, s, cx, cy, cz, cn)) best = s;
             }
         }
         // pop the next subtree that may still hold a smaller s
@@ -90,21 +94,29 @@ __device__ __forceinline__ float bvh_bound(const RtDevScene &sc, Vec3D o, Vec3D 
 }
 
 // trace_ray with the bound: returns the triangle index or -1 and the hit's
-// barycentric coordinates, bit-identical to trace()
-template <typename STACK>
+// barycentric coordinates, bit-identical to trace().  COUNT (RT_TRAVERSAL_
+// BOUNDED_COUNTED): this traversal's own work — RT_CNT_RAY, RT_CNT_NODE / _TRI
+// (KD nodes / plane tests), RT_CNT_B_* (BVH nodes / plane tests, barycentric
+// records of both phases)
+template <bool COUNT, typename STACK>
 __device__ __forceinline__ int trace_bvh(const RtDevScene &sc, const Vec3D o, const Vec3D d, float &hbx, float &hby,
-                                         float &hbz, STACK &stk)
+                                         float &hbz, STACK &stk, Cnt &c)
 {
+    if (COUNT) c.v[RT_CNT_RAY]++;
     float entry, exit_;
     if (!bbox_hit(sc, o, d, entry, exit_)) return -1;
     const float root_exit = exit_;
-    const float s_min = bvh_bound(sc, o, d, exit_, stk);
-    if (!(s_min < root_exit)) return -1;
+    float s_min = -INFINITY; // (the plain KD traversal)
+    if (rt_bounded_ray(o, d)) {
+        s_min = bvh_bound<COUNT>(sc, o, d, exit_, stk, c);
+        if (!(s_min < root_exit)) return -1;
+    }
     const float yx = rt_recip_guard(d.x), yy = rt_recip_guard(d.y), yz = rt_recip_guard(d.z);
     int sp = 0;
     uint32_t node = 0;
     while (true) {
         uint2 nd = *reinterpret_cast<const uint2 *>(sc.nodes + 2 * (size_t)node);
+        if (COUNT) c.v[RT_CNT_NODE]++;
         while ((nd.y & 3u) != RT_LEAF_TAG) {
             const uint32_t axis = nd.y & 3u;
             const float split = as_float(nd.x);
@@ -131,6 +143,7 @@ __device__ __forceinline__ int trace_bvh(const RtDevScene &sc, const Vec3D o, co
                 exit_ = t;
             }
             nd = *reinterpret_cast<const uint2 *>(sc.nodes + 2 * (size_t)node);
+            if (COUNT) c.v[RT_CNT_NODE]++;
         }
         const uint32_t count = nd.y >> 2;
         if (count > 0 && exit_ > s_min) {
@@ -140,7 +153,8 @@ __device__ __forceinline__ int trace_bvh(const RtDevScene &sc, const Vec3D o, co
             float bx = 0.0f, by = 0.0f, bz = 0.0f;
             for (uint32_t e = nd.x; e < nd.x + count; ++e) {
                 float s, cx, cy, cz;
-                if (tri_test(sc.isect_a, sc.isect_bary, e, o, d, smallest, s, cx, cy, cz)) {
+                if (COUNT) c.v[RT_CNT_TRI]++;
+                if (tri_test<COUNT>(sc.isect_a, sc.isect_bary, e, o, d, smallest, s, cx, cy, cz, c)) {
                     smallest = s;
                     best = (int)sc.isect_bary[e].tri;
                     bx = cx;
@@ -149,6 +163,7 @@ __device__ __forceinline__ int trace_bvh(const RtDevScene &sc, const Vec3D o, co
                 }
             }
             if (best >= 0) {
+                if (COUNT) c.v[RT_CNT_HIT]++;
                 hbx = bx;
                 hby = by;
                 hbz = bz;

@@ -268,8 +268,12 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_trace(RtDevScene sc, WfState st, 
 // trace_ray bounded by the conservative BVH (bvh_trace.h): one ray per lane,
 // lanes refill from the queue (one wave-aggregated atomic per refill round)
 // so a wave is not held by its slowest ray's successors
-__global__ void __launch_bounds__(WF_BLOCK, WF_BVH_WAVES) wf_trace_bvh(RtDevScene sc, WfState st, int q)
+template <bool COUNT>
+__global__ void __launch_bounds__(WF_BLOCK, WF_BVH_WAVES) wf_trace_bvh(RtDevScene sc, WfState st, int q,
+                                                                      unsigned long long *counters)
 {
+    Cnt c;
+    if (COUNT) c.zero();
     __shared__ uint32_t s_node[WF_BVH_LDS * WF_BLOCK];
     __shared__ float s_entry[WF_BVH_LDS * WF_BLOCK];
     const int tid = threadIdx.x;
@@ -289,9 +293,10 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_BVH_WAVES) wf_trace_bvh(RtDevScen
         if (e >= n) break;
         const RtF4 o4 = ldf4(rays + 2 * (size_t)e), d4 = ldf4(rays + 2 * (size_t)e + 1);
         float bx = 0.0f, by = 0.0f, bz = 0.0f;
-        const int hit = trace_bvh(sc, ld3(o4), ld3(d4), bx, by, bz, stk);
+        const int hit = trace_bvh<COUNT>(sc, ld3(o4), ld3(d4), bx, by, bz, stk, c);
         *reinterpret_cast<float4 *>(st.hits + e) = make_float4(__int_as_float(hit), bx, by, bz);
     }
+    if (COUNT) flush_counters(c, counters);
 }
 
 // Persistent trace with dynamic ray fetch: every lane runs rays one leaf at a
@@ -836,6 +841,56 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_finish(RtDevScene sc, RtDevFrame 
     }
 }
 
+// Tail finisher with the BVH-bounded traversal (bvh_trace.h): every lane runs
+// one path to the end of its pixel's passes (trace + shade in registers) and
+// then takes the next queued path (wave-aggregated atomic on counts[4]).
+__global__ void __launch_bounds__(WF_BLOCK, WF_BVH_WAVES) wf_finish_bvh(RtDevScene sc, RtDevFrame fr, RtDevCamera cam,
+                                                                       WfState st, int q)
+{
+    __shared__ uint32_t s_node[WF_BVH_LDS * WF_BLOCK];
+    __shared__ float s_entry[WF_BVH_LDS * WF_BLOCK];
+    const int tid = threadIdx.x;
+    const int gtid = blockIdx.x * WF_BLOCK + tid;
+    Stack<WF_BVH_LDS> stk{s_node + tid, s_entry + tid, WF_BLOCK, st.spill + gtid, st.spill_threads};
+    Cnt c; // (unused: the counting build runs wf_finish_coop)
+    const uint32_t n = st.counts[6 + q]; // paths of path list q
+    uint32_t *fetch = st.counts + 4;
+    const int limit = fr.max_depth > 0 ? fr.max_depth : RT_WATCHDOG_BOUNCES;
+    const int lane = __lane_id();
+    PathRegs p;
+    p.slot = 0;
+    p.ro = p.rd = rt_v3(0, 0, 0);
+    bool active = false, exhausted = false;
+    while (true) {
+        const bool need = !active && !exhausted;
+        const unsigned long long m = __ballot(need);
+        if (m) {
+            const int leader = __ffsll((long long)m) - 1;
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(fetch, (uint32_t)__popcll(m));
+            base = __shfl(base, leader);
+            if (need) {
+                const uint32_t e = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+                if (e >= n) {
+                    exhausted = true;
+                } else {
+                    active = true;
+                    first_ray(st, fr, st.q_slot[q][e], p);
+                }
+            }
+        }
+        if (!__any(active)) break; // every lane exhausted
+        if (active) {
+            float bx = 0.0f, by = 0.0f, bz = 0.0f;
+            const int hit = trace_bvh<false>(sc, p.ro, p.rd, bx, by, bz, stk, c);
+            if (!shade_step<false>(sc, fr, cam, p, hit, bx, by, bz, limit, c)) {
+                store_regs(st, fr, p);
+                active = false;
+            }
+        }
+    }
+}
+
 // Cooperative finisher: runs queued paths to the end of their passes in
 // registers (shade_step right after each ray query), megakernel style, while
 // the whole wave tests leaf entries for its live rays together (coop_round).
@@ -971,8 +1026,10 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_FIN_OCC) wf_finish_coop(RtDevScen
 // published) drains what is left.
 template <bool COUNT>
 __global__ void __launch_bounds__(WF_BLOCK, WF_LONG_WAVES) wf_long(RtDevScene sc, RtDevFrame fr, RtDevCamera cam, WfState st,
-                                                    int final_slice)
+                                                    int final_slice, int bvh)
 {
+    __shared__ uint32_t s_bnode[WF_BVH_LDS * WF_BLOCK]; // bounded traversal stacks (lane 0 of each wave)
+    __shared__ float s_bentry[WF_BVH_LDS * WF_BLOCK];
     __shared__ WideItem s_wide[(WF_BLOCK / 64) * WIDE_CAP];
     __shared__ unsigned long long s_key[(WF_BLOCK / 64) * 4];
     __shared__ int s_mark[2 * WF_BLOCK]; // 128 per wave: chunk_owner marks + junk slots
@@ -1025,20 +1082,31 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_LONG_WAVES) wf_long(RtDevScene sc
         PathRegs p;
         p.slot = 0;
         p.ro = p.rd = rt_v3(0, 0, 0);
+        int want_more = 1;
         if (lane == 0) {
             load_regs(st, fr, flag - 1u, p);
             p.ro = ld3(ldf4(st.long_ray + 2 * (size_t)e));
             p.rd = ld3(ldf4(st.long_ray + 2 * (size_t)e + 1));
         }
         while (true) {
+            int hit = -1;
+            float bx = 0.0f, by = 0.0f, bz = 0.0f;
+            if (!COUNT && bvh) { // the bounded traversal by lane 0 alone
+                if (lane == 0) {
+                    Stack<WF_BVH_LDS> stk{s_bnode + threadIdx.x, s_bentry + threadIdx.x, WF_BLOCK,
+                                          st.spill + blockIdx.x * WF_BLOCK + threadIdx.x, st.spill_threads};
+                    hit = trace_bvh<false>(sc, p.ro, p.rd, bx, by, bz, stk, c);
+                    if (!shade_step<COUNT>(sc, fr, cam, p, hit, bx, by, bz, limit, c)) want_more = 0;
+                }
+                if (!__shfl(want_more, 0)) break;
+                continue;
+            }
             CoopRay r;
             coop_idle(r);
             if (lane == 0) {
                 if (COUNT) c.v[RT_CNT_RAY]++;
                 coop_begin(sc, r, p.ro, p.rd);
             }
-            int hit = -1;
-            float bx = 0.0f, by = 0.0f, bz = 0.0f;
             if (__shfl((int)r.live, 0)) {
                 const Vec3D o = rt_v3(__shfl(r.o.x, 0), __shfl(r.o.y, 0), __shfl(r.o.z, 0));
                 const Vec3D d = rt_v3(__shfl(r.d.x, 0), __shfl(r.d.y, 0), __shfl(r.d.z, 0));
@@ -1243,7 +1311,12 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
     const bool count = fr.counters != nullptr;
     const bool prof = profile != 0;
     // the queue trace launches run the BVH-bounded traversal (counting calls: the KD one, whose counters are the reference's)
-    const bool bounded = !count && traversal == RT_TRAVERSAL_BOUNDED && sc.bvh_nodes != nullptr;
+    const bool bounded = sc.bvh_nodes != nullptr && ((traversal == RT_TRAVERSAL_BOUNDED && !count) ||
+                                                     traversal == RT_TRAVERSAL_BOUNDED_COUNTED);
+    // ... and the tail finisher too (RT_WF_FIN_BVH=0: the cooperative KD finisher; experiments)
+    static const bool fin_bvh = !getenv("RT_WF_FIN_BVH") || atoi(getenv("RT_WF_FIN_BVH")) != 0;
+    // long paths (wf_long): one lane's bounded traversal instead of 64 lanes' wide KD one (RT_WF_LONG_BVH=1; experiments)
+    static const bool long_bvh = getenv("RT_WF_LONG_BVH") && atoi(getenv("RT_WF_LONG_BVH")) != 0;
     const int tiles = ((fr.width + 15) / 16) * ((fr.height + 15) / 16);
     int npipes = pipes_opt > 0 ? pipes_opt : WF_PIPES_DEFAULT;
     npipes = npipes > WF_MAX_PIPES ? WF_MAX_PIPES : npipes;
@@ -1308,9 +1381,10 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
         }
         const int fin = final ? 1 : 0;
         if (count)
-            hipLaunchKernelGGL(wf_long<true>, dim3(WF_LONG_BLOCKS), dim3(WF_BLOCK), 0, stream, sc, fr, cam, lst, fin);
+            hipLaunchKernelGGL(wf_long<true>, dim3(WF_LONG_BLOCKS), dim3(WF_BLOCK), 0, stream, sc, fr, cam, lst, fin, 0);
         else
-            hipLaunchKernelGGL(wf_long<false>, dim3(WF_LONG_BLOCKS), dim3(WF_BLOCK), 0, stream, sc, fr, cam, lst, fin);
+            hipLaunchKernelGGL(wf_long<false>, dim3(WF_LONG_BLOCKS), dim3(WF_BLOCK), 0, stream, sc, fr, cam, lst, fin,
+                               bounded && long_bvh ? 1 : 0);  // (counting calls: the KD wide traversal)
         if (hipGetLastError() != hipSuccess) return -1;
         long_final = final;
         if (hipEventRecord(w.long_ev, stream) != hipSuccess) return -1;
@@ -1346,7 +1420,13 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
         // run the `live` paths of queue qq to the end of the call in the finisher
         auto finish = [&](int qq, uint32_t live) -> int {
             if (!mark(2)) return -1;
-            if (trace_kind == 1) {
+            if (bounded && fin_bvh) {
+                // one path per lane (lanes refill from the list), within the spill area (grid blocks)
+                int fgrid = (int)((live + WF_BLOCK - 1) / WF_BLOCK);
+                fgrid = fgrid > grid ? grid : fgrid;
+                if (hipMemsetAsync(st.counts + 4, 0, 4, s) != hipSuccess) return -1;
+                hipLaunchKernelGGL(wf_finish_bvh, dim3(fgrid), dim3(WF_BLOCK), 0, s, sc, fr, cam, st, qq);
+            } else if (trace_kind == 1) {
                 // paths per wave: spread over up to finish_waves waves, within the spill area (grid * WF_BLOCK threads)
                 const uint32_t max_waves = (uint32_t)grid * (WF_BLOCK / 64);
                 uint32_t ppw = (live + finish_waves - 1) / finish_waves;
@@ -1387,7 +1467,10 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
                 if (hipMemsetAsync(st.counts + 2 + q, 0, 4, s) != hipSuccess) return -1; // fetch cursor
                 if (!mark(4)) return -1;
                 if (bounded) {
-                    hipLaunchKernelGGL(wf_trace_bvh, dim3(grid), dim3(WF_BLOCK), 0, s, sc, st, q);
+                    if (count)
+                        hipLaunchKernelGGL(wf_trace_bvh<true>, dim3(grid), dim3(WF_BLOCK), 0, s, sc, st, q, fr.counters);
+                    else
+                        hipLaunchKernelGGL(wf_trace_bvh<false>, dim3(grid), dim3(WF_BLOCK), 0, s, sc, st, q, nullptr);
                 } else if (trace_kind == 1) {
                     const int li = it * npipes + pi;
                     unsigned long long *tl = fr.wave_times && li < WF_TIMELINE_LAUNCHES ? fr.wave_times + 3 * li : nullptr;

@@ -99,7 +99,7 @@ COUNTER_NAMES = ["node", "tri", "hit", "texel", "nee", "sample", "skip", "ray", 
 FINISH_COUNTER_NAMES = ["finish_node", "finish_tri", "finish_ray", "cand", "plane", "deep_push", "t_descend", "t_leaves",
                         "t_fetch", "rounds", "chunks", "bary", "wide_calls", "wide_rounds", "t_wide", "t_wide_load", "t_wide_leaf", "t_wide_expand",
                        "t_leaf_wait", "t_leaf_setup", "t_leaf_test", "t_leaf_bary", "spill_push", "spill_pop",
-                        "pend_lanes", "leaf_tests", "t_desc_wait"]
+                        "pend_lanes", "leaf_tests", "t_desc_wait", "b_bvh_node", "b_bvh_tri", "b_bary"]
 N_COUNTERS = 40
 
 _lib = None
@@ -349,6 +349,7 @@ KERNEL_MEGA = 0
 KERNEL_WAVEFRONT = 1
 TRAVERSAL_BOUNDED = 0
 TRAVERSAL_KD = 1
+TRAVERSAL_BOUNDED_COUNTED = 2  # measurement: the bounded queue trace kernel counts its own work
 
 
 def options(width, height, passes=1, adaptive=True, min_samples=100, tolerance=0.05, max_depth=0, stream=None,
@@ -371,7 +372,8 @@ def options(width, height, passes=1, adaptive=True, min_samples=100, tolerance=0
     o.wf_pipelines = wf_pipelines
     o.wf_long_depth = wf_long_depth
     if traversal is None and os.environ.get("RT_TRAVERSAL"):
-        traversal = {"bounded": TRAVERSAL_BOUNDED, "kd": TRAVERSAL_KD}[os.environ["RT_TRAVERSAL"]]
+        traversal = {"bounded": TRAVERSAL_BOUNDED, "kd": TRAVERSAL_KD,
+                     "bounded_counted": TRAVERSAL_BOUNDED_COUNTED}[os.environ["RT_TRAVERSAL"]]
     if traversal is not None:
         o.traversal = traversal
     return o

@@ -17,6 +17,7 @@ import oracle
 
 KERNEL_MEGA = 0
 KERNEL_WAVEFRONT = 1
+TRAVERSAL_BOUNDED, TRAVERSAL_KD, TRAVERSAL_BOUNDED_COUNTED = 0, 1, 2
 SLOW_RANK = int(os.environ.get("STUB_SLOW_RANK", "1"))
 SLOW_S = float(os.environ.get("STUB_SLOW_S", "0.25"))
 calls = []  # (rank, sample_count, passes) of every render
@@ -140,7 +141,7 @@ class DeviceCounters:
         out = {k: self.c.get(k, 0) for k in oracle.COUNTER_NAMES}
         out["deep_push"] = self.c.get("deep_push", 0)
         if finisher:
-            out.update(finish_node=0, finish_tri=0, finish_ray=0)
+            out.update(finish_node=0, finish_tri=0, finish_ray=0, b_bvh_node=0, b_bvh_tri=0, b_bary=0)
         return out
 
 

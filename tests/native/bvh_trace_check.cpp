@@ -9,7 +9,8 @@
 // Links the library's host code (rt_host::*): the scene loader, the KD
 // build and prepare_host, i.e. the very arrays the GPU gets.
 //
-// Usage: bvh_trace_check scene.txt [rays] [seed]; exit 0 = all identical.
+// Usage: bvh_trace_check scene.txt [rays] [seed] ["x y z" camera position,
+// hex floats]; exit 0 = all identical.
 #include <math.h>
 #include <omp.h>
 #include <stdio.h>
@@ -23,6 +24,8 @@
 #include "host/rt_host.h"
 
 namespace {
+
+bool g_debug = false;
 
 float bitsf(uint32_t u)
 {
@@ -97,6 +100,7 @@ Hit kd_trace(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, float entry, floa
             ++w.nodes;
         }
         const uint32_t count = ny >> 2;
+        if (g_debug) printf("  leaf node %u count %u entry %a exit %a sp %d\n", node, count, entry, exit_, sp);
         if (count > 0 && exit_ > s_min) {
             ++w.leaves;
             float smallest = exit_;
@@ -175,6 +179,7 @@ Hit bounded_trace(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, Work &w)
 {
     float t1, t2;
     if (!scene_box(h, o, d, t1, t2)) return Hit{};
+    if (!rt_bounded_ray(o, d)) return kd_trace(h, o, d, t1, t2, -INFINITY, w);
     const float s_min = bvh_bound(h, o, d, t2, w);
     if (!(s_min < t2)) return Hit{};
     return kd_trace(h, o, d, t1, t2, s_min, w);
@@ -213,6 +218,36 @@ int main(int argc, char **argv)
     if (rt_host::prepare_host(scene.tris.data(), n, nodes.data(), (int)nodes.size(), indices.data(),
                               (int)indices.size(), lights.data(), (int)lights.size(), bounds, h) != RT_OK) {
         fprintf(stderr, "prepare failed\n");
+        return 2;
+    }
+    if (argc > 3 && strcmp(argv[2], "ray") == 0) { // debug one ray: "ox oy oz dx dy dz" (hex floats)
+        Vec3D o, d;
+        if (sscanf(argv[3], "%a %a %a %a %a %a", &o.x, &o.y, &o.z, &d.x, &d.y, &d.z) != 6) return 2;
+        Work w;
+        float t1, t2;
+        const bool in = scene_box(h, o, d, t1, t2);
+        const float s_min = in ? bvh_bound(h, o, d, t2, w) : NAN;
+        g_debug = true;
+        printf("plain:\n");
+        const Hit a = plain_trace(h, o, d, w);
+        printf("bounded:\n");
+        const Hit b = bounded_trace(h, o, d, w);
+        g_debug = false;
+        printf("box %d [%a, %a] s_min %a kd %d bounded %d\n", in, t1, t2, s_min, a.tri, b.tri);
+        for (int e = 0; e < (int)h.isect_a.size(); ++e) { // every passing test (KD entry order)
+            float s, bb[3];
+            if (test(h.isect_a.data(), h.isect_bary.data(), (uint32_t)e, o, d, INFINITY, s, bb))
+                printf("  pass: entry %d tri %u s %a\n", e, h.isect_bary[e].tri, s);
+        }
+        for (size_t k = 0; k < h.bvh_a.size(); ++k) {
+            float s, bb[3];
+            if (test(h.bvh_a.data(), h.bvh_bary.data(), (uint32_t)k, o, d, INFINITY, s, bb))
+                printf("  bvh pass: slot %zu tri %u s %a\n", k, h.bvh_bary[k].tri, s);
+        }
+        return 0;
+    }
+    if (argc > 4 && sscanf(argv[4], "%a %a %a", &cam.position.x, &cam.position.y, &cam.position.z) != 3) {
+        fprintf(stderr, "bad camera position '%s'\n", argv[4]);
         return 2;
     }
     if (h.bvh_depth < 0) {

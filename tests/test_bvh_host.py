@@ -1,0 +1,89 @@
+"""CPU checks of the BVH-bounded traversal (csrc/bvh_trace.h; host side
+csrc/host/bvh_build.*):
+
+* tests/native/bvh_margin_check.cpp — the conservative margins never cull a
+  passing triangle test (adversarial triangles and rays), and triangles left
+  out of the BVH never pass;
+* tests/native/bvh_trace_check.cpp — a host restatement of the bounded
+  traversal over the library's own prepared arrays returns the plain KD
+  traversal's (= trace_ray's) result bit for bit on millions of camera and
+  bounce rays, including the hazard scenes (walls on split planes, the camera
+  on the root split, axis-parallel and grazing rays, zero-area triangles, the
+  glass light guide).
+
+The GPU kernel itself is compared with the oracle and the KD traversal in
+tests/test_gpu_traversal.py.
+"""
+import os
+import subprocess
+
+import pytest
+
+import hazards
+import helpers
+import oracle
+import rt
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NATIVE = os.path.join(ROOT, "tests", "native")
+CSRC = os.path.join(ROOT, "isaklm-raytracer_amd", "csrc")
+INC = os.path.join(ROOT, "include")
+FLAGS = ["-O2", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-I" + INC, "-I" + CSRC]
+
+
+def _build(tmp_path_factory, name, link_lib):
+    out = str(tmp_path_factory.mktemp("bvh") / name)
+    cmd = ["g++"] + FLAGS + [os.path.join(NATIVE, name + ".cpp"), "-o", out]
+    if link_lib:
+        libdir = os.path.dirname(rt.LIB_PATH)
+        cmd += ["-fopenmp", "-L" + libdir, "-lisaklm_rt", "-Wl,-rpath," + libdir, "-Wl,-rpath,/opt/rocm/lib"]
+    subprocess.run(cmd, check=True, capture_output=True, text=True)
+    return out
+
+
+@pytest.fixture(scope="module")
+def margin_check(tmp_path_factory):
+    return _build(tmp_path_factory, "bvh_margin_check", False)
+
+
+@pytest.fixture(scope="module")
+def trace_check(tmp_path_factory):
+    rt.lib()  # the library must exist (and match the header)
+    return _build(tmp_path_factory, "bvh_trace_check", True)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_margins_never_cull_a_passing_test(margin_check, seed):
+    r = subprocess.run([margin_check, "3", str(seed)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    stats = dict(zip(r.stdout.split()[::2], r.stdout.split()[1::2]))
+    assert int(stats["passes"]) > 1_000_000 and int(stats["violations"]) == 0 and int(stats["nan_passes"]) == 0
+    # the margins are generous: a hit point never used more than a small part of them
+    assert float(stats["max_used"]) < 0.05, stats
+
+
+def _run_trace_check(exe, scene, rays=1_000_000, seed=7, cam=None):
+    args = [exe, scene, str(rays), str(seed)] + ([" ".join(float(v).hex() for v in cam)] if cam is not None else [])
+    r = subprocess.run(args, capture_output=True, text=True, timeout=600, env=dict(os.environ, OMP_NUM_THREADS="4"))
+    assert r.returncode == 0, r.stdout + r.stderr
+    return r.stdout
+
+
+@pytest.mark.parametrize("name", ["cornell", "cornell_blob", "room_small"])
+def test_bounded_equals_kd_host(trace_check, name):
+    out = _run_trace_check(trace_check, helpers.scene_path(name))
+    assert "mismatches 0" in out, out
+
+
+def test_bounded_equals_kd_hazard_scenes(trace_check, tmp_path):
+    aligned = hazards.cornell_variant(str(tmp_path / "a"), "aligned", yaw_room=0.0)
+    assert "mismatches 0" in _run_trace_check(trace_check, aligned, 500_000)
+    degen = hazards.cornell_variant(str(tmp_path / "d"), "degenerate", yaw_room=0.1, extra_obj=hazards.DEGENERATE_OBJ)
+    out = _run_trace_check(trace_check, degen, 500_000)
+    assert "mismatches 0" in out and "dropped 0" not in out, out  # the zero-area triangles are left out
+    trap = helpers.make_trap_scene(str(tmp_path / "t"))
+    assert "mismatches 0" in _run_trace_check(trace_check, trap, 500_000)
+    # camera rays from exactly the root split plane
+    path = helpers.scene_path("cornell")
+    on, _ = hazards.h5_cameras(oracle.OracleScene(path))
+    assert "mismatches 0" in _run_trace_check(trace_check, path, 500_000, cam=on[:3])
