@@ -237,10 +237,13 @@ def measure_pmc(args, save_dir):
         cmd = ["timeout", "-s", "KILL", "240", "rocprofv3", "--pmc", *ctrs, "--kernel-trace", "-d", d, "-o", "run",
                "--output-format", "csv", "--", sys.executable, os.path.abspath(__file__)] + child
         t = time.perf_counter()
-        r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True)
+        print(f"[bench] counter pass '{tag}' ({' '.join(ctrs)})", file=sys.stderr, flush=True)
+        # stderr passes through (rocprofv3's log and the child's progress lines: a
+        # pass of a 256-pass call runs for minutes); stdout carries the child's result
+        r = subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.PIPE, text=True)
         if r.returncode != 0:
             shutil.rmtree(d, ignore_errors=True)
-            return {"error": f"rocprofv3 {tag} pass rc={r.returncode}: {(r.stderr or r.stdout)[-400:]}"}
+            return {"error": f"rocprofv3 {tag} pass rc={r.returncode} (its log: this run's stderr): {r.stdout[-300:]}"}
         cc, kt = _collect_csv(d, "counter_collection"), _collect_csv(d, "kernel_trace")
         try:
             total, per_kernel, ndisp, ktrace = _window_sums(cc, kt)
@@ -272,12 +275,26 @@ def pmc_child(args, rt):
     kw = dict(adaptive=args.adaptive, min_samples=args.min_samples, max_depth=args.max_depth, kernel=kernel,
               traversal=traversal_of(args, rt))
     rt.render(dscene, g, host.camera, 0, rt.options(W, H, 8, **kw))
+    print("[bench pmc child] warm-up call done", file=sys.stderr, flush=True)
     rgba = ctypes.c_void_p()
     rt.check(rt.lib().rt_device_alloc(ctypes.byref(rgba), W * H * 4))
     rt.check(rt.lib().rt_synchronize())
     before = int(g.download()[2].sum(dtype=np.int64))
     rt.check(rt.lib().rt_tonemap(g.g, rgba, W, H, None))
+    # the profiled call (a heartbeat on stderr meanwhile: under the counters a
+    # 256-pass call runs for minutes)
+    import threading
+
+    done = threading.Event()
+
+    def heartbeat():
+        while not done.wait(30.0):
+            print("[bench pmc child] profiled call running", file=sys.stderr, flush=True)
+
+    threading.Thread(target=heartbeat, daemon=True).start()
     rt.render(dscene, g, host.camera, 1, rt.options(W, H, args.passes, **kw))
+    done.set()
+    print(f"[bench pmc child] profiled call of {args.passes} passes done", file=sys.stderr, flush=True)
     rt.check(rt.lib().rt_synchronize())
     rt.check(rt.lib().rt_tonemap(g.g, rgba, W, H, None))
     rt.check(rt.lib().rt_synchronize())

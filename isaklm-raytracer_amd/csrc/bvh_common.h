@@ -14,18 +14,39 @@ RT_HD float rt_ray_margin(float ox, float oy, float oz, float scale)
     return 0x1p-16f * (fabsf(ox) + fabsf(oy) + fabsf(oz) + 2.0f * scale);
 }
 
+// whether v is one of the sorted values vals[lo, hi) (float ==: -0 == +0)
+RT_HD bool rt_sorted_contains(const float *vals, int lo, int hi, float v)
+{
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        const float m = vals[mid];
+        if (m == v) return true;
+        if (m < v) lo = mid + 1;
+        else hi = mid;
+    }
+    return false;
+}
+
 // Whether the bound applies to this ray.  The skip rule needs every KD
 // split distance t = (split - o) / d to be a number (+-inf allowed): then
-// the exits inside a near subtree never exceed its split distance.  A
-// direction component of exactly 0 makes t = 0 / 0 = NaN for a ray lying in a
-// split plane; the reference then pushes with NaN, and later pushes inside
-// that subtree can carry exits beyond the split (its leaf order is no longer
-// front to back).  Such rays (and non-finite ones) take the plain KD
-// traversal.
-RT_HD bool rt_bounded_ray(Vec3D o, Vec3D d)
+// the exits inside a near subtree never exceed its split distance.  Only a
+// ray lying IN a split plane (direction component exactly 0, origin
+// coordinate == the split value) makes t = 0 / 0 = NaN; the reference then
+// pushes with NaN, and later pushes inside that subtree can carry exits
+// beyond the split (its leaf order is no longer front to back).  So a ray
+// with a zero component is checked against the tree's split values on that
+// axis (`splits`: per axis sorted, `off[a]..off[a+1]`); one lying in a split
+// plane (and any non-finite ray) takes the plain KD traversal.  About 0.2 % of
+// room2m's rays have a zero component; lying in a split plane is rarer still.
+RT_HD bool rt_bounded_ray(Vec3D o, Vec3D d, const float *splits, const int *off)
 {
-    return fabsf(d.x) > 0.0f && fabsf(d.y) > 0.0f && fabsf(d.z) > 0.0f && o.x - o.x == 0.0f && o.y - o.y == 0.0f &&
-           o.z - o.z == 0.0f && d.x - d.x == 0.0f && d.y - d.y == 0.0f && d.z - d.z == 0.0f;
+    if (!(o.x - o.x == 0.0f && o.y - o.y == 0.0f && o.z - o.z == 0.0f && d.x - d.x == 0.0f && d.y - d.y == 0.0f &&
+          d.z - d.z == 0.0f))
+        return false;
+    if (d.x == 0.0f && rt_sorted_contains(splits, off[0], off[1], o.x)) return false;
+    if (d.y == 0.0f && rt_sorted_contains(splits, off[1], off[2], o.y)) return false;
+    if (d.z == 0.0f && rt_sorted_contains(splits, off[2], off[3], o.z)) return false;
+    return true;
 }
 
 // Slab test of a box grown by the ray's margin: om = o + margin, op = o -

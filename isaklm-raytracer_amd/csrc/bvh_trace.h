@@ -107,7 +107,7 @@ __device__ __forceinline__ int trace_bvh(const RtDevScene &sc, const Vec3D o, co
     if (!bbox_hit(sc, o, d, entry, exit_)) return -1;
     const float root_exit = exit_;
     float s_min = -INFINITY; // (the plain KD traversal)
-    if (rt_bounded_ray(o, d)) {
+    if (rt_bounded_ray(o, d, sc.split_vals, sc.split_off)) {
         s_min = bvh_bound<COUNT>(sc, o, d, exit_, stk, c);
         if (!(s_min < root_exit)) return -1;
     }

@@ -62,6 +62,8 @@ struct PreparedHost {
     std::vector<RtF4> bvh_a;              // BVH leaf-slot order
     std::vector<RtIsectBary> bvh_bary;    // BVH leaf-slot order
     float bvh_scale = 0.0f;
+    std::vector<float> split_vals;        // per axis sorted, unique (rt_bounded_ray)
+    int split_off[4] = {0, 0, 0, 0};
     int bvh_depth = -1, bvh_always = 0, bvh_dropped = 0;
 };
 int prepare_host(const Triangle *tris, int ntris, const KD_Tree_Node *nodes, int nnodes, const int *indices,

@@ -12,6 +12,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <map>
 #include <string>
 #include <vector>
@@ -195,6 +196,27 @@ int prepare_host(const Triangle *tris, int ntris, const KD_Tree_Node *nodes, int
         out.bvh_dropped = bvh.dropped;
     } else if (brc != RT_OK && brc != RT_E_UNSUPPORTED) {
         return brc;
+    }
+    // the KD split values per axis, sorted (bvh_common.h rt_bounded_ray); a
+    // NaN split makes t NaN for every ray that reaches it: no bound then
+    {
+        std::vector<float> ax[3];
+        bool nan_split = false;
+        for (int k = 0; k < nnodes; ++k)
+            if (!nodes[k].is_leaf_node) {
+                const float v = nodes[k].plane_offset;
+                if (v != v) nan_split = true;
+                else ax[nodes[k].plane_axis].push_back(v);
+            }
+        out.split_vals.clear();
+        for (int a = 0; a < 3; ++a) {
+            std::sort(ax[a].begin(), ax[a].end());
+            ax[a].erase(std::unique(ax[a].begin(), ax[a].end()), ax[a].end());
+            out.split_off[a] = (int)out.split_vals.size();
+            out.split_vals.insert(out.split_vals.end(), ax[a].begin(), ax[a].end());
+        }
+        out.split_off[3] = (int)out.split_vals.size();
+        if (nan_split) out.bvh_depth = -1;
     }
 
     // --- lights: one padding entry for the xi == 1.0 draw -----

@@ -94,6 +94,8 @@ struct RtDevScene {
     const RtF4 *bvh_a;          // per BVH leaf slot: plane (as isect_a)
     const RtIsectBary *bvh_bary; // per BVH leaf slot: barycentric-test record (as isect_bary)
     float bvh_scale;            // largest |vertex|_1 (rt_ray_margin)
+    const float *split_vals;    // the KD tree's split values, per axis sorted (rt_bounded_ray)
+    int split_off[4];           // axis a: split_vals[split_off[a], split_off[a + 1])
 };
 
 // BVH child reference: an inner node's index, or RT_BVH_LEAF | first << 3 |

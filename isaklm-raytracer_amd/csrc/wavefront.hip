@@ -19,6 +19,7 @@
 #include <time.h>
 
 #include <algorithm>
+#include <chrono>
 #include <atomic>
 #include <map>
 #include <mutex>
@@ -880,14 +881,19 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_BVH_WAVES) wf_finish_bvh(RtDevSce
             }
         }
         if (!__any(active)) break; // every lane exhausted
+        bool to_long = false;
         if (active) {
             float bx = 0.0f, by = 0.0f, bz = 0.0f;
             const int hit = trace_bvh<false>(sc, p.ro, p.rd, bx, by, bz, stk, c);
-            if (!shade_step<false>(sc, fr, cam, p, hit, bx, by, bz, limit, c)) {
+            const bool want = shade_step<false>(sc, fr, cam, p, hit, bx, by, bz, limit, c);
+            // a path deeper than long_depth goes on in wf_long (64 lanes per ray)
+            to_long = want && st.long_depth > 0 && p.depth > st.long_depth;
+            if (!want || to_long) {
                 store_regs(st, fr, p);
                 active = false;
             }
         }
+        if (__any(to_long)) publish_long(st, to_long, p.slot, p.ro, p.rd);
     }
 }
 
@@ -1026,10 +1032,8 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_FIN_OCC) wf_finish_coop(RtDevScen
 // published) drains what is left.
 template <bool COUNT>
 __global__ void __launch_bounds__(WF_BLOCK, WF_LONG_WAVES) wf_long(RtDevScene sc, RtDevFrame fr, RtDevCamera cam, WfState st,
-                                                    int final_slice, int bvh)
+                                                    int final_slice)
 {
-    __shared__ uint32_t s_bnode[WF_BVH_LDS * WF_BLOCK]; // bounded traversal stacks (lane 0 of each wave)
-    __shared__ float s_bentry[WF_BVH_LDS * WF_BLOCK];
     __shared__ WideItem s_wide[(WF_BLOCK / 64) * WIDE_CAP];
     __shared__ unsigned long long s_key[(WF_BLOCK / 64) * 4];
     __shared__ int s_mark[2 * WF_BLOCK]; // 128 per wave: chunk_owner marks + junk slots
@@ -1082,7 +1086,6 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_LONG_WAVES) wf_long(RtDevScene sc
         PathRegs p;
         p.slot = 0;
         p.ro = p.rd = rt_v3(0, 0, 0);
-        int want_more = 1;
         if (lane == 0) {
             load_regs(st, fr, flag - 1u, p);
             p.ro = ld3(ldf4(st.long_ray + 2 * (size_t)e));
@@ -1091,16 +1094,6 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_LONG_WAVES) wf_long(RtDevScene sc
         while (true) {
             int hit = -1;
             float bx = 0.0f, by = 0.0f, bz = 0.0f;
-            if (!COUNT && bvh) { // the bounded traversal by lane 0 alone
-                if (lane == 0) {
-                    Stack<WF_BVH_LDS> stk{s_bnode + threadIdx.x, s_bentry + threadIdx.x, WF_BLOCK,
-                                          st.spill + blockIdx.x * WF_BLOCK + threadIdx.x, st.spill_threads};
-                    hit = trace_bvh<false>(sc, p.ro, p.rd, bx, by, bz, stk, c);
-                    if (!shade_step<COUNT>(sc, fr, cam, p, hit, bx, by, bz, limit, c)) want_more = 0;
-                }
-                if (!__shfl(want_more, 0)) break;
-                continue;
-            }
             CoopRay r;
             coop_idle(r);
             if (lane == 0) {
@@ -1140,6 +1133,7 @@ struct Pipe {
     uint32_t *host_count = nullptr;
     hipEvent_t ev[6] = {};   // RtOptions.profile
     hipEvent_t join = nullptr;
+    hipEvent_t fin_done = nullptr; // after the finisher (the host polls it while kicking wf_long slices)
     bool joined = false; // join recorded by a previous call
     RtProfile prof{};
 };
@@ -1178,6 +1172,7 @@ int ensure_streams(Workspace &w, int npipes)
         if (hipStreamCreateWithFlags(&p.stream, hipStreamNonBlocking) != hipSuccess) return -1;
         if (hipHostMalloc((void **)&p.host_count, 64) != hipSuccess) return -1;
         if (hipEventCreateWithFlags(&p.join, hipEventDisableTiming) != hipSuccess) return -1;
+        if (hipEventCreateWithFlags(&p.fin_done, hipEventDisableTiming) != hipSuccess) return -1;
         for (auto &e : p.ev)
             if (hipEventCreate(&e) != hipSuccess) return -1;
         hipLaunchKernelGGL(wf_bind_stream, dim3(1), dim3(64), 0, p.stream);
@@ -1315,8 +1310,8 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
                                                      traversal == RT_TRAVERSAL_BOUNDED_COUNTED);
     // ... and the tail finisher too (RT_WF_FIN_BVH=0: the cooperative KD finisher; experiments)
     static const bool fin_bvh = !getenv("RT_WF_FIN_BVH") || atoi(getenv("RT_WF_FIN_BVH")) != 0;
-    // long paths (wf_long): one lane's bounded traversal instead of 64 lanes' wide KD one (RT_WF_LONG_BVH=1; experiments)
-    static const bool long_bvh = getenv("RT_WF_LONG_BVH") && atoi(getenv("RT_WF_LONG_BVH")) != 0;
+    // (wf_long keeps the 64-lane wide KD traversal: one lane's bounded traversal per long path measured
+    // 13 % slower per call, profiles/r03/bounded_ab.json)
     const int tiles = ((fr.width + 15) / 16) * ((fr.height + 15) / 16);
     int npipes = pipes_opt > 0 ? pipes_opt : WF_PIPES_DEFAULT;
     npipes = npipes > WF_MAX_PIPES ? WF_MAX_PIPES : npipes;
@@ -1381,10 +1376,9 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
         }
         const int fin = final ? 1 : 0;
         if (count)
-            hipLaunchKernelGGL(wf_long<true>, dim3(WF_LONG_BLOCKS), dim3(WF_BLOCK), 0, stream, sc, fr, cam, lst, fin, 0);
+            hipLaunchKernelGGL(wf_long<true>, dim3(WF_LONG_BLOCKS), dim3(WF_BLOCK), 0, stream, sc, fr, cam, lst, fin);
         else
-            hipLaunchKernelGGL(wf_long<false>, dim3(WF_LONG_BLOCKS), dim3(WF_BLOCK), 0, stream, sc, fr, cam, lst, fin,
-                               bounded && long_bvh ? 1 : 0);  // (counting calls: the KD wide traversal)
+            hipLaunchKernelGGL(wf_long<false>, dim3(WF_LONG_BLOCKS), dim3(WF_BLOCK), 0, stream, sc, fr, cam, lst, fin);
         if (hipGetLastError() != hipSuccess) return -1;
         long_final = final;
         if (hipEventRecord(w.long_ev, stream) != hipSuccess) return -1;
@@ -1455,10 +1449,27 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
             return 0;
         };
         int rc = 0;
+        // the bounded finisher publishes deep paths to wf_long too: its pipeline
+        // is a producer until the finisher is done (meanwhile wf_long slices are
+        // kicked as they end; the last producer queues the final slice)
+        auto finish_and_release = [&](int qq, uint32_t live) -> int {
+            const bool publishes = bounded && fin_bvh && long_depth > 0;
+            if (!publishes && producer_done(pi) != 0) return -1;
+            if (finish(qq, live) != 0) return -1;
+            if (!publishes) return 0;
+            if (hipEventRecord(pp.fin_done, s) != hipSuccess) return -1;
+            while (true) {
+                const hipError_t e = hipEventQuery(pp.fin_done);
+                if (e == hipSuccess) break;
+                if (e != hipErrorNotReady) return -1;
+                if (kick_long(false) != 0) return -1;
+                std::this_thread::sleep_for(std::chrono::microseconds(200));
+            }
+            return producer_done(pi);
+        };
         if (trace_kind == 1 && tail > slots) {
             // wf_tail above the frame size: the whole call runs in the finisher (no queue iterations)
-            if (producer_done(pi) != 0) return -1;
-            rc = finish(0, (uint32_t)slots);
+            rc = finish_and_release(0, (uint32_t)slots);
         } else {
             for (int it = 0;; ++it) {
                 const int q = it & 1;
@@ -1509,8 +1520,8 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
                 }
                 if (kick_long(false) != 0) return -1; // paths published by this shade launch
                 if (live == 0 || live < tail) {
-                    if (producer_done(pi) != 0) return -1;
-                    if (live != 0) rc = finish(q ^ 1, live);
+                    if (live != 0) rc = finish_and_release(q ^ 1, live);
+                    else if (producer_done(pi) != 0) return -1;
                     break;
                 }
             }
