@@ -98,14 +98,15 @@ def traversal_of(args, rt):
     return rt.TRAVERSAL_BOUNDED if args.traversal == "bounded" else rt.TRAVERSAL_KD
 
 
-def bounded_trace_bytes(c):
-    """Bytes the bounded queue trace kernel's algorithm reads / writes
-    (counters of a RT_TRAVERSAL_BOUNDED_COUNTED call; DESIGN.md "Roofline"):
-    per ray its 32-B ray and 16-B hit record, 64 B per BVH node (both child
-    boxes), 16 B per plane test (BVH or KD), 56 B per barycentric record
-    read, 8 B per KD node."""
-    return (48 * c["ray"] + 64 * c["b_bvh_node"] + 16 * (c["b_bvh_tri"] + c["tri"]) + 56 * c["b_bary"] +
-            8 * c["node"])
+def bounded_kernel_bytes(c):
+    """Bytes the bounded finisher's algorithm reads / writes (counters of a
+    RT_TRAVERSAL_BOUNDED_COUNTED call; DESIGN.md "Roofline"): per ray query
+    64 B per BVH node (both child boxes), 16 B per plane test (BVH or KD),
+    56 B per barycentric record read, 8 B per KD node; per hit its 112-B
+    shading record and 64-B material; per sample the pixel's fb / sq / count
+    read and written (40 B)."""
+    return (64 * c["b_bvh_node"] + 16 * (c["b_bvh_tri"] + c["tri"]) + 56 * c["b_bary"] + 8 * c["node"] +
+            176 * c["hit"] + 40 * c["sample"])
 
 
 def call_steps(args):
@@ -576,35 +577,46 @@ def main(argv=None, binding=None):
         launches = sum(p["trace_launches"] for p in profiles)
         avg_launch_ms = sum(p["trace_ms"] for p in profiles) / max(launches, 1)
         if bounded:
-            # the dominant kernel's own work: one more call, the bounded queue
-            # trace kernel counting (RT_TRAVERSAL_BOUNDED_COUNTED)
+            # the dominant kernel (the bounded finisher runs the whole call, one
+            # launch per pipeline) and its own work: one more call with the
+            # kernels counting (RT_TRAVERSAL_BOUNDED_COUNTED)
+            # (the timed calls' shape: passes x steps-per-call, so its bytes per
+            # launch and the timed launches' duration describe the same launch)
             bcnt = rt.DeviceCounters()
-            rt.render(dscene, gb, host.camera, 1, rt.options(W, H, P, counters=bcnt.p, profile=True,
+            cp = P * call_steps(args)
+            rt.render(dscene, gb, host.camera, 1, rt.options(W, H, cp, counters=bcnt.p, profile=True,
                                                              **dict(render_kw, traversal=rt.TRAVERSAL_BOUNDED_COUNTED)))
             bc = bcnt.read(finisher=True)
             cprof = rt.last_profile()
-            trace_bytes = bounded_trace_bytes(bc)
-            kname = "wf_trace_bvh<false>"
+            trace_bytes = bounded_kernel_bytes(bc)
+            kname = "wf_finish_bvh<false>"
+            launches = sum(p["finish_launches"] for p in profiles)
+            avg_launch_ms = sum(p["finish_ms"] for p in profiles) / max(launches, 1)
+            counted_launches = cprof["finish_launches"]
             work = {"rays": bc["ray"], "bvh_nodes_per_ray": round(bc["b_bvh_node"] / max(bc["ray"], 1), 2),
                     "bvh_tests_per_ray": round(bc["b_bvh_tri"] / max(bc["ray"], 1), 2),
                     "kd_nodes_per_ray": round(bc["node"] / max(bc["ray"], 1), 2),
                     "kd_tests_per_ray": round(bc["tri"] / max(bc["ray"], 1), 2),
                     "bary_per_ray": round(bc["b_bary"] / max(bc["ray"], 1), 2),
-                    "bytes_per_ray": round(trace_bytes / max(bc["ray"], 1), 1),
-                    "counted_call_passes": P}
+                    "rays_per_sample": round(bc["ray"] / max(bc["sample"], 1), 3),
+                    "bytes_per_sample": round(trace_bytes / max(bc["sample"], 1), 1),
+                    "counted_call_passes": cp,
+                    "scope": "the finisher's paths; the deep paths handed to wf_long (depth > 64) are not counted"}
         else:
             cprof = rt.last_profile()
             trace_bytes = 8 * (c["node"] - c["finish_node"]) + 40 * (c["tri"] - c["finish_tri"])
             kname = "wf_trace_coop<false>"
+            counted_launches = cprof["trace_launches"]
             work = {}
-        bytes_per_launch = trace_bytes / max(cprof["trace_launches"], 1)
+        bytes_per_launch = trace_bytes / max(counted_launches, 1)
         kernel_detail = {
             "kernel": kname,
             "pipelines": cprof["pipelines"],
-            "trace_launches_per_call": launches / max(len(profiles), 1),
+            "launches_per_call": launches / max(len(profiles), 1),
             "avg_launch_ms": round(avg_launch_ms, 4),
             "algorithmic_bytes_per_launch": round(bytes_per_launch),
-            "algorithmic_GBps_per_launch": round(bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9, 1),
+            "algorithmic_GBps_per_launch": (round(bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9, 1)
+                                            if avg_launch_ms > 0 else None),
             "trace_union_ms_per_call": round(float(np.mean([p["trace_union_ms"] for p in profiles])), 3),
             "trace_ms_per_call": round(float(np.mean([p["trace_ms"] for p in profiles])), 3),
             "shade_ms_per_call": round(float(np.mean([p["shade_ms"] for p in profiles])), 3),

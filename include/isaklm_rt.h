@@ -435,7 +435,7 @@ typedef struct RtOptions {
      * RT_TRAVERSAL_BOUNDED_COUNTED: the wavefront queue trace launches then
      * run the bounded traversal and count its own work (RT_CNT_RAY, _NODE,
      * _TRI, _HIT, RT_CNT_B_*; measurement: the finisher and the long-path
-     * kernel are not counted).  The megakernel always runs the KD traversal. */
+     * kernel are not counted; the megakernel then runs its counting KD build). */
     int traversal;
 } RtOptions;
 

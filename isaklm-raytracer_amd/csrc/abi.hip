@@ -18,7 +18,7 @@
 #include "host/rt_host.h"
 
 int rt_launch_path(const RtDevScene &sc, const RtDevFrame &fr, const RtDevCamera &cam, int stack_depth,
-                   hipStream_t stream);
+                   hipStream_t stream, int traversal);
 int rt_launch_tonemap(const Vec3D *fb, const int *count, RtUChar4 *out, int n, hipStream_t stream);
 int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevCamera &cam, hipStream_t stream,
                         int variant, int tail, int finish_waves, int profile, int cap, int postpone, int wide,
@@ -715,7 +715,7 @@ int rt_render(rt_scene_t scene, G_Buffer g, Camera cam, int sample_count, const 
             rt_set_error("rt_render: wavefront launch failed: %s", hipGetErrorString(hipGetLastError()));
             return RT_E_HIP;
         }
-    } else if (rt_launch_path(scene->dev, fr, dc, scene->max_depth, stream) != 0) {
+    } else if (rt_launch_path(scene->dev, fr, dc, scene->max_depth, stream, o.traversal) != 0) {
         rt_set_error("rt_render: kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
         return RT_E_HIP;
     }

@@ -26,17 +26,46 @@
 
 namespace rtk {
 
-// one triangle test of intersect_triangle + calculate_barycentric_coordinates
-// (rt/trace_ray.cuh:48-113) on precomputed records: the same operations as
-// trace()'s leaf loop; true and s when it passes with s < closest
+// The tests of leaf entries [e0, e1) in order (trace_leaf_node,
+// rt/trace_ray.cuh:115-172: intersect_triangle + calculate_barycentric_
+// coordinates, :48-113, on precomputed records): an entry passes with
+// dn != 0, s >= 1e-5, s < smallest and barycentrics in [0, 1], and then
+// becomes the smallest.  The plane records are loaded 4 at a time (a leaf
+// costs a few load round trips instead of one per entry), the plane test is
+// pre-screened against the smallest at the start of the chunk (a superset)
+// and re-checked in entry order against the running smallest — the
+// reference's result.  Returns the passing entry that is the smallest (-1: none) and its
+// barycentric coordinates.
 template <bool COUNT>
-__device__ __forceinline__ bool tri_test(const RtF4 *plane, const RtIsectBary *bary, uint32_t e, Vec3D o, Vec3D d,
-                                         float closest, float &s, float &cx, float &cy, float &cz, Cnt &c)
+__device__ __forceinline__ int leaf_scan(const RtF4 *plane, const RtIsectBary *bary, uint32_t e0, uint32_t e1, Vec3D o,
+                                         Vec3D d, float &smallest, float &bx, float &by, float &bz, Cnt &c)
 {
-    if (!rt_tri_plane(ldf4(plane + e), o, d, closest, s)) return false;
-    if (COUNT) c.v[RT_CNT_B_BARY]++;
-    return rt_tri_bary(ldf4(&bary[e].b), ldf4(&bary[e].c), ldf4(&bary[e].d), as_float(bary[e].rd), o, d, s, cx, cy,
-                       cz);
+    int best = -1;
+    for (uint32_t e = e0; e < e1; e += 4) {
+        float s[4];
+        bool p[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const bool in = e + k < e1;
+            const RtF4 A = ldf4(plane + (in ? e + k : e));
+            p[k] = rt_tri_plane(A, o, d, smallest, s[k]) && in;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (!p[k] || !(s[k] < smallest)) continue;
+            if (COUNT) c.v[RT_CNT_B_BARY]++;
+            float cx, cy, cz;
+            if (rt_tri_bary(ldf4(&bary[e + k].b), ldf4(&bary[e + k].c), ldf4(&bary[e + k].d),
+                            as_float(bary[e + k].rd), o, d, s[k], cx, cy, cz)) {
+                smallest = s[k];
+                best = (int)(e + k);
+                bx = cx;
+                by = cy;
+                bz = cz;
+            }
+        }
+    }
+    return best;
 }
 
 // s_min of step 2: the smallest s < best of any passing test (best if none)
@@ -70,11 +99,9 @@ __device__ __forceinline__ float bvh_bound(const RtDevScene &sc, Vec3D o, Vec3D 
             }
         } else {
             const uint32_t first = (cur & ~RT_BVH_LEAF) >> 3, end = first + (cur & 7u) + 1u;
-            for (uint32_t e = first; e < end; ++e) {
-                float s, cx, cy, cz;
-                if (COUNT) cn.v[RT_CNT_B_BVH_TRI]++;
-                if (tri_test<COUNT>(sc.bvh_a, sc.bvh_bary, e, o, d, best, s, cx, cy, cz, cn)) best = s;
-            }
+            if (COUNT) cn.v[RT_CNT_B_BVH_TRI] += end - first;
+            float bx, by, bz;
+            (void)leaf_scan<COUNT>(sc.bvh_a, sc.bvh_bary, first, end, o, d, best, bx, by, bz, cn);
         }
         // pop the next subtree that may still hold a smaller s
         bool more = false;
@@ -149,19 +176,10 @@ __device__ __forceinline__ int trace_bvh(const RtDevScene &sc, const Vec3D o, co
         if (count > 0 && exit_ > s_min) {
             // trace_leaf_node (:115-172): closest starts at the leaf's exit
             float smallest = exit_;
-            int best = -1;
             float bx = 0.0f, by = 0.0f, bz = 0.0f;
-            for (uint32_t e = nd.x; e < nd.x + count; ++e) {
-                float s, cx, cy, cz;
-                if (COUNT) c.v[RT_CNT_TRI]++;
-                if (tri_test<COUNT>(sc.isect_a, sc.isect_bary, e, o, d, smallest, s, cx, cy, cz, c)) {
-                    smallest = s;
-                    best = (int)sc.isect_bary[e].tri;
-                    bx = cx;
-                    by = cy;
-                    bz = cz;
-                }
-            }
+            if (COUNT) c.v[RT_CNT_TRI] += count;
+            const int be = leaf_scan<COUNT>(sc.isect_a, sc.isect_bary, nd.x, nd.x + count, o, d, smallest, bx, by, bz, c);
+            const int best = be >= 0 ? (int)sc.isect_bary[be].tri : -1;
             if (best >= 0) {
                 if (COUNT) c.v[RT_CNT_HIT]++;
                 hbx = bx;

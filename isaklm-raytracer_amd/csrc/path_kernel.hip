@@ -19,16 +19,29 @@
 //  * KD stack (node, entry t) in LDS, [depth][lane] => conflict-free.
 #include <hip/hip_runtime.h>
 
+#include <map>
+#include <mutex>
+
+#include "bvh_trace.h"
 #include "rt_kernels.h"
 
 #define RT_BLOCK 256
+#ifndef RT_MEGA_BVH_LDS
+#define RT_MEGA_BVH_LDS 12 // bounded megakernel: stack entries in LDS; deeper ones spill to HBM
+#endif
+#ifndef RT_MEGA_BVH_WAVES
+#define RT_MEGA_BVH_WAVES 6
+#endif
 
 using namespace rtk;
 
 // path_tracing (rt/path_tracing.cuh:338-395) for `passes` passes, with
 // reset_frame (rt/render.cuh:18-34) fused in when fr.reset is set.
-template <bool COUNT, int STACK>
-__global__ void __launch_bounds__(RT_BLOCK, STACK <= RT_STACK_SMALL ? 4 : 2) rt_path_kernel(RtDevScene sc, RtDevFrame fr, RtDevCamera cam)
+// BOUNDED: the BVH-bounded traversal (bvh_trace.h), stack entries past STACK
+// in `spill` (spill_threads entries apart, indexed by the global thread id)
+template <bool COUNT, int STACK, bool BOUNDED>
+__global__ void __launch_bounds__(RT_BLOCK, BOUNDED ? RT_MEGA_BVH_WAVES : (STACK <= RT_STACK_SMALL ? 4 : 2))
+    rt_path_kernel(RtDevScene sc, RtDevFrame fr, RtDevCamera cam, uint2 *spill, int spill_threads)
 {
     __shared__ uint32_t s_node[STACK * RT_BLOCK];
     __shared__ float s_entry[STACK * RT_BLOCK];
@@ -40,7 +53,8 @@ __global__ void __launch_bounds__(RT_BLOCK, STACK <= RT_STACK_SMALL ? 4 : 2) rt_
     const int y = (tile / tiles_x) * 16 + (wave >> 1) * 8 + (lane >> 3);
     const bool valid = x < fr.width && y < fr.height && rt_row_owned(fr, y);
     const int pi = valid ? y * fr.width + x : 0;
-    Stack<STACK> stk{s_node + tid, s_entry + tid, RT_BLOCK, nullptr, 0};
+    Stack<STACK> stk{s_node + tid, s_entry + tid, RT_BLOCK,
+                     BOUNDED ? spill + (size_t)blockIdx.x * RT_BLOCK + tid : nullptr, spill_threads};
 
     Cnt c;
     unsigned long long t_start = 0;
@@ -105,7 +119,8 @@ __global__ void __launch_bounds__(RT_BLOCK, STACK <= RT_STACK_SMALL ? 4 : 2) rt_
         } else {
             if (!shadow) ++depth;
             float bx = 0.0f, by = 0.0f, bz = 0.0f;
-            const int hit = trace<COUNT>(sc, ro, rd, bx, by, bz, stk, c);
+            const int hit = BOUNDED ? trace_bvh<false>(sc, ro, rd, bx, by, bz, stk, c)
+                                    : trace<COUNT>(sc, ro, rd, bx, by, bz, stk, c);
             bool roulette = true;
             if (!shadow) {
                 if (hit < 0) {
@@ -195,18 +210,60 @@ __global__ void __launch_bounds__(256) rt_tonemap_kernel(const Vec3D *fb, const 
 }
 
 // ---- host launchers (called by abi.hip) ----
+namespace {
+// per-device spill area of the bounded megakernel (grown on demand)
+std::mutex g_spill_mu;
+std::map<int, std::pair<uint2 *, size_t>> g_spill;
+
+uint2 *mega_spill(size_t entries)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> g(g_spill_mu);
+    auto &e = g_spill[dev];
+    if (e.second < entries) {
+        if (e.first) (void)hipFree(e.first);
+        e.first = nullptr;
+        e.second = 0;
+        void *p = nullptr;
+        if (hipMalloc(&p, entries * sizeof(uint2)) != hipSuccess) return nullptr;
+        e.first = (uint2 *)p;
+        e.second = entries;
+    }
+    return e.first;
+}
+} // namespace
+
 int rt_launch_path(const RtDevScene &sc, const RtDevFrame &fr, const RtDevCamera &cam, int stack_depth,
-                   hipStream_t stream)
+                   hipStream_t stream, int traversal)
 {
     const int tiles = ((fr.width + 15) / 16) * ((fr.height + 15) / 16);
     dim3 grid(tiles), block(RT_BLOCK);
     const bool count = fr.counters != nullptr;
+    if (!count && traversal == RT_TRAVERSAL_BOUNDED && sc.bvh_nodes != nullptr) {
+        // the bounded traversal: the KD part needs <= RT_STACK_DEPTH entries, the BVH part <= RT_BVH_STACK
+        const size_t threads = (size_t)tiles * RT_BLOCK;
+        const int deeper = (RT_BVH_STACK > RT_STACK_DEPTH ? RT_BVH_STACK : RT_STACK_DEPTH) - RT_MEGA_BVH_LDS;
+        uint2 *spill = mega_spill(threads * (size_t)deeper);
+        if (!spill) return -1;
+        hipLaunchKernelGGL((rt_path_kernel<false, RT_MEGA_BVH_LDS, true>), grid, block, 0, stream, sc, fr, cam, spill,
+                           (int)threads);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
     if (stack_depth <= RT_STACK_SMALL) {
-        if (count) hipLaunchKernelGGL((rt_path_kernel<true, RT_STACK_SMALL>), grid, block, 0, stream, sc, fr, cam);
-        else hipLaunchKernelGGL((rt_path_kernel<false, RT_STACK_SMALL>), grid, block, 0, stream, sc, fr, cam);
+        if (count)
+            hipLaunchKernelGGL((rt_path_kernel<true, RT_STACK_SMALL, false>), grid, block, 0, stream, sc, fr, cam,
+                               nullptr, 0);
+        else
+            hipLaunchKernelGGL((rt_path_kernel<false, RT_STACK_SMALL, false>), grid, block, 0, stream, sc, fr, cam,
+                               nullptr, 0);
     } else {
-        if (count) hipLaunchKernelGGL((rt_path_kernel<true, RT_STACK_DEPTH>), grid, block, 0, stream, sc, fr, cam);
-        else hipLaunchKernelGGL((rt_path_kernel<false, RT_STACK_DEPTH>), grid, block, 0, stream, sc, fr, cam);
+        if (count)
+            hipLaunchKernelGGL((rt_path_kernel<true, RT_STACK_DEPTH, false>), grid, block, 0, stream, sc, fr, cam,
+                               nullptr, 0);
+        else
+            hipLaunchKernelGGL((rt_path_kernel<false, RT_STACK_DEPTH, false>), grid, block, 0, stream, sc, fr, cam,
+                               nullptr, 0);
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

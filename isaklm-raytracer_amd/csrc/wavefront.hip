@@ -78,6 +78,9 @@ static_assert(WF_BLOCK % WF_TBLOCK == 0 && WF_TBLOCK % 64 == 0, "WF_TBLOCK must 
 #ifndef WF_BVH_WAVES
 #define WF_BVH_WAVES 6  // wf_trace_bvh occupancy target
 #endif
+#ifndef WF_FIN_BVH_WAVES
+#define WF_FIN_BVH_WAVES 6 // wf_finish_bvh occupancy target
+#endif
 // per-thread spill entries: the deeper of the KD stack (past WF_LDS_STACK) and the BVH stack (past WF_BVH_LDS)
 #define WF_SPILL_ENTRIES \
     ((RT_STACK_DEPTH - WF_LDS_STACK) > (RT_BVH_STACK - WF_BVH_LDS) ? (RT_STACK_DEPTH - WF_LDS_STACK) \
@@ -115,6 +118,18 @@ struct WfState {
     RtF4 *long_ray;       // 2 per entry
     uint32_t *long_ctr;   // [0] entries reserved, [1] entries claimed, [3] paths running in wf_long
     int long_depth;       // 0 = off
+    uint32_t long_cap;    // entries of long_flag / long_ray (the pixels)
+    // whole-call finisher (bounded traversal): wf_long runs a handed-over path
+    // only to the end of its SAMPLE and returns the pixel through this ring to
+    // the finishers, whose lanes run its remaining passes
+    int long_return;
+    unsigned long long *ret_ring; // entry e at e % long_cap: (e + 1) << 32 | slot once published
+    // ret_ctr: u64 [0] = finisher waves alive << 32 | returns reserved (wf_long
+    // reserves only while a finisher wave is alive; a wave leaves only when
+    // every reserved return is claimed: no pixel is stranded, and neither
+    // kernel ever waits for the other — they may share a hardware queue);
+    // u32 [2] = returns claimed
+    uint32_t *ret_ctr;
 };
 
 namespace {
@@ -171,6 +186,44 @@ __device__ __forceinline__ void publish_long(const WfState &st, bool to_long, ui
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __hip_atomic_store(st.long_flag + e, slot + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+}
+
+// the finisher's hand-off: as publish_long, but the wave reserves its entries
+// with one compare-and-swap that never passes long_cap (a pixel can be handed
+// over several times per call when wf_long returns it after each deep
+// sample).  Returns false (wave-uniform) when the entries would not fit: the
+// lanes then keep their paths.  The path state is stored by the caller first.
+__device__ __forceinline__ bool publish_long_capped(const WfState &st, bool to_long, uint32_t slot, Vec3D o, Vec3D d)
+{
+    const unsigned long long m = __ballot(to_long);
+    const int lane = __lane_id();
+    const int leader = __ffsll((long long)m) - 1;
+    const uint32_t k = (uint32_t)__popcll(m);
+    uint32_t base = 0xffffffffu;
+    if (lane == leader) {
+        uint32_t r = __hip_atomic_load(st.long_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        while (r + k <= st.long_cap) {
+            if (__hip_atomic_compare_exchange_strong(st.long_ctr, &r, r + k, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT)) {
+                base = r;
+                break;
+            }
+        }
+    }
+    base = (uint32_t)__shfl((int)base, leader);
+    if (base == 0xffffffffu) return false;
+    const uint32_t e = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+    if (to_long) {
+        st.long_ray[2 * (size_t)e] = RtF4{o.x, o.y, o.z, 0.0f};
+        st.long_ray[2 * (size_t)e + 1] = RtF4{d.x, d.y, d.z, 0.0f};
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (to_long) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(st.long_flag + e, slot + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return true;
 }
 
 // start the pixel's next pass(es): adaptive test, camera ray.  Returns true
@@ -842,10 +895,15 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_finish(RtDevScene sc, RtDevFrame 
     }
 }
 
-// Tail finisher with the BVH-bounded traversal (bvh_trace.h): every lane runs
-// one path to the end of its pixel's passes (trace + shade in registers) and
-// then takes the next queued path (wave-aggregated atomic on counts[4]).
-__global__ void __launch_bounds__(WF_BLOCK, WF_BVH_WAVES) wf_finish_bvh(RtDevScene sc, RtDevFrame fr, RtDevCamera cam,
+// Finisher with the BVH-bounded traversal (bvh_trace.h): every lane runs one
+// path to the end of its pixel's passes (trace + shade in registers,
+// megakernel style) and then takes the next queued path (wave-aggregated
+// atomic on counts[4]); a path deeper than long_depth goes on in wf_long.
+// With the bounded traversal this runs the WHOLE call (wf_start's path list:
+// no queue iterations), see rt_launch_wavefront.  COUNT: the traversal's own
+// work (trace_bvh) and the reference's shading counters.
+template <bool COUNT>
+__global__ void __launch_bounds__(WF_BLOCK, WF_FIN_BVH_WAVES) wf_finish_bvh(RtDevScene sc, RtDevFrame fr, RtDevCamera cam,
                                                                        WfState st, int q)
 {
     __shared__ uint32_t s_node[WF_BVH_LDS * WF_BLOCK];
@@ -853,15 +911,20 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_BVH_WAVES) wf_finish_bvh(RtDevSce
     const int tid = threadIdx.x;
     const int gtid = blockIdx.x * WF_BLOCK + tid;
     Stack<WF_BVH_LDS> stk{s_node + tid, s_entry + tid, WF_BLOCK, st.spill + gtid, st.spill_threads};
-    Cnt c; // (unused: the counting build runs wf_finish_coop)
+    Cnt c;
+    if (COUNT) c.zero();
     const uint32_t n = st.counts[6 + q]; // paths of path list q
     uint32_t *fetch = st.counts + 4;
     const int limit = fr.max_depth > 0 ? fr.max_depth : RT_WATCHDOG_BOUNCES;
     const int lane = __lane_id();
+    unsigned long long *const ret_word = reinterpret_cast<unsigned long long *>(st.ret_ctr);
+    uint32_t *const ret_claimed = st.ret_ctr + 2;
+    if (st.long_return && lane == 0) // this wave is alive: wf_long may return pixels to it
+        __hip_atomic_fetch_add(ret_word, 1ull << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     PathRegs p;
     p.slot = 0;
     p.ro = p.rd = rt_v3(0, 0, 0);
-    bool active = false, exhausted = false;
+    bool active = false, exhausted = false; // exhausted: this lane found the path list empty
     while (true) {
         const bool need = !active && !exhausted;
         const unsigned long long m = __ballot(need);
@@ -880,21 +943,68 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_BVH_WAVES) wf_finish_bvh(RtDevSce
                 }
             }
         }
-        if (!__any(active)) break; // every lane exhausted
+        if (st.long_return) {
+            // idle lanes take pixels wf_long returned (one compare-and-swap per wave)
+            const bool idle = !active && exhausted;
+            const unsigned long long im = __ballot(idle);
+            if (im) {
+                const int leader = __ffsll((long long)im) - 1;
+                uint32_t base = 0, got = 0;
+                if (lane == leader) {
+                    uint32_t c0 = __hip_atomic_load(ret_claimed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const uint32_t r =
+                        (uint32_t)__hip_atomic_load(ret_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const uint32_t want_n = (uint32_t)__popcll(im);
+                    const uint32_t take = r > c0 ? (r - c0 < want_n ? r - c0 : want_n) : 0u;
+                    if (take && __hip_atomic_compare_exchange_strong(ret_claimed, &c0, c0 + take, __ATOMIC_RELAXED,
+                                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                        base = c0;
+                        got = take;
+                    }
+                }
+                base = (uint32_t)__shfl((int)base, leader);
+                got = (uint32_t)__shfl((int)got, leader);
+                const uint32_t rank = (uint32_t)__popcll(im & ((1ull << lane) - 1ull));
+                if (idle && rank < got) {
+                    const uint32_t e = base + rank;
+                    unsigned long long v;
+                    do { // reserved by wf_long, its store may still be in flight
+                        v = __hip_atomic_load(st.ret_ring + e % st.long_cap, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    } while ((uint32_t)(v >> 32) != e + 1u);
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    active = true;
+                    first_ray(st, fr, (uint32_t)v, p);
+                }
+            }
+        }
+        if (!__any(active)) {
+            if (!st.long_return) break; // every lane exhausted
+            // leave only while every reserved return is claimed (else: claim them next round)
+            int leave = 0;
+            if (lane == 0) {
+                unsigned long long w = __hip_atomic_load(ret_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t cl = __hip_atomic_load(ret_claimed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if ((uint32_t)w == cl &&
+                    __hip_atomic_compare_exchange_strong(ret_word, &w, w - (1ull << 32), __ATOMIC_RELAXED,
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                    leave = 1;
+            }
+            if (__shfl(leave, 0)) break;
+            continue;
+        }
         bool to_long = false;
         if (active) {
             float bx = 0.0f, by = 0.0f, bz = 0.0f;
-            const int hit = trace_bvh<false>(sc, p.ro, p.rd, bx, by, bz, stk, c);
-            const bool want = shade_step<false>(sc, fr, cam, p, hit, bx, by, bz, limit, c);
+            const int hit = trace_bvh<COUNT>(sc, p.ro, p.rd, bx, by, bz, stk, c);
+            const bool want = shade_step<COUNT>(sc, fr, cam, p, hit, bx, by, bz, limit, c);
             // a path deeper than long_depth goes on in wf_long (64 lanes per ray)
             to_long = want && st.long_depth > 0 && p.depth > st.long_depth;
-            if (!want || to_long) {
-                store_regs(st, fr, p);
-                active = false;
-            }
+            if (!want || to_long) store_regs(st, fr, p);
+            if (!want) active = false;
         }
-        if (__any(to_long)) publish_long(st, to_long, p.slot, p.ro, p.rd);
+        if (__any(to_long) && publish_long_capped(st, to_long, p.slot, p.ro, p.rd) && to_long) active = false;
     }
+    if (COUNT) flush_counters(c, fr.counters);
 }
 
 // Cooperative finisher: runs queued paths to the end of their passes in
@@ -1091,6 +1201,8 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_LONG_WAVES) wf_long(RtDevScene sc
             p.ro = ld3(ldf4(st.long_ray + 2 * (size_t)e));
             p.rd = ld3(ldf4(st.long_ray + 2 * (size_t)e + 1));
         }
+        int want = 0; // after the loop: 0 the pixel's passes are done, 2 returned to the finishers
+        uint32_t ret_e = 0;
         while (true) {
             int hit = -1;
             float bx = 0.0f, by = 0.0f, bz = 0.0f;
@@ -1105,12 +1217,38 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_LONG_WAVES) wf_long(RtDevScene sc
                 const Vec3D d = rt_v3(__shfl(r.d.x, 0), __shfl(r.d.y, 0), __shfl(r.d.z, 0));
                 wide_trace<COUNT>(sc, o, d, __shfl(r.entry, 0), __shfl(r.exit_, 0), W, lane == 0, hit, bx, by, bz, c);
             }
-            int want = 0;
-            if (lane == 0) want = shade_step<COUNT>(sc, fr, cam, p, hit, bx, by, bz, limit, c) ? 1 : 0;
-            if (!__shfl(want, 0)) break;
+            want = 0;
+            if (lane == 0) {
+                want = shade_step<COUNT>(sc, fr, cam, p, hit, bx, by, bz, limit, c) ? 1 : 0;
+                // return mode: the deep sample is over once the pixel's next one starts (depth 1);
+                // the pixel goes back to the finishers if one is still alive to take it
+                if (want && st.long_return && p.depth == 1 && !p.shadow) {
+                    unsigned long long *const ret_word = reinterpret_cast<unsigned long long *>(st.ret_ctr);
+                    unsigned long long w = __hip_atomic_load(ret_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    while ((w >> 32) != 0ull) {
+                        if (__hip_atomic_compare_exchange_strong(ret_word, &w, w + 1ull, __ATOMIC_RELAXED,
+                                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                            want = 2;
+                            ret_e = (uint32_t)w;
+                            break;
+                        }
+                    }
+                }
+            }
+            want = __shfl(want, 0);
+            if (want != 1) break;
         }
         if (lane == 0) {
             store_regs(st, fr, p);
+            if (want == 2) { // back to the finishers: its next ray, then its ring entry
+                st.ro[p.slot] = p.ro;
+                st.cont[p.slot] = p.rd;
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __hip_atomic_store(st.ret_ring + ret_e % st.long_cap, ((unsigned long long)(ret_e + 1u) << 32) | p.slot,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
             __hip_atomic_fetch_sub(running, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         t_idle = __builtin_amdgcn_s_memrealtime();
@@ -1199,7 +1337,8 @@ int ensure(Workspace &w, size_t slots, int grid, int npipes)
                  o_c = take(slots * 12), o_n = take(slots * 12), o_rp = take(slots * 12), o_li = take(slots * 4),
                  o_ro = take(slots * 12), o_es = take(slots * 4), o_ee = take(slots * 4);
     // long-path hand-off (shared by the pipelines), wf_long's stack-free wide traversal needs no spill
-    const size_t o_lf = take(slots * 4), o_lr = take(slots * 32), o_lc = take(256);
+    const size_t o_lf = take(slots * 4), o_lr = take(slots * 32), o_lc = take(256), o_rr = take(slots * 8),
+                 o_rc = take(256);
     // per pipeline (path lists sized for every pixel: a pipeline never holds
     // more; ray queues for two rays per path: a shadow and an extension ray)
     size_t o_qs0[WF_MAX_PIPES], o_qs1[WF_MAX_PIPES], o_qr0[WF_MAX_PIPES], o_qr1[WF_MAX_PIPES], o_h[WF_MAX_PIPES],
@@ -1243,6 +1382,10 @@ int ensure(Workspace &w, size_t slots, int grid, int npipes)
         st.long_ray = (RtF4 *)(b + o_lr);
         st.long_ctr = (uint32_t *)(b + o_lc);
         st.long_depth = 0;
+        st.long_cap = (uint32_t)slots;
+        st.long_return = 0;
+        st.ret_ring = (unsigned long long *)(b + o_rr);
+        st.ret_ctr = (uint32_t *)(b + o_rc);
     }
     w.slots = slots;
     w.grid = grid;
@@ -1318,7 +1461,12 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
     npipes = npipes > tiles ? tiles : npipes;
     if (ensure(w, slots, grid, npipes) != 0) return -1;
     // below this many live paths the rest of the call runs in one finisher launch
-    const uint32_t tail = tail_opt > 0 ? (uint32_t)tail_opt : WF_TAIL_DEFAULT;
+    // (bounded traversal: the whole call in the finisher by default — one path
+    // per lane to the end of its passes beats queue iterations once a ray
+    // query is ~30 dependent loads: 1.22 vs 1.61 s per 256-pass room2m call
+    // with deep paths cut, profiles/r03)
+    const uint32_t tail = tail_opt > 0 ? (uint32_t)tail_opt
+                          : bounded && fin_bvh ? (uint32_t)slots + 1u : WF_TAIL_DEFAULT;
     // the cooperative finisher runs on at most this many waves (up to 64 paths in flight each)
     // (small trees: rays are short, so more paths per finisher wave keep its
     // cooperative rounds full — the 36-triangle Cornell box at 256x256 runs
@@ -1354,9 +1502,17 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
     if (w.recorded && hipStreamWaitEvent(stream, w.long_ev, 0) != hipSuccess) return -1;
     for (int pi = 0; pi < WF_MAX_PIPES; ++pi)
         if (w.pipe[pi].joined && hipStreamWaitEvent(stream, w.pipe[pi].join, 0) != hipSuccess) return -1;
+    // the whole call in the bounded finisher: wf_long returns pixels after their deep sample
+    const int long_return = long_depth > 0 && bounded && fin_bvh && trace_kind == 1 && tail > slots ? 1 : 0;
+    for (int pi = 0; pi < WF_MAX_PIPES; ++pi) w.pipe[pi].st.long_return = long_return;
     if (long_depth > 0) {
-        if (hipMemsetAsync(lst.long_flag, 0, slots * 4, stream) != hipSuccess) return -1;
+        // (every entry of the arrays: in return mode a pixel may be handed over more than once per call)
+        if (hipMemsetAsync(lst.long_flag, 0, (size_t)lst.long_cap * 4, stream) != hipSuccess) return -1;
         if (hipMemsetAsync(lst.long_ctr, 0, 256, stream) != hipSuccess) return -1;
+    }
+    if (long_return) {
+        if (hipMemsetAsync(lst.ret_ring, 0, (size_t)lst.long_cap * 8, stream) != hipSuccess) return -1;
+        if (hipMemsetAsync(lst.ret_ctr, 0, 256, stream) != hipSuccess) return -1;
     }
     // fork: every pipeline stream starts after the caller's stream
     if (hipEventRecord(w.fork, stream) != hipSuccess) return -1;
@@ -1415,11 +1571,16 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
         auto finish = [&](int qq, uint32_t live) -> int {
             if (!mark(2)) return -1;
             if (bounded && fin_bvh) {
-                // one path per lane (lanes refill from the list), within the spill area (grid blocks)
+                // one path per lane (lanes refill from the list), within the spill area (grid blocks),
+                // leaving the wf_long slices their blocks: the pipelines' finishers together would
+                // otherwise hold every wave slot until they end, and the deep paths they hand over
+                // would start only then
                 int fgrid = (int)((live + WF_BLOCK - 1) / WF_BLOCK);
-                fgrid = fgrid > grid ? grid : fgrid;
+                const int fmax = long_depth > 0 ? grid - (WF_LONG_BLOCKS + npipes - 1) / npipes : grid;
+                fgrid = fgrid > fmax ? fmax : fgrid;
                 if (hipMemsetAsync(st.counts + 4, 0, 4, s) != hipSuccess) return -1;
-                hipLaunchKernelGGL(wf_finish_bvh, dim3(fgrid), dim3(WF_BLOCK), 0, s, sc, fr, cam, st, qq);
+                if (count) hipLaunchKernelGGL(wf_finish_bvh<true>, dim3(fgrid), dim3(WF_BLOCK), 0, s, sc, fr, cam, st, qq);
+                else hipLaunchKernelGGL(wf_finish_bvh<false>, dim3(fgrid), dim3(WF_BLOCK), 0, s, sc, fr, cam, st, qq);
             } else if (trace_kind == 1) {
                 // paths per wave: spread over up to finish_waves waves, within the spill area (grid * WF_BLOCK threads)
                 const uint32_t max_waves = (uint32_t)grid * (WF_BLOCK / 64);
