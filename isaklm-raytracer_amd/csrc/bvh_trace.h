@@ -26,6 +26,78 @@
 
 namespace rtk {
 
+// Scene data is read-only for a kernel's lifetime: loaded through the
+// constant address space, so that a wave-uniform address (a traversal every
+// lane of the wave runs on the same ray: wf_long) becomes a scalar load
+// through the scalar cache; a divergent one stays a vector load.
+// (the host pass of the single-source compile sees plain loads: these are
+// __device__ functions and never run there)
+#if defined(__HIP_DEVICE_COMPILE__)
+#define RT_CONST __attribute__((address_space(4)))
+#else
+#define RT_CONST
+#endif
+__device__ __forceinline__ RtF4 ldc4(const RtF4 *p)
+{
+    const RT_CONST RtF4 *q = (const RT_CONST RtF4 *)p;
+    return RtF4{q->x, q->y, q->z, q->w};
+}
+__device__ __forceinline__ uint2 ldc_u2(const void *p)
+{
+    const RT_CONST uint32_t *q = (const RT_CONST uint32_t *)p;
+    return make_uint2(q[0], q[1]);
+}
+__device__ __forceinline__ float ldc_f(const uint32_t *p) { return __uint_as_float(*(const RT_CONST uint32_t *)p); }
+
+// A traversal stack shared by the 64 lanes of a wave that all trace the same
+// ray (entries [0, LDS_DEPTH) in the wave's LDS slice, deeper ones in its
+// spill column): popped values are made wave-uniform (readfirstlane), so the
+// loads they address stay scalar.  Same interface as Stack.
+template <int LDS_DEPTH>
+struct WaveStack {
+    uint32_t *lds_node;
+    float *lds_entry;
+    uint2 *spill;
+    int spill_stride;
+    __device__ __forceinline__ void put(int k, uint32_t node, float t)
+    {
+        if (k < LDS_DEPTH) {
+            lds_node[k] = node;
+            lds_entry[k] = t;
+        } else {
+            spill[(size_t)(k - LDS_DEPTH) * spill_stride] = make_uint2(node, __float_as_uint(t));
+        }
+    }
+    __device__ __forceinline__ void get(int k, uint32_t &node, float &entry) const
+    {
+        if (k < LDS_DEPTH) {
+            node = lds_node[k];
+            entry = lds_entry[k];
+        } else {
+            unsigned long long *p = reinterpret_cast<unsigned long long *>(spill + (size_t)(k - LDS_DEPTH) * spill_stride);
+            const unsigned long long v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+            node = (uint32_t)v;
+            entry = __uint_as_float((uint32_t)(v >> 32));
+        }
+        node = (uint32_t)__builtin_amdgcn_readfirstlane((int)node);
+        entry = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(entry)));
+    }
+    __device__ __forceinline__ uint32_t node_at(int k) const
+    {
+        uint32_t n;
+        float e;
+        get(k, n, e);
+        return n;
+    }
+    __device__ __forceinline__ float entry_at(int k) const
+    {
+        uint32_t n;
+        float e;
+        get(k, n, e);
+        return e;
+    }
+};
+
 // The tests of leaf entries [e0, e1) in order (trace_leaf_node,
 // rt/trace_ray.cuh:115-172: intersect_triangle + calculate_barycentric_
 // coordinates, :48-113, on precomputed records): an entry passes with
@@ -47,7 +119,7 @@ __device__ __forceinline__ int leaf_scan(const RtF4 *plane, const RtIsectBary *b
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const bool in = e + k < e1;
-            const RtF4 A = ldf4(plane + (in ? e + k : e));
+            const RtF4 A = ldc4(plane + (in ? e + k : e));
             p[k] = rt_tri_plane(A, o, d, smallest, s[k]) && in;
         }
 #pragma unroll
@@ -55,8 +127,8 @@ __device__ __forceinline__ int leaf_scan(const RtF4 *plane, const RtIsectBary *b
             if (!p[k] || !(s[k] < smallest)) continue;
             if (COUNT) c.v[RT_CNT_B_BARY]++;
             float cx, cy, cz;
-            if (rt_tri_bary(ldf4(&bary[e + k].b), ldf4(&bary[e + k].c), ldf4(&bary[e + k].d),
-                            as_float(bary[e + k].rd), o, d, s[k], cx, cy, cz)) {
+            if (rt_tri_bary(ldc4(&bary[e + k].b), ldc4(&bary[e + k].c), ldc4(&bary[e + k].d),
+                            ldc_f(&bary[e + k].rd), o, d, s[k], cx, cy, cz)) {
                 smallest = s[k];
                 best = (int)(e + k);
                 bx = cx;
@@ -81,8 +153,8 @@ __device__ __forceinline__ float bvh_bound(const RtDevScene &sc, Vec3D o, Vec3D 
         if (!(cur & RT_BVH_LEAF)) {
             const RtF4 *nd = sc.bvh_nodes + 4 * (size_t)cur;
             if (COUNT) cn.v[RT_CNT_B_BVH_NODE]++;
-            const RtF4 a = ldf4(nd), b = ldf4(nd + 1), c = ldf4(nd + 2);
-            const uint2 ch = *reinterpret_cast<const uint2 *>(nd + 3);
+            const RtF4 a = ldc4(nd), b = ldc4(nd + 1), c = ldc4(nd + 2);
+            const uint2 ch = ldc_u2(nd + 3);
             float tn0, tn1;
             const bool h0 = rt_bvh_box(a.x, a.y, a.z, a.w, b.x, b.y, om, op, inv, best, tn0) && ch.x != RT_BVH_EMPTY;
             const bool h1 = rt_bvh_box(b.z, b.w, c.x, c.y, c.z, c.w, om, op, inv, best, tn1) && ch.y != RT_BVH_EMPTY;
@@ -142,7 +214,7 @@ __device__ __forceinline__ int trace_bvh(const RtDevScene &sc, const Vec3D o, co
     int sp = 0;
     uint32_t node = 0;
     while (true) {
-        uint2 nd = *reinterpret_cast<const uint2 *>(sc.nodes + 2 * (size_t)node);
+        uint2 nd = ldc_u2(sc.nodes + 2 * (size_t)node);
         if (COUNT) c.v[RT_CNT_NODE]++;
         while ((nd.y & 3u) != RT_LEAF_TAG) {
             const uint32_t axis = nd.y & 3u;
@@ -169,7 +241,7 @@ __device__ __forceinline__ int trace_bvh(const RtDevScene &sc, const Vec3D o, co
                 node = near_c;
                 exit_ = t;
             }
-            nd = *reinterpret_cast<const uint2 *>(sc.nodes + 2 * (size_t)node);
+            nd = ldc_u2(sc.nodes + 2 * (size_t)node);
             if (COUNT) c.v[RT_CNT_NODE]++;
         }
         const uint32_t count = nd.y >> 2;
@@ -179,7 +251,7 @@ __device__ __forceinline__ int trace_bvh(const RtDevScene &sc, const Vec3D o, co
             float bx = 0.0f, by = 0.0f, bz = 0.0f;
             if (COUNT) c.v[RT_CNT_TRI] += count;
             const int be = leaf_scan<COUNT>(sc.isect_a, sc.isect_bary, nd.x, nd.x + count, o, d, smallest, bx, by, bz, c);
-            const int best = be >= 0 ? (int)sc.isect_bary[be].tri : -1;
+            const int best = be >= 0 ? (int)ldc_u2(&sc.isect_bary[be].rd).y : -1;
             if (best >= 0) {
                 if (COUNT) c.v[RT_CNT_HIT]++;
                 hbx = bx;

@@ -58,7 +58,16 @@ static_assert(WF_BLOCK % WF_TBLOCK == 0 && WF_TBLOCK % 64 == 0, "WF_TBLOCK must 
 // Measured (as WF_SHADE_WAVES): 13.16 s at 126 VGPRs, 13.16 at 128 (4
 // waves), 12.87 at 80, 12.86 at 72, 12.92 at 64
 #ifndef WF_LONG_WAVES
-#define WF_LONG_WAVES 6
+#define WF_LONG_WAVES 5
+#endif
+#ifndef WF_LONG_PRIO
+#define WF_LONG_PRIO 0 // wf_long wave priority (a lone deep path's chain is the call's critical path)
+#endif
+#ifndef WF_FIN_LINGER
+#define WF_FIN_LINGER 100000000ull // s_memrealtime ticks (100 MHz): 1 s
+#endif
+#ifndef WF_FIN_LINGER_WAVES
+#define WF_FIN_LINGER_WAVES 256u // finisher waves that linger for returned pixels
 #endif
 #ifndef WF_FIN_OCC
 #define WF_FIN_OCC 1 // wf_finish_coop occupancy floor (1: the compiler's choice, 2 waves/SIMD; 3: no change)
@@ -128,8 +137,16 @@ struct WfState {
     // reserves only while a finisher wave is alive; a wave leaves only when
     // every reserved return is claimed: no pixel is stranded, and neither
     // kernel ever waits for the other — they may share a hardware queue);
-    // u32 [2] = returns claimed
+    // u32 [2] = returns claimed, u32 [3] = pixels out (handed to wf_long, not
+    // yet returned or done): an idle finisher wave lingers (s_sleep) while
+    // pixels are out — for at most WF_FIN_LINGER ticks, so that it never
+    // depends on wf_long making progress
     uint32_t *ret_ctr;
+    // pixels whose path went to wf_long in the previous call run first (their
+    // passes are the call's longest chains): wf_start puts them on path list 1,
+    // the whole-call finisher takes list 1 before list 0
+    uint8_t *heavy;
+    int heavy_first;
 };
 
 namespace {
@@ -176,6 +193,7 @@ __device__ __forceinline__ void publish_long(const WfState &st, bool to_long, ui
 {
     uint32_t e = 0;
     if (to_long) {
+        st.heavy[slot] = 1;
         e = __hip_atomic_fetch_add(st.long_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         st.long_ray[2 * (size_t)e] = RtF4{o.x, o.y, o.z, 0.0f};
         st.long_ray[2 * (size_t)e + 1] = RtF4{d.x, d.y, d.z, 0.0f};
@@ -209,11 +227,14 @@ __device__ __forceinline__ bool publish_long_capped(const WfState &st, bool to_l
                 break;
             }
         }
+        if (base != 0xffffffffu && st.long_return) // out before the entries can be seen
+            __hip_atomic_fetch_add(st.ret_ctr + 3, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     base = (uint32_t)__shfl((int)base, leader);
     if (base == 0xffffffffu) return false;
     const uint32_t e = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
     if (to_long) {
+        st.heavy[slot] = 1;
         st.long_ray[2 * (size_t)e] = RtF4{o.x, o.y, o.z, 0.0f};
         st.long_ray[2 * (size_t)e + 1] = RtF4{d.x, d.y, d.z, 0.0f};
     }
@@ -289,9 +310,19 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_start(RtDevFrame fr, RtDevCamera 
         st.ro[slot] = ro;
         st.cont[slot] = rd;
     }
-    const uint32_t e = enqueue_ray(st, 0, want, ro, rd);
-    if (want) st.e_ext[slot] = e;
-    enqueue_path(st, 0, want, (uint32_t)slot);
+    if (st.heavy_first) { // the whole-call finisher: no ray queue; heavy pixels on list 1
+        bool h = false;
+        if (valid && slot < n) {
+            h = st.heavy[slot] != 0;
+            if (h) st.heavy[slot] = 0; // set again by this call's hand-offs
+        }
+        enqueue_path(st, 1, want && h, (uint32_t)slot);
+        enqueue_path(st, 0, want && !h, (uint32_t)slot);
+    } else {
+        const uint32_t e = enqueue_ray(st, 0, want, ro, rd);
+        if (want) st.e_ext[slot] = e;
+        enqueue_path(st, 0, want, (uint32_t)slot);
+    }
     if (COUNT) flush_counters(c, fr.counters);
 }
 
@@ -913,7 +944,9 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_FIN_BVH_WAVES) wf_finish_bvh(RtDe
     Stack<WF_BVH_LDS> stk{s_node + tid, s_entry + tid, WF_BLOCK, st.spill + gtid, st.spill_threads};
     Cnt c;
     if (COUNT) c.zero();
-    const uint32_t n = st.counts[6 + q]; // paths of path list q
+    // paths of path list q (heavy_first: list 1's, the heavy pixels, first)
+    const uint32_t n1 = st.heavy_first ? st.counts[6 + 1] : 0u;
+    const uint32_t n = st.counts[6 + q] + n1;
     uint32_t *fetch = st.counts + 4;
     const int limit = fr.max_depth > 0 ? fr.max_depth : RT_WATCHDOG_BOUNCES;
     const int lane = __lane_id();
@@ -925,6 +958,8 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_FIN_BVH_WAVES) wf_finish_bvh(RtDe
     p.slot = 0;
     p.ro = p.rd = rt_v3(0, 0, 0);
     bool active = false, exhausted = false; // exhausted: this lane found the path list empty
+    unsigned long long idle_since = 0;      // (lane 0) when the wave first had nothing to do
+    bool seated = false;                    // (lane 0) holds a linger seat
     while (true) {
         const bool need = !active && !exhausted;
         const unsigned long long m = __ballot(need);
@@ -939,7 +974,7 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_FIN_BVH_WAVES) wf_finish_bvh(RtDe
                     exhausted = true;
                 } else {
                     active = true;
-                    first_ray(st, fr, st.q_slot[q][e], p);
+                    first_ray(st, fr, e < n1 ? st.q_slot[1][e] : st.q_slot[q][e - n1], p);
                 }
             }
         }
@@ -972,6 +1007,7 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_FIN_BVH_WAVES) wf_finish_bvh(RtDe
                         v = __hip_atomic_load(st.ret_ring + e % st.long_cap, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     } while ((uint32_t)(v >> 32) != e + 1u);
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    __hip_atomic_fetch_sub(st.ret_ctr + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     active = true;
                     first_ray(st, fr, (uint32_t)v, p);
                 }
@@ -979,19 +1015,33 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_FIN_BVH_WAVES) wf_finish_bvh(RtDe
         }
         if (!__any(active)) {
             if (!st.long_return) break; // every lane exhausted
-            // leave only while every reserved return is claimed (else: claim them next round)
+            // leave only while every reserved return is claimed (else: claim them next round), and
+            // while pixels are out in wf_long linger for them (bounded: WF_FIN_LINGER)
             int leave = 0;
             if (lane == 0) {
+                if (idle_since == 0) idle_since = __builtin_amdgcn_s_memrealtime();
+                bool out = __hip_atomic_load(st.ret_ctr + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+                // only WF_FIN_LINGER_WAVES waves linger (a seat each, kept until they leave): the
+                // others leave their slots to wf_long, which the deep paths are waiting for
+                if (out && !seated) {
+                    if (__hip_atomic_fetch_add(st.ret_ctr + 4, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+                        WF_FIN_LINGER_WAVES)
+                        seated = true;
+                    else
+                        out = false;
+                }
                 unsigned long long w = __hip_atomic_load(ret_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 const uint32_t cl = __hip_atomic_load(ret_claimed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if ((uint32_t)w == cl &&
+                if ((uint32_t)w == cl && (!out || __builtin_amdgcn_s_memrealtime() - idle_since > WF_FIN_LINGER) &&
                     __hip_atomic_compare_exchange_strong(ret_word, &w, w - (1ull << 32), __ATOMIC_RELAXED,
                                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
                     leave = 1;
             }
             if (__shfl(leave, 0)) break;
+            __builtin_amdgcn_s_sleep(8);
             continue;
         }
+        idle_since = 0;
         bool to_long = false;
         if (active) {
             float bx = 0.0f, by = 0.0f, bz = 0.0f;
@@ -1142,11 +1192,14 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_FIN_OCC) wf_finish_coop(RtDevScen
 // published) drains what is left.
 template <bool COUNT>
 __global__ void __launch_bounds__(WF_BLOCK, WF_LONG_WAVES) wf_long(RtDevScene sc, RtDevFrame fr, RtDevCamera cam, WfState st,
-                                                    int final_slice)
+                                                    int final_slice, int bounded)
 {
+    __shared__ uint32_t s_wnode[(WF_BLOCK / 64) * WF_BVH_LDS]; // bounded: one stack per wave (WaveStack)
+    __shared__ float s_wentry[(WF_BLOCK / 64) * WF_BVH_LDS];
     __shared__ WideItem s_wide[(WF_BLOCK / 64) * WIDE_CAP];
     __shared__ unsigned long long s_key[(WF_BLOCK / 64) * 4];
     __shared__ int s_mark[2 * WF_BLOCK]; // 128 per wave: chunk_owner marks + junk slots
+    if (WF_LONG_PRIO > 0) __builtin_amdgcn_s_setprio(WF_LONG_PRIO);
     const int lane = __lane_id();
     const int wave = threadIdx.x >> 6;
     const WideLds W{s_wide + wave * WIDE_CAP, WIDE_CAP, s_key + wave * 4,
@@ -1189,9 +1242,10 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_LONG_WAVES) wf_long(RtDevScene sc
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
         }
-        if (__shfl(quit, 0)) break;
-        e = (uint32_t)__shfl((int)e, 0);
-        flag = (uint32_t)__shfl((int)flag, 0);
+        // (lane 0's values, wave-uniform: readfirstlane — every lane is active here)
+        if (__builtin_amdgcn_readfirstlane(quit)) break;
+        e = (uint32_t)__builtin_amdgcn_readfirstlane((int)e);
+        flag = (uint32_t)__builtin_amdgcn_readfirstlane((int)flag);
         // ---- run the path (state in lane 0) to the end of its pixel's passes
         PathRegs p;
         p.slot = 0;
@@ -1206,6 +1260,16 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_LONG_WAVES) wf_long(RtDevScene sc
         while (true) {
             int hit = -1;
             float bx = 0.0f, by = 0.0f, bz = 0.0f;
+            if (!COUNT && bounded) {
+                // every lane traces lane 0's ray with the bounded traversal: wave-uniform
+                // addresses, so its node and record loads are scalar loads
+                auto uni = [](float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); };
+                const Vec3D o = rt_v3(uni(p.ro.x), uni(p.ro.y), uni(p.ro.z));
+                const Vec3D d = rt_v3(uni(p.rd.x), uni(p.rd.y), uni(p.rd.z));
+                WaveStack<WF_BVH_LDS> ws{s_wnode + wave * WF_BVH_LDS, s_wentry + wave * WF_BVH_LDS,
+                                         st.spill + blockIdx.x * (WF_BLOCK / 64) + wave, st.spill_threads};
+                hit = trace_bvh<false>(sc, o, d, bx, by, bz, ws, c);
+            } else {
             CoopRay r;
             coop_idle(r);
             if (lane == 0) {
@@ -1216,6 +1280,7 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_LONG_WAVES) wf_long(RtDevScene sc
                 const Vec3D o = rt_v3(__shfl(r.o.x, 0), __shfl(r.o.y, 0), __shfl(r.o.z, 0));
                 const Vec3D d = rt_v3(__shfl(r.d.x, 0), __shfl(r.d.y, 0), __shfl(r.d.z, 0));
                 wide_trace<COUNT>(sc, o, d, __shfl(r.entry, 0), __shfl(r.exit_, 0), W, lane == 0, hit, bx, by, bz, c);
+            }
             }
             want = 0;
             if (lane == 0) {
@@ -1235,7 +1300,7 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_LONG_WAVES) wf_long(RtDevScene sc
                     }
                 }
             }
-            want = __shfl(want, 0);
+            want = __builtin_amdgcn_readfirstlane(want);
             if (want != 1) break;
         }
         if (lane == 0) {
@@ -1248,6 +1313,8 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_LONG_WAVES) wf_long(RtDevScene sc
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __hip_atomic_store(st.ret_ring + ret_e % st.long_cap, ((unsigned long long)(ret_e + 1u) << 32) | p.slot,
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else if (st.long_return) { // the pixel's passes are done: no longer out
+                __hip_atomic_fetch_sub(st.ret_ctr + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             __hip_atomic_fetch_sub(running, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -1279,6 +1346,7 @@ struct Pipe {
 struct Workspace {
     size_t slots = 0;
     int grid = 0;
+    int spill_pipes = 0;
     void *blob = nullptr;
     Pipe pipe[WF_MAX_PIPES];
     bool streams_ok = false;
@@ -1322,7 +1390,9 @@ int ensure_streams(Workspace &w, int npipes)
 int ensure(Workspace &w, size_t slots, int grid, int npipes)
 {
     if (ensure_streams(w, npipes) != 0) return -1;
-    if (w.slots >= slots && w.grid >= grid) return 0;
+    if (w.slots >= slots && w.grid >= grid && w.spill_pipes >= npipes) return 0;
+    // traversal stack spill for the pipelines in use (at least the default 3)
+    const int spill_pipes = npipes > WF_PIPES_DEFAULT ? npipes : WF_PIPES_DEFAULT;
     if (w.blob) (void)hipFree(w.blob);
     w.blob = nullptr;
     const size_t spill_threads = (size_t)grid * WF_BLOCK;
@@ -1338,7 +1408,7 @@ int ensure(Workspace &w, size_t slots, int grid, int npipes)
                  o_ro = take(slots * 12), o_es = take(slots * 4), o_ee = take(slots * 4);
     // long-path hand-off (shared by the pipelines), wf_long's stack-free wide traversal needs no spill
     const size_t o_lf = take(slots * 4), o_lr = take(slots * 32), o_lc = take(256), o_rr = take(slots * 8),
-                 o_rc = take(256);
+                 o_rc = take(256), o_hv = take(slots);
     // per pipeline (path lists sized for every pixel: a pipeline never holds
     // more; ray queues for two rays per path: a shadow and an extension ray)
     size_t o_qs0[WF_MAX_PIPES], o_qs1[WF_MAX_PIPES], o_qr0[WF_MAX_PIPES], o_qr1[WF_MAX_PIPES], o_h[WF_MAX_PIPES],
@@ -1350,13 +1420,14 @@ int ensure(Workspace &w, size_t slots, int grid, int npipes)
         o_qr1[i] = take(2 * slots * 32);
         o_h[i] = take(2 * slots * 16);
         o_cnt[i] = take(256);
-        o_sp[i] = take(spill_threads * 8 * WF_SPILL_ENTRIES);
+        o_sp[i] = i < spill_pipes ? take(spill_threads * 8 * WF_SPILL_ENTRIES) : 0;
     }
     if (hipMalloc(&w.blob, off) != hipSuccess) {
         w.blob = nullptr;
         return -1;
     }
     char *b = (char *)w.blob;
+    if (hipMemset(b + o_hv, 0, slots) != hipSuccess) return -1; // no history yet
     for (int i = 0; i < WF_MAX_PIPES; ++i) {
         WfState &st = w.pipe[i].st;
         st.passes_left = (int *)(b + o_pl);
@@ -1376,7 +1447,7 @@ int ensure(Workspace &w, size_t slots, int grid, int npipes)
         st.q_ray[1] = (RtF4 *)(b + o_qr1[i]);
         st.hits = (RtF4 *)(b + o_h[i]);
         st.counts = (uint32_t *)(b + o_cnt[i]);
-        st.spill = (uint2 *)(b + o_sp[i]);
+        st.spill = i < spill_pipes ? (uint2 *)(b + o_sp[i]) : nullptr;
         st.spill_threads = (int)spill_threads;
         st.long_flag = (uint32_t *)(b + o_lf);
         st.long_ray = (RtF4 *)(b + o_lr);
@@ -1386,9 +1457,12 @@ int ensure(Workspace &w, size_t slots, int grid, int npipes)
         st.long_return = 0;
         st.ret_ring = (unsigned long long *)(b + o_rr);
         st.ret_ctr = (uint32_t *)(b + o_rc);
+        st.heavy = (uint8_t *)(b + o_hv);
+        st.heavy_first = 0;
     }
     w.slots = slots;
     w.grid = grid;
+    w.spill_pipes = spill_pipes;
     return 0;
 }
 
@@ -1429,6 +1503,20 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return -1;
     Workspace &w = g_ws[dev];
+    const size_t slots = (size_t)fr.width * fr.height;
+    const bool count = fr.counters != nullptr;
+    // the queue trace launches run the BVH-bounded traversal (counting calls: the KD one, whose counters are the reference's)
+    const bool bounded = sc.bvh_nodes != nullptr && ((traversal == RT_TRAVERSAL_BOUNDED && !count) ||
+                                                     traversal == RT_TRAVERSAL_BOUNDED_COUNTED);
+    // ... and the tail finisher too (RT_WF_FIN_BVH=0: the cooperative KD finisher; experiments)
+    static const bool fin_bvh = !getenv("RT_WF_FIN_BVH") || atoi(getenv("RT_WF_FIN_BVH")) != 0;
+    // bounded traversal: the whole call in the finisher by default — one path
+    // per lane to the end of its passes beats queue iterations once a ray
+    // query is ~30 dependent loads: 1.22 vs 1.61 s per 256-pass room2m call
+    // with deep paths cut (profiles/r03).  It runs as ONE pipeline whose
+    // finisher spans the chip: three pipelines' fixed pixel sets finished up
+    // to 0.7 s apart, each leaving its third of the chip idle.
+    const bool whole = bounded && fin_bvh && trace_kind == 1 && (tail_opt <= 0 || (size_t)tail_opt > slots);
     // persistent-ish grid for trace/shade (grid-stride over the queue); RT_WF_GRID overrides (experiments)
     static const int grid_env = getenv("RT_WF_GRID") ? atoi(getenv("RT_WF_GRID")) : 0;
     // 512 blocks = 2,048 waves = a third of the chip's 6,144 wave slots at the
@@ -1437,7 +1525,8 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
     // the launch's first round of rays (1,536 blocks: ~1.2 rays per lane, most
     // of the launch was its tail).  Measured 512 / 704 / 1,536: 37.5 / 37.6 /
     // 33.1 Msamples/s on room2m 1080p (tools/gpu_sweep.sh, profiles/r02).
-    const int grid = grid_env >= 64 && grid_env <= 16384 ? grid_env : 512;
+    // The whole-call finisher: 1,536 blocks = every slot at 6 waves/SIMD.
+    const int grid = grid_env >= 64 && grid_env <= 16384 ? grid_env : (whole ? 1536 : 512);
     const int tgrid = grid * (WF_BLOCK / WF_TBLOCK); // the same waves in WF_TBLOCK-thread blocks
     // wf_shade: half the trace grid (~2 paths per lane per launch).  Measured
     // per 256-pass room2m call (2 rounds each): 64 / 128 / 256 / 384 / 512 /
@@ -1445,28 +1534,21 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
     // 13.21 s.  RT_WF_SHADE_GRID overrides (experiments)
     static const int sgrid_env = getenv("RT_WF_SHADE_GRID") ? atoi(getenv("RT_WF_SHADE_GRID")) : 0;
     const int sgrid = sgrid_env >= 16 && sgrid_env <= 16384 ? sgrid_env : (tgrid / 2 > 16 ? tgrid / 2 : 16);
-    const size_t slots = (size_t)fr.width * fr.height;
-    const bool count = fr.counters != nullptr;
     const bool prof = profile != 0;
-    // the queue trace launches run the BVH-bounded traversal (counting calls: the KD one, whose counters are the reference's)
-    const bool bounded = sc.bvh_nodes != nullptr && ((traversal == RT_TRAVERSAL_BOUNDED && !count) ||
-                                                     traversal == RT_TRAVERSAL_BOUNDED_COUNTED);
-    // ... and the tail finisher too (RT_WF_FIN_BVH=0: the cooperative KD finisher; experiments)
-    static const bool fin_bvh = !getenv("RT_WF_FIN_BVH") || atoi(getenv("RT_WF_FIN_BVH")) != 0;
-    // (wf_long keeps the 64-lane wide KD traversal: one lane's bounded traversal per long path measured
-    // 13 % slower per call, profiles/r03/bounded_ab.json)
+    // wf_long: RT_WF_LONG_UNI=1 runs the bounded traversal wave-uniformly (every lane on the path's ray,
+    // scalar node loads) instead of the 64-lane wide KD traversal — experiments: per bounce no faster on
+    // the light guide (9.5 us either way: a lone path is bound by its dependent instruction chain, not by
+    // load latency) and 25 % slower per room2m call (profiles/r03/deep_paths.md)
+    static const bool long_uni = getenv("RT_WF_LONG_UNI") && atoi(getenv("RT_WF_LONG_UNI")) != 0;
+    // (RT_WF_HEAVY_FIRST=0: the whole-call finisher takes pixels in tile order only; experiments)
+    static const bool heavy_first_opt = !getenv("RT_WF_HEAVY_FIRST") || atoi(getenv("RT_WF_HEAVY_FIRST")) != 0;
     const int tiles = ((fr.width + 15) / 16) * ((fr.height + 15) / 16);
-    int npipes = pipes_opt > 0 ? pipes_opt : WF_PIPES_DEFAULT;
+    int npipes = pipes_opt > 0 ? pipes_opt : (whole ? 1 : WF_PIPES_DEFAULT);
     npipes = npipes > WF_MAX_PIPES ? WF_MAX_PIPES : npipes;
     npipes = npipes > tiles ? tiles : npipes;
     if (ensure(w, slots, grid, npipes) != 0) return -1;
     // below this many live paths the rest of the call runs in one finisher launch
-    // (bounded traversal: the whole call in the finisher by default — one path
-    // per lane to the end of its passes beats queue iterations once a ray
-    // query is ~30 dependent loads: 1.22 vs 1.61 s per 256-pass room2m call
-    // with deep paths cut, profiles/r03)
-    const uint32_t tail = tail_opt > 0 ? (uint32_t)tail_opt
-                          : bounded && fin_bvh ? (uint32_t)slots + 1u : WF_TAIL_DEFAULT;
+    const uint32_t tail = whole ? (uint32_t)slots + 1u : tail_opt > 0 ? (uint32_t)tail_opt : WF_TAIL_DEFAULT;
     // the cooperative finisher runs on at most this many waves (up to 64 paths in flight each)
     // (small trees: rays are short, so more paths per finisher wave keep its
     // cooperative rounds full — the 36-triangle Cornell box at 256x256 runs
@@ -1504,7 +1586,10 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
         if (w.pipe[pi].joined && hipStreamWaitEvent(stream, w.pipe[pi].join, 0) != hipSuccess) return -1;
     // the whole call in the bounded finisher: wf_long returns pixels after their deep sample
     const int long_return = long_depth > 0 && bounded && fin_bvh && trace_kind == 1 && tail > slots ? 1 : 0;
-    for (int pi = 0; pi < WF_MAX_PIPES; ++pi) w.pipe[pi].st.long_return = long_return;
+    for (int pi = 0; pi < WF_MAX_PIPES; ++pi) {
+        w.pipe[pi].st.long_return = long_return;
+        w.pipe[pi].st.heavy_first = long_return && heavy_first_opt;
+    }
     if (long_depth > 0) {
         // (every entry of the arrays: in return mode a pixel may be handed over more than once per call)
         if (hipMemsetAsync(lst.long_flag, 0, (size_t)lst.long_cap * 4, stream) != hipSuccess) return -1;
@@ -1519,6 +1604,7 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
     if (prof && hipEventRecord(w.ev0, stream) != hipSuccess) return -1;
     std::mutex long_mu;
     bool long_final = false;
+    int n_slices = 0; // (debug output)
     // launches a wf_long slice on the caller's stream unless the previous one
     // is still running; the final slice (every producer done) is queued after it
     auto kick_long = [&](bool final) -> int {
@@ -1532,11 +1618,13 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
         }
         const int fin = final ? 1 : 0;
         if (count)
-            hipLaunchKernelGGL(wf_long<true>, dim3(WF_LONG_BLOCKS), dim3(WF_BLOCK), 0, stream, sc, fr, cam, lst, fin);
+            hipLaunchKernelGGL(wf_long<true>, dim3(WF_LONG_BLOCKS), dim3(WF_BLOCK), 0, stream, sc, fr, cam, lst, fin, 0);
         else
-            hipLaunchKernelGGL(wf_long<false>, dim3(WF_LONG_BLOCKS), dim3(WF_BLOCK), 0, stream, sc, fr, cam, lst, fin);
+            hipLaunchKernelGGL(wf_long<false>, dim3(WF_LONG_BLOCKS), dim3(WF_BLOCK), 0, stream, sc, fr, cam, lst, fin,
+                               bounded && long_uni ? 1 : 0);
         if (hipGetLastError() != hipSuccess) return -1;
         long_final = final;
+        ++n_slices;
         if (hipEventRecord(w.long_ev, stream) != hipSuccess) return -1;
         w.recorded = true;
         return 0;
@@ -1625,6 +1713,11 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
                 if (e != hipErrorNotReady) return -1;
                 if (kick_long(false) != 0) return -1;
                 std::this_thread::sleep_for(std::chrono::microseconds(200));
+            }
+            if (trace_iters) {
+                timespec ts;
+                clock_gettime(CLOCK_MONOTONIC, &ts);
+                fprintf(stderr, "[wf] pipe %d finisher done t %.4f\n", pi, ts.tv_sec + ts.tv_nsec * 1e-9);
             }
             return producer_done(pi);
         };
@@ -1722,8 +1815,14 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
         (void)hipStreamSynchronize(stream);
         (void)hipMemcpy(lc, lst.long_ctr, sizeof lc, hipMemcpyDeviceToHost);
         clock_gettime(CLOCK_MONOTONIC, &ts);
-        fprintf(stderr, "[wf] long paths %u claimed %u running %u; caller stream done t %.4f\n", lc[0], lc[1], lc[3],
-                ts.tv_sec + ts.tv_nsec * 1e-9);
+        fprintf(stderr, "[wf] long paths %u claimed %u running %u; slices %d; caller stream done t %.4f\n", lc[0],
+                lc[1], lc[3], n_slices, ts.tv_sec + ts.tv_nsec * 1e-9);
+        if (long_return) {
+            uint32_t rc4[4] = {};
+            (void)hipMemcpy(rc4, lst.ret_ctr, sizeof rc4, hipMemcpyDeviceToHost);
+            fprintf(stderr, "[wf] returns reserved %u claimed %u, finisher waves alive %u, pixels out %u\n", rc4[0],
+                    rc4[2], rc4[1], rc4[3]);
+        }
     }
     for (int pi = 0; pi < npipes; ++pi)
         if (rcs[pi] != 0) return rcs[pi];
