@@ -149,8 +149,23 @@ __device__ __forceinline__ float bvh_bound(const RtDevScene &sc, Vec3D o, Vec3D 
     const Vec3D inv = rt_v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     int sp = 0;
     uint32_t cur = 0; // the root (always an inner node)
+    // pop the next subtree that may still hold a smaller s (RT_BVH_EMPTY: none)
+    auto pop = [&]() -> uint32_t {
+        while (sp > 0) {
+            --sp;
+            uint32_t n;
+            float tn;
+            stk.get(sp, n, tn);
+            if (tn <= best) return n;
+        }
+        return RT_BVH_EMPTY;
+    };
+    // "while-while" (SIMT): the lanes descend inner nodes together until each
+    // holds a leaf (or is done), then test their leaves together — a lane at a
+    // leaf does not drag its wave through every other lane's node steps one
+    // iteration at a time
     while (true) {
-        if (!(cur & RT_BVH_LEAF)) {
+        while (!(cur & RT_BVH_LEAF)) {
             const RtF4 *nd = sc.bvh_nodes + 4 * (size_t)cur;
             if (COUNT) cn.v[RT_CNT_B_BVH_NODE]++;
             const RtF4 a = ldc4(nd), b = ldc4(nd + 1), c = ldc4(nd + 2);
@@ -163,32 +178,19 @@ __device__ __forceinline__ float bvh_bound(const RtDevScene &sc, Vec3D o, Vec3D 
                 stk.put(sp, second_first ? ch.x : ch.y, second_first ? tn0 : tn1);
                 ++sp;
                 cur = second_first ? ch.y : ch.x;
-                continue;
-            }
-            if (h0 || h1) {
+            } else if (h0 || h1) {
                 cur = h0 ? ch.x : ch.y;
-                continue;
-            }
-        } else {
-            const uint32_t first = (cur & ~RT_BVH_LEAF) >> 3, end = first + (cur & 7u) + 1u;
-            if (COUNT) cn.v[RT_CNT_B_BVH_TRI] += end - first;
-            float bx, by, bz;
-            (void)leaf_scan<COUNT>(sc.bvh_a, sc.bvh_bary, first, end, o, d, best, bx, by, bz, cn);
-        }
-        // pop the next subtree that may still hold a smaller s
-        bool more = false;
-        while (sp > 0) {
-            --sp;
-            uint32_t n;
-            float tn;
-            stk.get(sp, n, tn);
-            if (tn <= best) {
-                cur = n;
-                more = true;
-                break;
+            } else {
+                cur = pop();
             }
         }
-        if (!more) return best;
+        if (cur == RT_BVH_EMPTY) return best;
+        const uint32_t first = (cur & ~RT_BVH_LEAF) >> 3, end = first + (cur & 7u) + 1u;
+        if (COUNT) cn.v[RT_CNT_B_BVH_TRI] += end - first;
+        float bx, by, bz;
+        (void)leaf_scan<COUNT>(sc.bvh_a, sc.bvh_bary, first, end, o, d, best, bx, by, bz, cn);
+        cur = pop();
+        if (cur == RT_BVH_EMPTY) return best;
     }
 }
 
