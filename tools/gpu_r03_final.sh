@@ -1,0 +1,9 @@
+#!/bin/bash
+# round 3 record run, part A: every GPU test, smoke, the default bench line with the counter passes
+set -o pipefail
+mkdir -p gpurun_out/r03final
+export PYTHONUNBUFFERED=1
+O=gpurun_out/r03final
+timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 400 --timeout-method thread > $O/pytest_gpu.log 2>&1 &&
+timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 &&
+timeout -k 10 500 python bench.py --pmc-save $O/pmc > $O/bench_default.json 2> $O/bench_default.err
