@@ -179,7 +179,7 @@ Hit bounded_trace(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, Work &w)
 {
     float t1, t2;
     if (!scene_box(h, o, d, t1, t2)) return Hit{};
-    if (!rt_bounded_ray(o, d)) return kd_trace(h, o, d, t1, t2, -INFINITY, w);
+    if (!rt_bounded_ray(o, d, h.split_vals.data(), h.split_off)) return kd_trace(h, o, d, t1, t2, -INFINITY, w);
     const float s_min = bvh_bound(h, o, d, t2, w);
     if (!(s_min < t2)) return Hit{};
     return kd_trace(h, o, d, t1, t2, s_min, w);
