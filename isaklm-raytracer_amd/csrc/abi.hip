@@ -101,11 +101,18 @@ int upload_prepared(const rt_host::PreparedHost &h, int ntris, int nindices, rt_
     dv.bvh_bary = nullptr;
     dv.bvh_scale = h.bvh_scale;
     dv.split_vals = nullptr;
+    dv.kd_start = dv.kd_rows = nullptr;
     for (int a = 0; a < 4; ++a) dv.split_off[a] = h.split_off[a];
     if (h.bvh_depth >= 0 && ((rc = upload_vec(*s, h.bvh_nodes, &dv.bvh_nodes)) ||
                              (rc = upload_vec(*s, h.bvh_a, &dv.bvh_a)) ||
                              (rc = upload_vec(*s, h.bvh_bary, &dv.bvh_bary)) ||
                              (rc = upload_vec(*s, h.split_vals, &dv.split_vals)))) {
+        release(s);
+        return rc;
+    }
+    // the KD descent shortcut (RT_KD_RESUME=1 at prepare time: experiments, see build_kd_starts)
+    if (h.bvh_depth >= 0 && !h.kd_rows.empty() &&
+        ((rc = upload_vec(*s, h.kd_start, &dv.kd_start)) || (rc = upload_vec(*s, h.kd_rows, &dv.kd_rows)))) {
         release(s);
         return rc;
     }

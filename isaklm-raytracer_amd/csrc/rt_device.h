@@ -96,6 +96,10 @@ struct RtDevScene {
     float bvh_scale;            // largest |vertex|_1 (rt_ray_margin)
     const float *split_vals;    // the KD tree's split values, per axis sorted (rt_bounded_ray)
     int split_off[4];           // axis a: split_vals[split_off[a], split_off[a + 1])
+    // KD descent shortcut (host/scene_prepare.cpp build_kd_starts, bvh_trace.h
+    // kd_resume); nullptr: none
+    const uint32_t *kd_start;   // per BVH leaf slot (its first): {start node, row offset << 5 | depth}
+    const uint32_t *kd_rows;    // 4 words per ancestor: split bits, y word, ancestor index, child taken
 };
 
 // BVH child reference: an inner node's index, or RT_BVH_LEAF | first << 3 |

@@ -193,7 +193,7 @@ __device__ __forceinline__ void publish_long(const WfState &st, bool to_long, ui
 {
     uint32_t e = 0;
     if (to_long) {
-        st.heavy[slot] = 1;
+        st.heavy[slot] = st.heavy[slot] | 1u;
         e = __hip_atomic_fetch_add(st.long_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         st.long_ray[2 * (size_t)e] = RtF4{o.x, o.y, o.z, 0.0f};
         st.long_ray[2 * (size_t)e + 1] = RtF4{d.x, d.y, d.z, 0.0f};
@@ -234,7 +234,7 @@ __device__ __forceinline__ bool publish_long_capped(const WfState &st, bool to_l
     if (base == 0xffffffffu) return false;
     const uint32_t e = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
     if (to_long) {
-        st.heavy[slot] = 1;
+        st.heavy[slot] = st.heavy[slot] | 1u;
         st.long_ray[2 * (size_t)e] = RtF4{o.x, o.y, o.z, 0.0f};
         st.long_ray[2 * (size_t)e + 1] = RtF4{d.x, d.y, d.z, 0.0f};
     }
@@ -313,8 +313,9 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_start(RtDevFrame fr, RtDevCamera 
     if (st.heavy_first) { // the whole-call finisher: no ray queue; heavy pixels on list 1
         bool h = false;
         if (valid && slot < n) {
-            h = st.heavy[slot] != 0;
-            if (h) st.heavy[slot] = 0; // set again by this call's hand-offs
+            const uint8_t v = st.heavy[slot];
+            h = v != 0;
+            if (v & 1u) st.heavy[slot] = v & 2u; // bit 0: set again by this call's hand-offs (bit 1 stays)
         }
         enqueue_path(st, 1, want && h, (uint32_t)slot);
         enqueue_path(st, 0, want && !h, (uint32_t)slot);
@@ -1046,7 +1047,11 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_FIN_BVH_WAVES) wf_finish_bvh(RtDe
         if (active) {
             float bx = 0.0f, by = 0.0f, bz = 0.0f;
             const int hit = trace_bvh<COUNT>(sc, p.ro, p.rd, bx, by, bz, stk, c);
+            const bool cam_ray = !p.shadow && p.depth == 1;
             const bool want = shade_step<COUNT>(sc, fr, cam, p, hit, bx, by, bz, limit, c);
+            // heavy-first ordering: a pixel whose camera ray enters glass (where the
+            // deep total-internal-reflection paths start) is marked for later calls
+            if (st.heavy_first && cam_ray && want && p.inside && !(st.heavy[p.slot] & 2u)) st.heavy[p.slot] |= 2u;
             // a path deeper than long_depth goes on in wf_long (64 lanes per ray)
             to_long = want && st.long_depth > 0 && p.depth > st.long_depth;
             if (!want || to_long) store_regs(st, fr, p);
@@ -1353,6 +1358,12 @@ struct Workspace {
     hipEvent_t fork = nullptr, ev0 = nullptr, ev1 = nullptr;
     hipEvent_t long_ev = nullptr; // after the last wf_long slice on the caller's stream
     bool recorded = false;   // long_ev recorded by a previous call
+    // CU partition of the whole-call finisher mode: wf_long on `long_cus` CUs of
+    // its own, the finisher pipeline on the rest (0: shared CUs, the caller's stream)
+    int long_cus = 0;
+    int total_cus = 0;
+    hipStream_t long_stream = nullptr, fin_stream = nullptr;
+    hipEvent_t part_ev = nullptr;
     RtProfile prof{};        // last profiled call
 };
 
@@ -1384,6 +1395,37 @@ int ensure_streams(Workspace &w, int npipes)
         hipLaunchKernelGGL(wf_bind_stream, dim3(1), dim3(64), 0, p.stream);
         if (hipGetLastError() != hipSuccess || hipStreamSynchronize(p.stream) != hipSuccess) return -1;
     }
+    return 0;
+}
+
+// the CU-partitioned streams (created once, on the first whole-call launch that
+// asks for them): wf_long's stream on `cus` CUs spread over the chip, the
+// finisher's on the others.  Returns 0 with no partition when the runtime
+// refuses a CU-masked stream.
+int ensure_partition(Workspace &w, int cus)
+{
+    if (w.long_stream || cus <= 0) return 0;
+    int dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return -1;
+    const int n = prop.multiProcessorCount;
+    if (cus >= n) return 0;
+    std::vector<uint32_t> lm((size_t)(n + 31) / 32, 0u), fm((size_t)(n + 31) / 32, 0u);
+    for (int k = 0; k < cus; ++k) {
+        const int cu = (int)(((long long)k * n) / cus);
+        lm[(size_t)cu / 32] |= 1u << (cu % 32);
+    }
+    for (int cu = 0; cu < n; ++cu)
+        if (!(lm[(size_t)cu / 32] >> (cu % 32) & 1u)) fm[(size_t)cu / 32] |= 1u << (cu % 32);
+    if (hipExtStreamCreateWithCUMask(&w.long_stream, (uint32_t)lm.size(), lm.data()) != hipSuccess ||
+        hipExtStreamCreateWithCUMask(&w.fin_stream, (uint32_t)fm.size(), fm.data()) != hipSuccess) {
+        (void)hipGetLastError();
+        w.long_stream = w.fin_stream = nullptr;
+        return 0;
+    }
+    if (hipEventCreateWithFlags(&w.part_ev, hipEventDisableTiming) != hipSuccess) return -1;
+    w.long_cus = cus;
+    w.total_cus = n;
     return 0;
 }
 
@@ -1573,6 +1615,12 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
     const int long_depth = trace_kind == 1 && long_opt >= 0 ? (long_opt > 0 ? long_opt : WF_LONG_DEPTH_DEFAULT) : 0;
     for (int pi = 0; pi < WF_MAX_PIPES; ++pi) w.pipe[pi].st.long_depth = long_depth;
     const WfState &lst = w.pipe[0].st;
+    // RT_WF_LONG_CUS=K (experiments): in the whole-call mode wf_long runs on K CUs of its own and the
+    // finisher on the others, so that a deep path's dependent loads do not queue behind the bulk's
+    static const int long_cus_env = getenv("RT_WF_LONG_CUS") ? atoi(getenv("RT_WF_LONG_CUS")) : 0;
+    if (whole && long_depth > 0 && long_cus_env > 0 && ensure_partition(w, long_cus_env) != 0) return -1;
+    const bool part = whole && long_depth > 0 && w.long_stream != nullptr;
+    hipStream_t const lstream = part ? w.long_stream : stream; // wf_long's slices
 
     // the workspace (per-pixel path state, long-path hand-off) is shared by every
     // call on this device: a call on another stream than the previous one must
@@ -1601,6 +1649,7 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
     }
     // fork: every pipeline stream starts after the caller's stream
     if (hipEventRecord(w.fork, stream) != hipSuccess) return -1;
+    if (part && hipStreamWaitEvent(lstream, w.fork, 0) != hipSuccess) return -1;
     if (prof && hipEventRecord(w.ev0, stream) != hipSuccess) return -1;
     std::mutex long_mu;
     bool long_final = false;
@@ -1618,14 +1667,14 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
         }
         const int fin = final ? 1 : 0;
         if (count)
-            hipLaunchKernelGGL(wf_long<true>, dim3(WF_LONG_BLOCKS), dim3(WF_BLOCK), 0, stream, sc, fr, cam, lst, fin, 0);
+            hipLaunchKernelGGL(wf_long<true>, dim3(WF_LONG_BLOCKS), dim3(WF_BLOCK), 0, lstream, sc, fr, cam, lst, fin, 0);
         else
-            hipLaunchKernelGGL(wf_long<false>, dim3(WF_LONG_BLOCKS), dim3(WF_BLOCK), 0, stream, sc, fr, cam, lst, fin,
+            hipLaunchKernelGGL(wf_long<false>, dim3(WF_LONG_BLOCKS), dim3(WF_BLOCK), 0, lstream, sc, fr, cam, lst, fin,
                                bounded && long_uni ? 1 : 0);
         if (hipGetLastError() != hipSuccess) return -1;
         long_final = final;
         ++n_slices;
-        if (hipEventRecord(w.long_ev, stream) != hipSuccess) return -1;
+        if (hipEventRecord(w.long_ev, lstream) != hipSuccess) return -1;
         w.recorded = true;
         return 0;
     };
@@ -1646,7 +1695,7 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
         Pipe &pp = w.pipe[pi];
         pp.trace_iv.clear();
         WfState &st = pp.st;
-        hipStream_t s = pp.stream;
+        hipStream_t s = part && pi == 0 ? w.fin_stream : pp.stream;
         if (hipStreamWaitEvent(s, w.fork, 0) != hipSuccess) return -1;
         RtProfile P{};
         auto mark = [&](int i) { return !prof || hipEventRecord(pp.ev[i], s) == hipSuccess; };
@@ -1664,7 +1713,11 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
                 // otherwise hold every wave slot until they end, and the deep paths they hand over
                 // would start only then
                 int fgrid = (int)((live + WF_BLOCK - 1) / WF_BLOCK);
-                const int fmax = long_depth > 0 ? grid - (WF_LONG_BLOCKS + npipes - 1) / npipes : grid;
+                int fmax = long_depth > 0 ? grid - (WF_LONG_BLOCKS + npipes - 1) / npipes : grid;
+                if (part) { // the finisher's CUs at its occupancy (every block resident)
+                    const int pmax = (w.total_cus - w.long_cus) * 4 * WF_FIN_BVH_WAVES / (WF_BLOCK / 64);
+                    fmax = pmax < grid ? pmax : grid;
+                }
                 fgrid = fgrid > fmax ? fmax : fgrid;
                 if (hipMemsetAsync(st.counts + 4, 0, 4, s) != hipSuccess) return -1;
                 if (count) hipLaunchKernelGGL(wf_finish_bvh<true>, dim3(fgrid), dim3(WF_BLOCK), 0, s, sc, fr, cam, st, qq);
@@ -1826,9 +1879,10 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
     }
     for (int pi = 0; pi < npipes; ++pi)
         if (rcs[pi] != 0) return rcs[pi];
-    // join: the caller's stream continues after every pipeline
+    // join: the caller's stream continues after every pipeline (and wf_long's own stream)
     for (int pi = 0; pi < npipes; ++pi)
         if (hipStreamWaitEvent(stream, w.pipe[pi].join, 0) != hipSuccess) return -1;
+    if (part && hipStreamWaitEvent(stream, w.long_ev, 0) != hipSuccess) return -1;
     if (prof) {
         RtProfile P{};
         for (int pi = 0; pi < npipes; ++pi) { // kernel times summed over the (concurrent) pipelines

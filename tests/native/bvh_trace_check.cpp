@@ -26,6 +26,7 @@
 namespace {
 
 bool g_debug = false;
+bool g_no_grid = false;
 
 float bitsf(uint32_t u)
 {
@@ -35,7 +36,18 @@ float bitsf(uint32_t u)
 }
 
 struct Work {
-    long long nodes = 0, tests = 0, bvh_nodes = 0, bvh_tests = 0, leaves = 0;
+    long long nodes = 0, tests = 0, bvh_nodes = 0, bvh_tests = 0, leaves = 0, resumed = 0, resume_failed = 0,
+              rows = 0;
+};
+
+struct E { uint32_t node; float entry; };
+
+// the state the descent resumes from (kd_resume): node, interval, stack
+struct Resume {
+    uint32_t node = 0;
+    float entry = 0, exit_ = 0;
+    int sp = 0;
+    E stk[64];
 };
 
 struct Hit {
@@ -61,14 +73,21 @@ bool test(const RtF4 *A, const RtIsectBary *R, uint32_t e, Vec3D o, Vec3D d, flo
 
 // the KD traversal with s_min = -inf is trace_ray itself; with the bound it
 // is bvh_trace.h's step 3
-Hit kd_trace(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, float entry, float exit_, float s_min, Work &w)
+Hit kd_trace(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, float entry, float exit_, float s_min, Work &w,
+             const Resume *from = nullptr)
 {
     Hit hit;
-    struct E { uint32_t node; float entry; };
     E stk[64];
     int sp = 0;
     const float root_exit = exit_;
     uint32_t node = 0;
+    if (from) {
+        node = from->node;
+        entry = from->entry;
+        exit_ = from->exit_;
+        sp = from->sp;
+        memcpy(stk, from->stk, sizeof(E) * (size_t)sp);
+    }
     while (true) {
         uint32_t nx = h.nodes[2 * node], ny = h.nodes[2 * node + 1];
         ++w.nodes;
@@ -123,8 +142,9 @@ Hit kd_trace(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, float entry, floa
     }
 }
 
-float bvh_bound(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, float best, Work &w)
+float bvh_bound(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, float best, Work &w, uint32_t *best_first = nullptr)
 {
+    if (best_first) *best_first = RT_BVH_EMPTY;
     const float m = rt_ray_margin(o.x, o.y, o.z, h.bvh_scale);
     const Vec3D om = rt_v3(o.x + m, o.y + m, o.z + m), op = rt_v3(o.x - m, o.y - m, o.z - m);
     const Vec3D inv = rt_v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
@@ -159,7 +179,10 @@ float bvh_bound(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, float best, Wo
             for (uint32_t e = first; e < end; ++e) {
                 float s, b[3];
                 ++w.bvh_tests;
-                if (test(h.bvh_a.data(), h.bvh_bary.data(), e, o, d, best, s, b)) best = s;
+                if (test(h.bvh_a.data(), h.bvh_bary.data(), e, o, d, best, s, b)) {
+                    best = s;
+                    if (best_first) *best_first = first;
+                }
             }
         }
         bool more = false;
@@ -175,13 +198,96 @@ float bvh_bound(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, float best, Wo
     }
 }
 
+// restatement of bvh_trace.h kd_resume: replay the bounded descent along the
+// stored root path of the leaf's start node, each decision checked
+// the start record of the ray: the deeper of its s_min leaf's and of the grid
+// cell of o + d * s_min (bvh_trace.h kd_pick)
+void kd_pick(const rt_host::PreparedHost &h, uint32_t best_first, Vec3D o, Vec3D d, float s_min, uint32_t &start,
+             uint32_t &packed)
+{
+    start = packed = 0xFFFFFFFFu;
+    if (best_first != RT_BVH_EMPTY) {
+        start = h.kd_start[2 * (size_t)best_first];
+        packed = h.kd_start[2 * (size_t)best_first + 1];
+    }
+    if (h.kd_grid > 0 && !g_no_grid) {
+        const int G = h.kd_grid;
+        const float p[3] = {o.x + d.x * s_min, o.y + d.y * s_min, o.z + d.z * s_min};
+        const float bmin[3] = {h.bounds.min.x, h.bounds.min.y, h.bounds.min.z};
+        int c[3];
+        for (int a = 0; a < 3; ++a) {
+            const float f = (p[a] - bmin[a]) * h.kd_grid_scale[a];
+            c[a] = f >= 0.0f ? (f < (float)(G - 1) ? (int)f : G - 1) : 0; // (NaN: 0)
+        }
+        const size_t k = ((size_t)c[2] * G + c[1]) * G + c[0];
+        const uint32_t cs = h.kd_cell[2 * k], cp = h.kd_cell[2 * k + 1];
+        if (cs != 0xFFFFFFFFu && (start == 0xFFFFFFFFu || (cp & 31u) > (packed & 31u))) {
+            start = cs;
+            packed = cp;
+        }
+    }
+}
+
+bool kd_resume(const rt_host::PreparedHost &h, uint32_t start, uint32_t packed, Vec3D o, Vec3D d, float entry,
+               float exit_, float s_min, Resume &r, Work &w)
+{
+    if (start == 0xFFFFFFFFu) return false;
+    const uint32_t depth = packed & 31u;
+    const uint32_t *row = h.kd_rows.data() + 4 * (size_t)(packed >> 5);
+    r.sp = 0;
+    for (uint32_t k = 0; k < depth; ++k) {
+        const uint32_t *rec = row + 4 * k;
+        ++w.rows;
+        const uint32_t axis = rec[1] & 3u, anc = rec[2];
+        const float split = bitsf(rec[0]);
+        const float oax = axis == 0 ? o.x : (axis == 1 ? o.y : o.z);
+        const float dax = axis == 0 ? d.x : (axis == 1 ? d.y : d.z);
+        uint32_t near_c = anc + 1, far_c = rec[1] >> 2;
+        if (oax >= split) {
+            near_c = rec[1] >> 2;
+            far_c = anc + 1;
+        }
+        const uint32_t taken = rec[3] ? rec[1] >> 2 : anc + 1;
+        const float t = (split - oax) / dax;
+        if (t >= exit_ || t < 0) {
+            if (near_c != taken) return false;
+        } else if (t <= entry) {
+            if (far_c != taken) return false;
+        } else if (t <= s_min) {
+            if (far_c != taken) return false;
+            entry = t;
+        } else {
+            if (near_c != taken) return false;
+            r.stk[r.sp++] = E{far_c, t};
+            exit_ = t;
+        }
+    }
+    r.node = start;
+    r.entry = entry;
+    r.exit_ = exit_;
+    return true;
+}
+
+bool g_resume = true;
+
 Hit bounded_trace(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, Work &w)
 {
     float t1, t2;
     if (!scene_box(h, o, d, t1, t2)) return Hit{};
     if (!rt_bounded_ray(o, d, h.split_vals.data(), h.split_off)) return kd_trace(h, o, d, t1, t2, -INFINITY, w);
-    const float s_min = bvh_bound(h, o, d, t2, w);
+    uint32_t bf;
+    const float s_min = bvh_bound(h, o, d, t2, w, &bf);
     if (!(s_min < t2)) return Hit{};
+    if (g_resume && !h.kd_start.empty()) {
+        Resume r;
+        uint32_t start, packed;
+        kd_pick(h, bf, o, d, s_min, start, packed);
+        if (kd_resume(h, start, packed, o, d, t1, t2, s_min, r, w)) {
+            ++w.resumed;
+            return kd_trace(h, o, d, t1, t2, s_min, w, &r);
+        }
+        ++w.resume_failed;
+    }
     return kd_trace(h, o, d, t1, t2, s_min, w);
 }
 
@@ -201,6 +307,9 @@ int main(int argc, char **argv)
         return 2;
     }
     const long long rays = argc > 2 ? atoll(argv[2]) : 200000;
+    g_resume = !getenv("RT_KD_RESUME") || atoi(getenv("RT_KD_RESUME")) != 0;
+    setenv("RT_KD_RESUME", g_resume ? "1" : "0", 1); // prepare_host builds the shortcut's tables
+    if (getenv("RT_KD_NO_GRID")) g_no_grid = true;
     std::mt19937_64 rng(argc > 3 ? strtoull(argv[3], nullptr, 10) : 7);
     RtHostScene scene;
     Camera cam;
@@ -327,6 +436,9 @@ int main(int argc, char **argv)
             wb.leaves += lb.leaves;
             wb.bvh_nodes += lb.bvh_nodes;
             wb.bvh_tests += lb.bvh_tests;
+            wb.resumed += lb.resumed;
+            wb.resume_failed += lb.resume_failed;
+            wb.rows += lb.rows;
         }
     }
     (void)unit;
@@ -335,5 +447,7 @@ int main(int argc, char **argv)
     printf("kd-only per ray: nodes %.1f leaves %.1f tests %.1f\n", wp.nodes / R, wp.leaves / R, wp.tests / R);
     printf("bounded per ray: bvh nodes %.1f bvh tests %.1f kd nodes %.1f leaves %.2f tests %.1f\n", wb.bvh_nodes / R,
            wb.bvh_tests / R, wb.nodes / R, wb.leaves / R, wb.tests / R);
+    printf("kd resume: %lld resumed, %lld fell back to the root, %.1f path records per ray (%zu rows)\n", wb.resumed,
+           wb.resume_failed, wb.rows / R, h.kd_rows.size() / 4);
     return mism == 0 ? 0 : 1;
 }
