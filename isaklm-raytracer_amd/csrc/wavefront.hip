@@ -105,6 +105,7 @@ static_assert(WF_BLOCK % WF_TBLOCK == 0 && WF_TBLOCK % 64 == 0, "WF_TBLOCK must 
 #define WF_MAX_PIPES 6                // concurrent pipelines (RtOptions.wf_pipelines); more than 3 need GPU_MAX_HW_QUEUES > 4
 #define WF_PIPES_DEFAULT 3
 #define WF_LONG_DEPTH_DEFAULT 64      // RtOptions.wf_long_depth: paths deeper than this go to wf_long
+#define WF_LONG_CUS_DEFAULT 16        // whole-call mode: CUs of wf_long's own (long_cus)
 #define WF_LONG_BLOCKS 64             // wf_long grid (4 waves each, one path per wave at a time)
 #define WF_LONG_IDLE 2000000000ull   // s_memrealtime ticks (100 MHz): 20 s without a claim ends a wf_long wave
 
@@ -133,6 +134,7 @@ struct WfState {
     // the finishers, whose lanes run its remaining passes
     int long_return;
     unsigned long long *ret_ring; // entry e at e % long_cap: (e + 1) << 32 | slot once published
+    unsigned long long *long_log; // debug (RT_WF_LONG_LOG): [0] call start, then per claim {claim, end, bounces, slot}
     // ret_ctr: u64 [0] = finisher waves alive << 32 | returns reserved (wf_long
     // reserves only while a finisher wave is alive; a wave leaves only when
     // every reserved return is claimed: no pixel is stranded, and neither
@@ -283,6 +285,7 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_start(RtDevFrame fr, RtDevCamera 
     const int x = (tile % tiles_x) * 16 + (wave & 1) * 8 + (lane & 7);
     const int y = (tile / tiles_x) * 16 + (wave >> 1) * 8 + (lane >> 3);
     const bool valid = x < fr.width && y < fr.height && rt_row_owned(fr, y);
+    if (st.long_log && blockIdx.x == 0 && tid == 0) st.long_log[0] = __builtin_amdgcn_s_memrealtime();
     const int slot = valid ? y * fr.width + x : 0;
     bool want = false;
     Vec3D ro = rt_v3(0, 0, 0), rd = rt_v3(0, 0, 0);
@@ -1262,7 +1265,10 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_LONG_WAVES) wf_long(RtDevScene sc
         }
         int want = 0; // after the loop: 0 the pixel's passes are done, 2 returned to the finishers
         uint32_t ret_e = 0;
+        const unsigned long long t_claim = __builtin_amdgcn_s_memrealtime();
+        uint32_t bounces = 0;
         while (true) {
+            ++bounces;
             int hit = -1;
             float bx = 0.0f, by = 0.0f, bz = 0.0f;
             if (!COUNT && bounded) {
@@ -1309,6 +1315,13 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_LONG_WAVES) wf_long(RtDevScene sc
             if (want != 1) break;
         }
         if (lane == 0) {
+            if (st.long_log && e < 65535u) {
+                unsigned long long *L = st.long_log + 4 + 4 * (size_t)e;
+                L[0] = t_claim;
+                L[1] = __builtin_amdgcn_s_memrealtime();
+                L[2] = bounces;
+                L[3] = p.slot;
+            }
             store_regs(st, fr, p);
             if (want == 2) { // back to the finishers: its next ray, then its ring entry
                 st.ro[p.slot] = p.ro;
@@ -1396,6 +1409,16 @@ int ensure_streams(Workspace &w, int npipes)
         if (hipGetLastError() != hipSuccess || hipStreamSynchronize(p.stream) != hipSuccess) return -1;
     }
     return 0;
+}
+
+// CUs of wf_long's own in the whole-call mode (RT_WF_LONG_CUS overrides; 0:
+// shared CUs).  Measured per 256-pass room2m call (median of 5 calls, two
+// rounds, tools/gpu_r03_cu.sh): 0 / 8 / 16 / 32 CUs 1.54-1.78 / 1.51-1.53 /
+// 1.49-1.51 / 1.59-2.00 s, the calls' spread smallest at 16
+int long_cus()
+{
+    static const int k = getenv("RT_WF_LONG_CUS") ? atoi(getenv("RT_WF_LONG_CUS")) : WF_LONG_CUS_DEFAULT;
+    return k;
 }
 
 // the CU-partitioned streams (created once, on the first whole-call launch that
@@ -1516,13 +1539,15 @@ float elapsed_ms(hipEvent_t a, hipEvent_t b)
 
 } // namespace
 
-// rt_set_device: the default pipelines' streams take their hardware queues
-// before anything else in the process (RCCL's streams in a multi-GPU run)
+// rt_set_device: the default pipelines' streams (and the CU-partitioned ones
+// of the whole-call mode) take their hardware queues before anything else in
+// the process (RCCL's streams in a multi-GPU run)
 int rt_wavefront_device_init()
 {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return -1;
-    return ensure_streams(g_ws[dev], WF_PIPES_DEFAULT);
+    if (ensure_streams(g_ws[dev], WF_PIPES_DEFAULT) != 0) return -1;
+    return long_cus() > 0 ? ensure_partition(g_ws[dev], long_cus()) : 0;
 }
 
 extern "C" int rt_last_profile(RtProfile *out)
@@ -1615,11 +1640,17 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
     const int long_depth = trace_kind == 1 && long_opt >= 0 ? (long_opt > 0 ? long_opt : WF_LONG_DEPTH_DEFAULT) : 0;
     for (int pi = 0; pi < WF_MAX_PIPES; ++pi) w.pipe[pi].st.long_depth = long_depth;
     const WfState &lst = w.pipe[0].st;
-    // RT_WF_LONG_CUS=K (experiments): in the whole-call mode wf_long runs on K CUs of its own and the
-    // finisher on the others, so that a deep path's dependent loads do not queue behind the bulk's
-    static const int long_cus_env = getenv("RT_WF_LONG_CUS") ? atoi(getenv("RT_WF_LONG_CUS")) : 0;
-    if (whole && long_depth > 0 && long_cus_env > 0 && ensure_partition(w, long_cus_env) != 0) return -1;
+    // in the whole-call mode wf_long runs on long_cus() CUs of its own and the finisher on the
+    // others (streams created by rt_set_device): a deep path's bounces do not wait behind the
+    // bulk's waves on its CU
+    if (whole && long_depth > 0 && long_cus() > 0 && ensure_partition(w, long_cus()) != 0) return -1;
     const bool part = whole && long_depth > 0 && w.long_stream != nullptr;
+    // RT_WF_LONG_LOG=1 (debug): log every deep sample's claim / end time and bounces, printed after the call
+    static const bool long_log = getenv("RT_WF_LONG_LOG") != nullptr;
+    static unsigned long long *long_log_buf = nullptr;
+    if (long_log && !long_log_buf && hipMalloc((void **)&long_log_buf, 8 * 4 * 65536) != hipSuccess) return -1;
+    for (int pi = 0; pi < WF_MAX_PIPES; ++pi) w.pipe[pi].st.long_log = long_log ? long_log_buf : nullptr;
+    if (long_log && hipMemsetAsync(long_log_buf, 0, 8 * 4 * 65536, stream) != hipSuccess) return -1;
     hipStream_t const lstream = part ? w.long_stream : stream; // wf_long's slices
 
     // the workspace (per-pixel path state, long-path hand-off) is shared by every
@@ -1876,6 +1907,30 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
             fprintf(stderr, "[wf] returns reserved %u claimed %u, finisher waves alive %u, pixels out %u\n", rc4[0],
                     rc4[2], rc4[1], rc4[3]);
         }
+    }
+    if (long_log) {
+        (void)hipDeviceSynchronize();
+        std::vector<unsigned long long> L(4 * 65536);
+        (void)hipMemcpy(L.data(), long_log_buf, 8 * L.size(), hipMemcpyDeviceToHost);
+        struct Rec { double start, end; unsigned long long bounces, slot; };
+        std::vector<Rec> v;
+        double last = 0;
+        for (size_t e = 1; e < 65536; ++e)
+            if (L[4 * e + 1]) {
+                v.push_back({(L[4 * e] - L[0]) * 1e-5, (L[4 * e + 1] - L[0]) * 1e-5, L[4 * e + 2], L[4 * e + 3]});
+                last = std::max(last, v.back().end);
+            }
+        std::sort(v.begin(), v.end(), [](const Rec &a, const Rec &b) { return a.end > b.end; });
+        fprintf(stderr, "[wf long log] %zu deep samples, last end %.1f ms; latest 12 (start ms, end ms, bounces, us/bounce, slot):\n",
+                v.size(), last);
+        for (size_t i = 0; i < v.size() && i < 12; ++i)
+            fprintf(stderr, "  %.1f %.1f %llu %.2f %llu\n", v[i].start, v[i].end, v[i].bounces,
+                    (v[i].end - v[i].start) * 1e3 / (double)(v[i].bounces ? v[i].bounces : 1), v[i].slot);
+        std::sort(v.begin(), v.end(), [](const Rec &a, const Rec &b) { return a.bounces > b.bounces; });
+        fprintf(stderr, "[wf long log] longest 8:\n");
+        for (size_t i = 0; i < v.size() && i < 8; ++i)
+            fprintf(stderr, "  %.1f %.1f %llu %.2f %llu\n", v[i].start, v[i].end, v[i].bounces,
+                    (v[i].end - v[i].start) * 1e3 / (double)(v[i].bounces ? v[i].bounces : 1), v[i].slot);
     }
     for (int pi = 0; pi < npipes; ++pi)
         if (rcs[pi] != 0) return rcs[pi];

@@ -314,12 +314,21 @@ def test_room2m_glass_adaptive_full_frame_sparse_pixels():
     assert helpers.rel_linf(gpu[0][pixels], gpu[2][pixels], ref[0][pixels], ref[2][pixels]) < 1e-4
 
 
-def test_consecutive_calls_on_different_streams():
+@pytest.mark.parametrize("long_depth,pipes,traversal", [
+    (1, (0, 0), None),
+    (-1, (3, 1), None),
+    (1, (1, 3), "kd"),
+    (-1, (0, 2), "kd"),
+])
+def test_consecutive_calls_on_different_streams(long_depth, pipes, traversal):
     """rt_render on stream A, then at once on stream B (no host sync between):
     the second call shares the device workspace (path state, long-path
     hand-off) and must wait for the first call's last wf_long slice and
-    pipelines.  Every path deeper than 1 bounce goes through wf_long here, so
-    the first call's slices are still running when the second starts."""
+    pipelines.  With wf_long_depth 1 every path deeper than 1 bounce goes
+    through wf_long, so the first call's slices are still running when the
+    second starts; with -1 (no hand-off) and a different pipeline count on
+    the second call, pixels move to other pipelines while the first call's
+    finisher may still write their path state."""
     import ctypes
 
     hip = ctypes.CDLL("libamdhip64.so")
@@ -330,8 +339,10 @@ def test_consecutive_calls_on_different_streams():
         run = helpers.GpuRun("room_small")
         W, H, P = 48, 27, 3
         g = rt.GBuffer(W, H)
+        trav = {None: None, "kd": rt.TRAVERSAL_KD}[traversal]
         for c, s in enumerate(streams):
-            opt = rt.options(W, H, P, adaptive=False, kernel=rt.KERNEL_WAVEFRONT, wf_long_depth=1, stream=s)
+            opt = rt.options(W, H, P, adaptive=False, kernel=rt.KERNEL_WAVEFRONT, wf_long_depth=long_depth, stream=s,
+                             wf_pipelines=pipes[c], traversal=trav)
             rt.render(run.dev, g, run.camera, 0 if c == 0 else 1, opt)
         rt.check(rt.lib().rt_synchronize())
         gpu = g.download()
