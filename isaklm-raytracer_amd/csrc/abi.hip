@@ -102,6 +102,8 @@ int upload_prepared(const rt_host::PreparedHost &h, int ntris, int nindices, rt_
     dv.bvh_scale = h.bvh_scale;
     dv.split_vals = nullptr;
     dv.kd_start = dv.kd_rows = nullptr;
+    dv.bvh8 = nullptr;
+    dv.kd_resume_bulk = getenv("RT_KD_RESUME") && atoi(getenv("RT_KD_RESUME")) != 0 ? 1 : 0;
     for (int a = 0; a < 4; ++a) dv.split_off[a] = h.split_off[a];
     if (h.bvh_depth >= 0 && ((rc = upload_vec(*s, h.bvh_nodes, &dv.bvh_nodes)) ||
                              (rc = upload_vec(*s, h.bvh_a, &dv.bvh_a)) ||
@@ -110,12 +112,18 @@ int upload_prepared(const rt_host::PreparedHost &h, int ntris, int nindices, rt_
         release(s);
         return rc;
     }
-    // the KD descent shortcut (RT_KD_RESUME=1 at prepare time: experiments, see build_kd_starts)
-    if (h.bvh_depth >= 0 && !h.kd_rows.empty() &&
-        ((rc = upload_vec(*s, h.kd_start, &dv.kd_start)) || (rc = upload_vec(*s, h.kd_rows, &dv.kd_rows)))) {
+    // the lone-ray traversal's tables (lone_trace.h): the 8-wide BVH and the KD descent shortcut
+    // (RT_LONE=1: wf_long's deep paths take it instead of the wide KD traversal; experiments —
+    // exact, but 26 vs 18 us per deep bounce on room2m)
+    static const bool lone = getenv("RT_LONE") && atoi(getenv("RT_LONE")) != 0;
+    if (h.bvh_depth >= 0 && !h.bvh8.empty() && (lone || dv.kd_resume_bulk) &&
+        ((rc = upload_vec(*s, h.bvh8, &dv.bvh8)) ||
+         (!h.kd_rows.empty() && ((rc = upload_vec(*s, h.kd_start, &dv.kd_start)) ||
+                                 (rc = upload_vec(*s, h.kd_rows, &dv.kd_rows)))))) {
         release(s);
         return rc;
     }
+    if (!lone) dv.bvh8 = nullptr;
     dv.nodes = nodes;
     dv.isect_a = a;
     dv.isect_bary = bary;

@@ -286,7 +286,7 @@ __device__ __forceinline__ int trace_bvh(const RtDevScene &sc, const Vec3D o, co
     const float yx = rt_recip_guard(d.x), yy = rt_recip_guard(d.y), yz = rt_recip_guard(d.z);
     int sp = 0;
     uint32_t node = 0;
-    if (sc.kd_rows && best_first != RT_BVH_EMPTY &&
+    if (sc.kd_resume_bulk && sc.kd_rows && best_first != RT_BVH_EMPTY &&
         !kd_resume<COUNT>(sc, best_first, o, d, yx, yy, yz, s_min, node, entry, exit_, sp, stk, c)) {
         node = 0; // (a difference: the descent from the root; entry / exit untouched)
         sp = 0;

@@ -71,6 +71,7 @@ struct PreparedHost {
     // ancestor {split bits, y word, ancestor index, 0 = child0 / 1 = child1}
     // ... and per cell of a kd_grid^3 grid over the scene box (kd_cell, the
     // same pairs; cell of a point: (p - bounds.min) * kd_grid_scale)
+    std::vector<RtF4> bvh8;               // 8-wide collapse of the BVH (lone_trace.h), 16 per node
     std::vector<uint32_t> kd_start;
     std::vector<uint32_t> kd_rows;
     std::vector<uint32_t> kd_cell;
@@ -79,6 +80,8 @@ struct PreparedHost {
 };
 // fills the shortcut tables from the prepared KD nodes and BVH (scene_prepare.cpp)
 void build_kd_starts(PreparedHost &out, const Bounding_Box &bounds);
+// fills bvh8 from bvh_nodes (scene_prepare.cpp)
+void build_bvh8(PreparedHost &out);
 int prepare_host(const Triangle *tris, int ntris, const KD_Tree_Node *nodes, int nnodes, const int *indices,
                  int nindices, const int *lights, int nlights, Bounding_Box bounds, PreparedHost &out);
 

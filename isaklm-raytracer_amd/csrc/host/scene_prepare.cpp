@@ -134,6 +134,88 @@ void build_kd_starts(PreparedHost &out, const Bounding_Box &bounds)
     for (int a = 0; a < 3; ++a) out.kd_grid_scale[a] = (float)G / ext[a];
 }
 
+// The 8-wide collapse of the binary BVH for lone_trace.h: starting from a
+// node's two children, the inner child with the largest box surface is
+// replaced by its two children until there are 8 (or only leaves).  Child
+// boxes and leaf references are the binary tree's own (the same conservative
+// boxes, the same leaves); an inner child refers to its 8-wide node.  Layout:
+// 16 RtF4 per node, child k = {lo.x, lo.y, lo.z, hi.x}, {hi.y, hi.z,
+// ref bits, 0}; ref RT_BVH_EMPTY for unused slots.
+void build_bvh8(PreparedHost &out)
+{
+    const size_t nb = out.bvh_nodes.size() / 4;
+    out.bvh8.clear();
+    if (nb == 0) return;
+    struct Child {
+        uint32_t ref;
+        float lo[3], hi[3];
+    };
+    auto child_of = [&](uint32_t node, int c) {
+        const RtF4 *nd = &out.bvh_nodes[4 * (size_t)node];
+        Child ch;
+        memcpy(&ch.ref, c == 0 ? &nd[3].x : &nd[3].y, 4);
+        if (c == 0) {
+            ch.lo[0] = nd[0].x; ch.lo[1] = nd[0].y; ch.lo[2] = nd[0].z;
+            ch.hi[0] = nd[0].w; ch.hi[1] = nd[1].x; ch.hi[2] = nd[1].y;
+        } else {
+            ch.lo[0] = nd[1].z; ch.lo[1] = nd[1].w; ch.lo[2] = nd[2].x;
+            ch.hi[0] = nd[2].y; ch.hi[1] = nd[2].z; ch.hi[2] = nd[2].w;
+        }
+        return ch;
+    };
+    std::vector<int> idx(nb, -1);
+    std::vector<std::vector<Child>> wide; // per 8-wide node, its children (binary refs)
+    std::vector<uint32_t> order{0};
+    idx[0] = 0;
+    for (size_t q = 0; q < order.size(); ++q) {
+        const uint32_t b = order[q];
+        std::vector<Child> ch;
+        for (int c = 0; c < 2; ++c) {
+            const Child x = child_of(b, c);
+            if (x.ref != RT_BVH_EMPTY) ch.push_back(x);
+        }
+        while (ch.size() < 8) {
+            int pick = -1;
+            float area = -1.0f;
+            for (size_t k = 0; k < ch.size(); ++k) {
+                if (ch[k].ref & RT_BVH_LEAF) continue;
+                const float ex = ch[k].hi[0] - ch[k].lo[0], ey = ch[k].hi[1] - ch[k].lo[1], ez = ch[k].hi[2] - ch[k].lo[2];
+                const float a = ex * ey + ey * ez + ez * ex;
+                if (!(a <= area)) { // (NaN or larger: take it)
+                    area = a;
+                    pick = (int)k;
+                }
+            }
+            if (pick < 0) break;
+            const uint32_t inner = ch[(size_t)pick].ref;
+            ch.erase(ch.begin() + pick);
+            for (int c = 0; c < 2; ++c) {
+                const Child x = child_of(inner, c);
+                if (x.ref != RT_BVH_EMPTY) ch.push_back(x);
+            }
+        }
+        for (const Child &x : ch)
+            if (!(x.ref & RT_BVH_LEAF) && idx[x.ref] < 0) {
+                idx[x.ref] = (int)order.size();
+                order.push_back(x.ref);
+            }
+        wide.push_back(std::move(ch));
+    }
+    out.bvh8.assign(16 * wide.size(), RtF4{0, 0, 0, 0});
+    for (size_t i = 0; i < wide.size(); ++i)
+        for (int k = 0; k < 8; ++k) {
+            RtF4 *d = &out.bvh8[16 * i + 2 * (size_t)k];
+            uint32_t ref = RT_BVH_EMPTY;
+            if ((size_t)k < wide[i].size()) {
+                const Child &x = wide[i][(size_t)k];
+                ref = (x.ref & RT_BVH_LEAF) ? x.ref : (uint32_t)idx[x.ref];
+                d[0] = RtF4{x.lo[0], x.lo[1], x.lo[2], x.hi[0]};
+                d[1] = RtF4{x.hi[1], x.hi[2], 0.0f, 0.0f};
+            }
+            memcpy(&d[1].z, &ref, 4);
+        }
+}
+
 int prepare_host(const Triangle *tris, int ntris, const KD_Tree_Node *nodes, int nnodes, const int *indices,
                  int nindices, const int *lights, int nlights, Bounding_Box bounds, PreparedHost &out)
 {
@@ -290,9 +372,14 @@ int prepare_host(const Triangle *tris, int ntris, const KD_Tree_Node *nodes, int
         }
         out.bvh_scale = bvh.scale;
         out.bvh_depth = bvh.depth;
-        // the KD descent shortcut: measured slower on the GPU (the bulk finisher is not bound by the
-        // descent's dependent loads: 1.04 vs 1.00 s per 256-pass room2m call), built on request only
-        if (getenv("RT_KD_RESUME") && atoi(getenv("RT_KD_RESUME")) != 0) build_kd_starts(out, bounds);
+        // the 8-wide BVH and the KD descent shortcut's tables, on request: the lone-ray traversal
+        // of the deep paths (RT_LONE=1, lone_trace.h) uses both, the bulk finisher the shortcut
+        // (RT_KD_RESUME=1).  Both measured slower than the defaults
+        auto on = [](const char *v) { return getenv(v) && atoi(getenv(v)) != 0; };
+        if (on("RT_LONE") || on("RT_KD_RESUME")) {
+            build_bvh8(out);
+            build_kd_starts(out, bounds);
+        }
         out.bvh_always = bvh.always;
         out.bvh_dropped = bvh.dropped;
     } else if (brc != RT_OK && brc != RT_E_UNSUPPORTED) {

@@ -100,6 +100,8 @@ struct RtDevScene {
     // kd_resume); nullptr: none
     const uint32_t *kd_start;   // per BVH leaf slot (its first): {start node, row offset << 5 | depth}
     const uint32_t *kd_rows;    // 4 words per ancestor: split bits, y word, ancestor index, child taken
+    int kd_resume_bulk;         // trace_bvh uses the shortcut too (RT_KD_RESUME=1; lone_trace always)
+    const RtF4 *bvh8;           // 8-wide BVH (lone_trace.h): 16 per node, child k {lo, hi.x}, {hi.yz, ref, 0}; nullptr: none
 };
 
 // BVH child reference: an inner node's index, or RT_BVH_LEAF | first << 3 |

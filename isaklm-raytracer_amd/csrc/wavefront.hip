@@ -27,6 +27,7 @@
 #include <vector>
 
 #include "bvh_trace.h"
+#include "lone_trace.h"
 #include "rt_kernels.h"
 
 using namespace rtk;
@@ -1207,6 +1208,8 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_LONG_WAVES) wf_long(RtDevScene sc
     __shared__ WideItem s_wide[(WF_BLOCK / 64) * WIDE_CAP];
     __shared__ unsigned long long s_key[(WF_BLOCK / 64) * 4];
     __shared__ int s_mark[2 * WF_BLOCK]; // 128 per wave: chunk_owner marks + junk slots
+    __shared__ uint32_t s_lnode[(WF_BLOCK / 64) * LONE_STACK]; // lone_trace: one stack per wave
+    __shared__ float s_lkey[(WF_BLOCK / 64) * LONE_STACK];
     if (WF_LONG_PRIO > 0) __builtin_amdgcn_s_setprio(WF_LONG_PRIO);
     const int lane = __lane_id();
     const int wave = threadIdx.x >> 6;
@@ -1271,7 +1274,16 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_LONG_WAVES) wf_long(RtDevScene sc
             ++bounces;
             int hit = -1;
             float bx = 0.0f, by = 0.0f, bz = 0.0f;
-            if (!COUNT && bounded) {
+            if (!COUNT && bounded == 2) {
+                // the deep path's ray with the lone-ray traversal (lone_trace.h): every lane on it
+                auto uni = [](float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); };
+                const Vec3D o = rt_v3(uni(p.ro.x), uni(p.ro.y), uni(p.ro.z));
+                const Vec3D d = rt_v3(uni(p.rd.x), uni(p.rd.y), uni(p.rd.z));
+                const LoneLds L{s_lnode + wave * LONE_STACK, s_lkey + wave * LONE_STACK};
+                WaveStack<WF_BVH_LDS> ws{s_wnode + wave * WF_BVH_LDS, s_wentry + wave * WF_BVH_LDS,
+                                         st.spill + blockIdx.x * (WF_BLOCK / 64) + wave, st.spill_threads};
+                hit = lone_trace(sc, o, d, bx, by, bz, L, ws, c);
+            } else if (!COUNT && bounded) {
                 // every lane traces lane 0's ray with the bounded traversal: wave-uniform
                 // addresses, so its node and record loads are scalar loads
                 auto uni = [](float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); };
@@ -1701,7 +1713,7 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
             hipLaunchKernelGGL(wf_long<true>, dim3(WF_LONG_BLOCKS), dim3(WF_BLOCK), 0, lstream, sc, fr, cam, lst, fin, 0);
         else
             hipLaunchKernelGGL(wf_long<false>, dim3(WF_LONG_BLOCKS), dim3(WF_BLOCK), 0, lstream, sc, fr, cam, lst, fin,
-                               bounded && long_uni ? 1 : 0);
+                               !bounded ? 0 : long_uni ? 1 : sc.bvh8 ? 2 : 0);
         if (hipGetLastError() != hipSuccess) return -1;
         long_final = final;
         ++n_slices;

@@ -62,9 +62,10 @@ def test_margins_never_cull_a_passing_test(margin_check, seed):
     assert float(stats["max_used"]) < 0.05, stats
 
 
-def _run_trace_check(exe, scene, rays=1_000_000, seed=7, cam=None):
+def _run_trace_check(exe, scene, rays=1_000_000, seed=7, cam=None, env=None):
     args = [exe, scene, str(rays), str(seed)] + ([" ".join(float(v).hex() for v in cam)] if cam is not None else [])
-    r = subprocess.run(args, capture_output=True, text=True, timeout=600, env=dict(os.environ, OMP_NUM_THREADS="4"))
+    r = subprocess.run(args, capture_output=True, text=True, timeout=600,
+                       env=dict(os.environ, OMP_NUM_THREADS="4", **(env or {})))
     assert r.returncode == 0, r.stdout + r.stderr
     return r.stdout
 
@@ -87,3 +88,18 @@ def test_bounded_equals_kd_hazard_scenes(trace_check, tmp_path):
     path = helpers.scene_path("cornell")
     on, _ = hazards.h5_cameras(oracle.OracleScene(path))
     assert "mismatches 0" in _run_trace_check(trace_check, path, 500_000, cam=on[:3])
+
+
+@pytest.mark.parametrize("grid", [True, False])
+def test_descent_shortcut_and_bvh8_host(trace_check, tmp_path, grid):
+    """The opt-in traversal tables (RT_KD_RESUME / RT_LONE): the KD descent
+    shortcut resumed from the s_min leaf's start node alone (the GPU's
+    lone_trace) or the deeper of it and the grid cell's, and the 8-wide BVH's
+    s_min, all equal to the plain KD traversal / the binary query."""
+    env = {} if grid else {"RT_KD_NO_GRID": "1"}
+    for path in (helpers.scene_path("cornell_blob"), helpers.make_trap_scene(str(tmp_path / "t"))):
+        out = _run_trace_check(trace_check, path, 300_000, seed=11, env=env)
+        assert "rays 300000" in out and " mismatches 0\n" in out, out
+        assert "s_min mismatches vs the binary query 0" in out, out
+        resumed = int(out.split("kd resume: ")[1].split(" resumed")[0])
+        assert resumed > 0, out
