@@ -103,6 +103,9 @@ int upload_prepared(const rt_host::PreparedHost &h, int ntris, int nindices, rt_
     dv.split_vals = nullptr;
     dv.kd_start = dv.kd_rows = nullptr;
     dv.bvh8 = nullptr;
+    dv.kd_cell = nullptr;
+    dv.kd_grid = 0;
+    for (int a = 0; a < 3; ++a) dv.kd_gscale[a] = h.kd_grid_scale[a];
     dv.kd_resume_bulk = getenv("RT_KD_RESUME") && atoi(getenv("RT_KD_RESUME")) != 0 ? 1 : 0;
     for (int a = 0; a < 4; ++a) dv.split_off[a] = h.split_off[a];
     if (h.bvh_depth >= 0 && ((rc = upload_vec(*s, h.bvh_nodes, &dv.bvh_nodes)) ||
@@ -117,13 +120,19 @@ int upload_prepared(const rt_host::PreparedHost &h, int ntris, int nindices, rt_
     // exact, but 26 vs 18 us per deep bounce on room2m)
     static const bool lone = getenv("RT_LONE") && atoi(getenv("RT_LONE")) != 0;
     if (h.bvh_depth >= 0 && !h.bvh8.empty() && (lone || dv.kd_resume_bulk) &&
-        ((rc = upload_vec(*s, h.bvh8, &dv.bvh8)) ||
-         (!h.kd_rows.empty() && ((rc = upload_vec(*s, h.kd_start, &dv.kd_start)) ||
-                                 (rc = upload_vec(*s, h.kd_rows, &dv.kd_rows)))))) {
+        ((rc = upload_vec(*s, h.bvh8, &dv.bvh8)) || (rc = upload_vec(*s, h.kd_start, &dv.kd_start)))) {
         release(s);
         return rc;
     }
     if (!lone) dv.bvh8 = nullptr;
+    // the root-path records (leaf and grid starts) and the grid (wf_long's deep bounces)
+    if (!h.kd_rows.empty() && ((rc = upload_vec(*s, h.kd_rows, &dv.kd_rows)) ||
+                               (h.kd_grid > 0 && (rc = upload_vec(*s, h.kd_cell, &dv.kd_cell))))) {
+        release(s);
+        return rc;
+    }
+    if (dv.kd_cell) dv.kd_grid = h.kd_grid;
+    if (h.kd_start.empty()) dv.kd_start = nullptr;
     dv.nodes = nodes;
     dv.isect_a = a;
     dv.isect_bary = bary;

@@ -673,6 +673,72 @@ __device__ __forceinline__ void wide_trace(const RtDevScene &sc, Vec3D o, Vec3D 
     wide_trace_from<COUNT>(sc, o, d, 1, W, counter_lane, tri, hbx, hby, hbz, c);
 }
 
+// The wide traversal of a fresh ray entered at the KD node of the grid cell
+// holding its origin (host/scene_prepare.cpp build_kd_starts): trace_ray goes
+// front to back from the origin, so it descends from the root toward the
+// origin's side of every split it crosses — the near child — until it
+// reaches that node, pushing the far child wherever the split lies inside
+// its interval.  The stored root path lets the wave replay those decisions
+// from records loaded at once (one per lane) instead of spending a frontier
+// round per level: each decision must be the path's child (near only: t >=
+// exit or t < 0; near with the far child pushed: entry < t < exit), anything
+// else (a far-only step, a NaN split distance, an origin off the cell) and
+// the frontier is the root as usual.  On success W.F holds the same ordered
+// frontier wide_resume builds from a sequential stack — pushed far children
+// under the start node — and its size is returned (0: not entered).
+// (Only for non-counting launches: the skipped levels' node fetches are not
+// charged to the reference's counters.)
+__device__ __forceinline__ int kd_origin_frontier(const RtDevScene &sc, Vec3D o, Vec3D d, float entry, float exit_,
+                                                  const WideLds &W)
+{
+    const int lane = __lane_id();
+    const int G = sc.kd_grid;
+    const float f[3] = {(o.x - sc.bmin[0]) * sc.kd_gscale[0], (o.y - sc.bmin[1]) * sc.kd_gscale[1],
+                        (o.z - sc.bmin[2]) * sc.kd_gscale[2]};
+    int cc[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) cc[a] = f[a] >= 0.0f ? (f[a] < (float)(G - 1) ? (int)f[a] : G - 1) : 0; // (NaN: 0)
+    const size_t k = ((size_t)cc[2] * (size_t)G + (size_t)cc[1]) * (size_t)G + (size_t)cc[0];
+    const uint2 st = *reinterpret_cast<const uint2 *>(sc.kd_cell + 2 * k);
+    if (st.x == 0xFFFFFFFFu) return 0;
+    const uint32_t depth = st.y & 31u;
+    uint4 mine = make_uint4(0u, 0u, 0u, 0u);
+    if ((uint32_t)lane < depth)
+        mine = *reinterpret_cast<const uint4 *>(sc.kd_rows + 4 * ((size_t)(st.y >> 5) + (size_t)lane));
+    const float yx = rt_recip_guard(d.x), yy = rt_recip_guard(d.y), yz = rt_recip_guard(d.z);
+    const float root_exit = exit_;
+    float ex = exit_, below = exit_;
+    int sp = 0;
+    for (uint32_t i = 0; i < depth; ++i) {
+        const uint32_t rx = (uint32_t)__builtin_amdgcn_readlane((int)mine.x, (int)i);
+        const uint32_t ry = (uint32_t)__builtin_amdgcn_readlane((int)mine.y, (int)i);
+        const uint32_t anc = (uint32_t)__builtin_amdgcn_readlane((int)mine.z, (int)i);
+        const uint32_t rw = (uint32_t)__builtin_amdgcn_readlane((int)mine.w, (int)i);
+        const uint32_t axis = ry & 3u;
+        const float split = as_float(rx);
+        const float oax = axis == 0 ? o.x : (axis == 1 ? o.y : o.z);
+        const float dax = axis == 0 ? d.x : (axis == 1 ? d.y : d.z);
+        const float yax = axis == 0 ? yx : (axis == 1 ? yy : yz);
+        uint32_t near_c = anc + 1, far_c = ry >> 2;
+        if (oax >= split) { // ray_behind_plane (rt/trace_ray.cuh:174-188)
+            near_c = ry >> 2;
+            far_c = anc + 1;
+        }
+        const uint32_t taken = rw ? ry >> 2 : anc + 1;
+        if (near_c != taken) return 0;
+        const float t = rt_div_by(split - oax, dax, yax); // intersect_plane (:190-210)
+        if (t >= ex || t < 0) continue; // near only
+        if (!(t > entry)) return 0;     // far only (or NaN): not the origin's way
+        if (lane == 0) W.F[sp] = WideItem{far_c, t, below, (uint32_t)sp << WIDE_SP_SHIFT};
+        ++sp;
+        below = t;
+        ex = t;
+    }
+    (void)root_exit;
+    if (lane == 0) W.F[sp] = WideItem{st.x, entry, ex, (uint32_t)sp << WIDE_SP_SHIFT};
+    return sp + 1;
+}
+
 // Finish lane `owner`'s ray, which is in the middle of its cooperative
 // traversal, with all 64 lanes: its sequential state is already an ordered
 // frontier — stack entries 0..sp-1 (bottom = last in traversal order, each

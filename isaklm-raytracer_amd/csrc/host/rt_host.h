@@ -79,7 +79,8 @@ struct PreparedHost {
     float kd_grid_scale[3] = {0, 0, 0};
 };
 // fills the shortcut tables from the prepared KD nodes and BVH (scene_prepare.cpp)
-void build_kd_starts(PreparedHost &out, const Bounding_Box &bounds);
+// (leaves: the per-BVH-leaf starts too; the grid always)
+void build_kd_starts(PreparedHost &out, const Bounding_Box &bounds, bool leaves);
 // fills bvh8 from bvh_nodes (scene_prepare.cpp)
 void build_bvh8(PreparedHost &out);
 int prepare_host(const Triangle *tris, int ntris, const KD_Tree_Node *nodes, int nnodes, const int *indices,

@@ -50,10 +50,10 @@ static inline RtF4 f4(float x, float y, float z, float w) { return RtF4{x, y, z,
 // check each against the path, falling back to the root on any difference,
 // so the shortcut never changes a result.  (The grid serves the large
 // triangles — walls — whose leaf boxes straddle the top splits.)
-void build_kd_starts(PreparedHost &out, const Bounding_Box &bounds)
+void build_kd_starts(PreparedHost &out, const Bounding_Box &bounds, bool leaves)
 {
-    const size_t nslots = out.bvh_a.size(), nb = out.bvh_nodes.size() / 4;
-    out.kd_start.assign(2 * nslots, 0xFFFFFFFFu);
+    const size_t nslots = out.bvh_a.size(), nb = leaves ? out.bvh_nodes.size() / 4 : 0;
+    out.kd_start.assign(leaves ? 2 * nslots : 0, 0xFFFFFFFFu);
     out.kd_rows.clear();
     out.kd_cell.clear();
     out.kd_grid = 0;
@@ -376,10 +376,11 @@ int prepare_host(const Triangle *tris, int ntris, const KD_Tree_Node *nodes, int
         // of the deep paths (RT_LONE=1, lone_trace.h) uses both, the bulk finisher the shortcut
         // (RT_KD_RESUME=1).  Both measured slower than the defaults
         auto on = [](const char *v) { return getenv(v) && atoi(getenv(v)) != 0; };
-        if (on("RT_LONE") || on("RT_KD_RESUME")) {
-            build_bvh8(out);
-            build_kd_starts(out, bounds);
-        }
+        const bool leaf_starts = on("RT_LONE") || on("RT_KD_RESUME");
+        if (leaf_starts) build_bvh8(out);
+        // the grid cells' start nodes always: wf_long enters each deep bounce's KD traversal at
+        // the cell of the ray's origin (wavefront.hip kd_origin_frontier); off with RT_KD_GRID=0
+        if (leaf_starts || !getenv("RT_KD_GRID") || on("RT_KD_GRID")) build_kd_starts(out, bounds, leaf_starts);
         out.bvh_always = bvh.always;
         out.bvh_dropped = bvh.dropped;
     } else if (brc != RT_OK && brc != RT_E_UNSUPPORTED) {

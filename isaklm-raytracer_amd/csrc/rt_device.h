@@ -101,6 +101,9 @@ struct RtDevScene {
     const uint32_t *kd_start;   // per BVH leaf slot (its first): {start node, row offset << 5 | depth}
     const uint32_t *kd_rows;    // 4 words per ancestor: split bits, y word, ancestor index, child taken
     int kd_resume_bulk;         // trace_bvh uses the shortcut too (RT_KD_RESUME=1; lone_trace always)
+    const uint32_t *kd_cell;    // per cell of a kd_grid^3 grid over the scene box: {start node, row offset << 5 | depth}
+    int kd_grid;                // cell of p: ((p - bmin) * kd_gscale), clamped to [0, kd_grid - 1]
+    float kd_gscale[3];
     const RtF4 *bvh8;           // 8-wide BVH (lone_trace.h): 16 per node, child k {lo, hi.x}, {hi.yz, ref, 0}; nullptr: none
 };
 

@@ -1302,7 +1302,11 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_LONG_WAVES) wf_long(RtDevScene sc
             if (__shfl((int)r.live, 0)) {
                 const Vec3D o = rt_v3(__shfl(r.o.x, 0), __shfl(r.o.y, 0), __shfl(r.o.z, 0));
                 const Vec3D d = rt_v3(__shfl(r.d.x, 0), __shfl(r.d.y, 0), __shfl(r.d.z, 0));
-                wide_trace<COUNT>(sc, o, d, __shfl(r.entry, 0), __shfl(r.exit_, 0), W, lane == 0, hit, bx, by, bz, c);
+                const float en = __shfl(r.entry, 0), ex = __shfl(r.exit_, 0);
+                // entered at the origin's grid cell (kd_origin_frontier), else from the root
+                const int nf = !COUNT && sc.kd_grid > 0 ? kd_origin_frontier(sc, o, d, en, ex, W) : 0;
+                if (nf > 0) wide_trace_from<COUNT>(sc, o, d, nf, W, lane == 0, hit, bx, by, bz, c);
+                else wide_trace<COUNT>(sc, o, d, en, ex, W, lane == 0, hit, bx, by, bz, c);
             }
             }
             want = 0;

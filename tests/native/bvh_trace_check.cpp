@@ -234,6 +234,7 @@ float bvh8_bound(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, float best)
 }
 
 long long g_bvh8_mism = 0;
+long long g_origin_mism = 0;
 
 // restatement of bvh_trace.h kd_resume: replay the bounded descent along the
 // stored root path of the leaf's start node, each decision checked
@@ -333,6 +334,34 @@ Hit bounded_trace(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, Work &w)
         ++w.resume_failed;
     }
     return kd_trace(h, o, d, t1, t2, s_min, w);
+}
+
+// the plain traversal entered at the KD node of the grid cell holding the
+// origin (wavefront.hip wf_long, coop_trace.h kd_origin_frontier): the
+// replay with s_min = -inf, then the rest from that state
+long long g_origin_resumed = 0;
+Hit origin_trace(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, Work &w)
+{
+    float t1, t2;
+    if (!scene_box(h, o, d, t1, t2)) return Hit{};
+    if (h.kd_grid > 0) {
+        const int G = h.kd_grid;
+        const float p[3] = {o.x, o.y, o.z};
+        const float bmin[3] = {h.bounds.min.x, h.bounds.min.y, h.bounds.min.z};
+        int c[3];
+        for (int a = 0; a < 3; ++a) {
+            const float f = (p[a] - bmin[a]) * h.kd_grid_scale[a];
+            c[a] = f >= 0.0f ? (f < (float)(G - 1) ? (int)f : G - 1) : 0;
+        }
+        const size_t k = ((size_t)c[2] * G + c[1]) * G + c[0];
+        Resume r;
+        if (kd_resume(h, h.kd_cell[2 * k], h.kd_cell[2 * k + 1], o, d, t1, t2, -INFINITY, r, w)) {
+#pragma omp atomic
+            ++g_origin_resumed;
+            return kd_trace(h, o, d, t1, t2, -INFINITY, w, &r);
+        }
+    }
+    return kd_trace(h, o, d, t1, t2, -INFINITY, w);
 }
 
 Hit plain_trace(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, Work &w)
@@ -459,6 +488,12 @@ int main(int argc, char **argv)
                 if (d.x != d.x) continue;
             }
             const Hit a = plain_trace(h, o, d, lp), b = bounded_trace(h, o, d, lb);
+            Work lo;
+            const Hit oc = origin_trace(h, o, d, lo);
+            if (oc.tri != a.tri || memcmp(oc.b, a.b, sizeof a.b) != 0) {
+#pragma omp atomic
+                ++g_origin_mism;
+            }
             if (a.tri >= 0) ++lh;
             if (a.tri != b.tri || memcmp(a.b, b.b, sizeof a.b) != 0) {
                 if (++lm <= 5) {
@@ -494,5 +529,6 @@ int main(int argc, char **argv)
     printf("kd resume: %lld resumed, %lld fell back to the root, %.1f path records per ray (%zu rows)\n", wb.resumed,
            wb.resume_failed, wb.rows / R, h.kd_rows.size() / 4);
     printf("8-wide BVH: %zu nodes, s_min mismatches vs the binary query %lld\n", h.bvh8.size() / 16, g_bvh8_mism);
-    return mism == 0 && g_bvh8_mism == 0 ? 0 : 1;
+    printf("origin-cell entry: %lld resumed, mismatches vs the plain traversal %lld\n", g_origin_resumed, g_origin_mism);
+    return mism == 0 && g_bvh8_mism == 0 && g_origin_mism == 0 ? 0 : 1;
 }
