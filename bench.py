@@ -232,10 +232,9 @@ def measure_pmc(args, save_dir):
     if args.adaptive:
         child.append("--adaptive")
     res = {"passes": {}}
-    # the counter children render without the deep-path CU partition (the same
-    # work and traffic on all CUs): a process holding CU-masked queues crashes in
-    # rocprofv3's exit under --pmc (SIGSEGV in __cxa_finalize, after the data is
-    # written; tools/gpu_r03_pmcdiag.sh), which would fail the pass
+    # the counter children never use the opt-in deep-path CU partition
+    # (RT_WF_LONG_CUS): a process holding CU-masked queues crashes in rocprofv3's
+    # exit (SIGSEGV in __cxa_finalize; tools/gpu_r03_pmcdiag.sh)
     env = dict(os.environ, TMPDIR="/tmp", RT_WF_LONG_CUS="0")
     for tag, ctrs in (("fetch", ["FETCH_SIZE"]), ("write", ["WRITE_SIZE"]), ("sq", SQ_COUNTERS)):
         d = tempfile.mkdtemp(prefix=f"rtpmc_{tag}_", dir="/tmp")

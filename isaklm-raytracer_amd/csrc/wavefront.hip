@@ -106,7 +106,7 @@ static_assert(WF_BLOCK % WF_TBLOCK == 0 && WF_TBLOCK % 64 == 0, "WF_TBLOCK must 
 #define WF_MAX_PIPES 6                // concurrent pipelines (RtOptions.wf_pipelines); more than 3 need GPU_MAX_HW_QUEUES > 4
 #define WF_PIPES_DEFAULT 3
 #define WF_LONG_DEPTH_DEFAULT 64      // RtOptions.wf_long_depth: paths deeper than this go to wf_long
-#define WF_LONG_CUS_DEFAULT 16        // whole-call mode: CUs of wf_long's own (long_cus)
+#define WF_LONG_CUS_DEFAULT 0         // whole-call mode: CUs of wf_long's own (long_cus; 0: shared)
 #define WF_LONG_BLOCKS 64             // wf_long grid (4 waves each, one path per wave at a time)
 #define WF_LONG_IDLE 2000000000ull   // s_memrealtime ticks (100 MHz): 20 s without a claim ends a wf_long wave
 
@@ -1427,10 +1427,13 @@ int ensure_streams(Workspace &w, int npipes)
     return 0;
 }
 
-// CUs of wf_long's own in the whole-call mode (RT_WF_LONG_CUS overrides; 0:
+// CUs of wf_long's own in the whole-call mode (RT_WF_LONG_CUS, default 0:
 // shared CUs).  Measured per 256-pass room2m call (median of 5 calls, two
 // rounds, tools/gpu_r03_cu.sh): 0 / 8 / 16 / 32 CUs 1.54-1.78 / 1.51-1.53 /
-// 1.49-1.51 / 1.59-2.00 s, the calls' spread smallest at 16
+// 1.49-1.51 / 1.59-2.00 s, but the driver-style 20-step bench equal within
+// its noise (325.5 vs 325.1 Msamples/s), and a process holding CU-masked
+// queues crashes in rocprofv3's exit (--pmc and --kernel-trace: SIGSEGV in
+// __cxa_finalize, the trace summary not written) — so not by default
 int long_cus()
 {
     static const int k = getenv("RT_WF_LONG_CUS") ? atoi(getenv("RT_WF_LONG_CUS")) : WF_LONG_CUS_DEFAULT;
