@@ -706,8 +706,7 @@ __device__ __forceinline__ int kd_origin_frontier(const RtDevScene &sc, Vec3D o,
     if ((uint32_t)lane < depth)
         mine = *reinterpret_cast<const uint4 *>(sc.kd_rows + 4 * ((size_t)(st.y >> 5) + (size_t)lane));
     const float yx = rt_recip_guard(d.x), yy = rt_recip_guard(d.y), yz = rt_recip_guard(d.z);
-    const float root_exit = exit_;
-    float ex = exit_, below = exit_;
+    float ex = exit_; // the current interval's exit: the root's, then the last push's t
     int sp = 0;
     for (uint32_t i = 0; i < depth; ++i) {
         const uint32_t rx = (uint32_t)__builtin_amdgcn_readlane((int)mine.x, (int)i);
@@ -729,12 +728,10 @@ __device__ __forceinline__ int kd_origin_frontier(const RtDevScene &sc, Vec3D o,
         const float t = rt_div_by(split - oax, dax, yax); // intersect_plane (:190-210)
         if (t >= ex || t < 0) continue; // near only
         if (!(t > entry)) return 0;     // far only (or NaN): not the origin's way
-        if (lane == 0) W.F[sp] = WideItem{far_c, t, below, (uint32_t)sp << WIDE_SP_SHIFT};
+        if (lane == 0) W.F[sp] = WideItem{far_c, t, ex, (uint32_t)sp << WIDE_SP_SHIFT}; // exit: the entry below
         ++sp;
-        below = t;
         ex = t;
     }
-    (void)root_exit;
     if (lane == 0) W.F[sp] = WideItem{st.x, entry, ex, (uint32_t)sp << WIDE_SP_SHIFT};
     return sp + 1;
 }
