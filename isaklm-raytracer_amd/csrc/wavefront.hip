@@ -62,7 +62,12 @@ static_assert(WF_BLOCK % WF_TBLOCK == 0 && WF_TBLOCK % 64 == 0, "WF_TBLOCK must 
 #define WF_LONG_WAVES 5
 #endif
 #ifndef WF_LONG_PRIO
-#define WF_LONG_PRIO 0 // wf_long wave priority (a lone deep path's chain is the call's critical path)
+// wf_long wave priority: a deep path's bounce chain is the call's critical
+// path, and in the whole-call mode its wave shares a CU with ~24 finisher
+// waves; s_setprio 3 wins it the issue arbitration.  Per 256-pass room2m call
+// (5 calls x 2 rounds, tools/gpu_ab_libs5.sh): 6.93 / 6.96 s vs 7.34 / 7.80 s
+// for 5 calls at priority 0 (-5.6 % / -11 %)
+#define WF_LONG_PRIO 3
 #endif
 #ifndef WF_FIN_LINGER
 #define WF_FIN_LINGER 100000000ull // s_memrealtime ticks (100 MHz): 1 s
