@@ -139,6 +139,12 @@ def parse_args(argv=None):
                          "(RtOptions.traversal; identical images)")
     ap.add_argument("--adaptive", action="store_true", help="adaptive sampling (configs[4]); value stays nominal "
                     "W*H*spp/s, value_actual = accumulated samples/s")
+    ap.add_argument("--overlap", type=int, choices=[0, 1], default=1,
+                    help="chained rt_render calls (RtOptions.overlap): a call's deep-path tail overlaps the next "
+                         "call; the timed region ends with the tonemap, which joins them (identical images)")
+    ap.add_argument("--check-interval", type=int, default=0,
+                    help="the bounded traversal's run-time guard: 1 ray in N re-traced by the KD traversal "
+                         "(RtOptions.check_interval; 0 = the library default 1024, < 0 off)")
     ap.add_argument("--min-samples", type=int, default=100)
     ap.add_argument("--max-depth", type=int, default=0, help="0 = unbounded (reference)")
     ap.add_argument("--scene-dir", default=os.environ.get("RT_SCENE_DIR", os.path.join(ROOT, "build", "scenes")))
@@ -232,10 +238,7 @@ def measure_pmc(args, save_dir):
     if args.adaptive:
         child.append("--adaptive")
     res = {"passes": {}}
-    # the counter children never use the opt-in deep-path CU partition
-    # (RT_WF_LONG_CUS): a process holding CU-masked queues crashes in rocprofv3's
-    # exit (SIGSEGV in __cxa_finalize; tools/gpu_r03_pmcdiag.sh)
-    env = dict(os.environ, TMPDIR="/tmp", RT_WF_LONG_CUS="0")
+    env = dict(os.environ, TMPDIR="/tmp")
     for tag, ctrs in (("fetch", ["FETCH_SIZE"]), ("write", ["WRITE_SIZE"]), ("sq", SQ_COUNTERS)):
         d = tempfile.mkdtemp(prefix=f"rtpmc_{tag}_", dir="/tmp")
         cmd = ["timeout", "-s", "KILL", "240", "rocprofv3", "--pmc", *ctrs, "--kernel-trace", "-d", d, "-o", "run",
@@ -503,7 +506,7 @@ def main(argv=None, binding=None):
     kernel = rt.KERNEL_WAVEFRONT if args.kernel == "wavefront" else rt.KERNEL_MEGA
     wavefront = kernel == rt.KERNEL_WAVEFRONT
     render_kw = dict(adaptive=args.adaptive, min_samples=args.min_samples, max_depth=args.max_depth, kernel=kernel,
-                     traversal=traversal_of(args, rt))
+                     traversal=traversal_of(args, rt), check_interval=args.check_interval)
     bounded = wavefront and args.traversal == "bounded"
     spc = max(1, args.steps_per_call)
     profiles = []
@@ -512,7 +515,7 @@ def main(argv=None, binding=None):
         """render steps [first, first + count) in calls of up to spc steps"""
         for start, k in call_plan(first, count, spc):
             rt.render(dscene, gb, host.camera, 0 if start == 0 else 1,
-                      rt.options(W, H, P * k, profile=wavefront, **render_kw))
+                      rt.options(W, H, P * k, profile=wavefront, overlap=bool(args.overlap), **render_kw))
             if wavefront:
                 profiles.append(dict(rt.last_profile(), passes=P * k))
 
@@ -552,14 +555,15 @@ def main(argv=None, binding=None):
     if dist:  # every rank's statistics (sums; max of the longest path)
         import torch
 
-        dv = torch.tensor([dev["watchdog_paths"], dev["cut_paths"], dev["deep_paths"]] + dev["deep_hist"],
-                          dtype=torch.int64)
+        dv = torch.tensor([dev["watchdog_paths"], dev["cut_paths"], dev["deep_paths"], dev["bounded_checked"],
+                           dev["bounded_mismatches"]] + dev["deep_hist"], dtype=torch.int64)
         dist.all_reduce(dv)
         mx = torch.tensor([dev["max_deep_depth"]], dtype=torch.int64)
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         v = [int(x) for x in dv.tolist()]
-        dev = {"watchdog_paths": v[0], "cut_paths": v[1], "deep_paths": v[2], "deep_hist": v[3:],
-               "max_deep_depth": int(mx.item())}
+        dev = {"watchdog_paths": v[0], "cut_paths": v[1], "deep_paths": v[2], "bounded_checked": v[3],
+               "bounded_mismatches": v[4], "deep_hist": v[5:], "max_deep_depth": int(mx.item()),
+               "mismatch_ray": dev.get("mismatch_ray")}
     total_samples = world * n * P * args.steps
     value = total_samples / elapsed / 1e6
     acc = gb.download()[2]
@@ -704,6 +708,10 @@ def main(argv=None, binding=None):
             "deep_path_hist": {f"{64 << k}-{(64 << (k + 1)) - 1}": h for k, h in enumerate(dev["deep_hist"]) if h},
             "watchdog_limit": 16777215,
             "deep_pushes": c["deep_push"], "deep_pushes_scope": "one extra counted call of the same options",
+            "bounded_checked": dev.get("bounded_checked"), "bounded_mismatches": dev.get("bounded_mismatches"),
+            "bounded_check_note": "run-time guard of the BVH-bounded traversal: a deterministic 1-in-"
+                                  f"{args.check_interval or 1024} sample of the finisher's rays, re-traced by the "
+                                  "plain KD traversal (trace_ray) inside the timed region and compared bit for bit",
             "note": "paths cut by the 2^24-1-bounce watchdog (SURVEY H8; the reference loops unbounded), paths cut "
                     "by max_depth, the longest path in bounces and the histogram of paths that ended at depth >= 64; "
                     "deep_pushes = traversal pushes at stack index >= 19 (past the reference's 19-entry arrays, "

@@ -26,14 +26,16 @@
  * code otherwise (rt_last_error() describes the last failure of the calling
  * thread).  Pointers named *_device are HIP device pointers.  The caller owns
  * every allocation and frees it explicitly (the reference leaks; see
- * rt/screen.cuh:24-31).  Calls are synchronous unless an RtOptions.stream is
- * given, in which case the megakernel (RT_KERNEL_MEGA) only enqueues.  The
- * wavefront kernels (the default) BLOCK the calling thread until the call's
- * queue iterations are done: their host threads read each iteration's live
- * path count to decide the next launch.  Only the last long-path slice and
- * the pipelines' join are left enqueued on the given stream when they return.
- * Consecutive calls may use different streams: a call waits for the previous
- * call's device work first (they share the per-device workspace).
+ * rt/screen.cuh:24-31); rt_shutdown releases the library's own per-device
+ * workspaces (it is also registered to run at exit).  Calls are synchronous
+ * unless an RtOptions.stream is given, in which case the default render (the
+ * bounded traversal, one persistent finisher per call) and the megakernel
+ * only enqueue; the queue variants (RT_TRAVERSAL_KD, counting calls) block the
+ * calling thread until their queue iterations are done (their host threads
+ * read each iteration's live path count).  Consecutive calls may use
+ * different streams: a call waits for the previous calls' device work first
+ * (they share the per-device workspace) — except a chained call
+ * (RtOptions.overlap), see there.
  */
 #ifndef ISAKLM_RT_H
 #define ISAKLM_RT_H
@@ -51,10 +53,12 @@ extern "C" {
 /* ABI version: 3 = rt_scene_prepare(const Scene *, rt_scene_t *) without
  * counts (the counted form is rt_scene_prepare_counts), RtDeviations and
  * rt_deviation_stats, rt_abi_version; 4 = RT_CNT_COUNT 40 (the optional
- * counters buffer grew); 5 = RtOptions.traversal.  An integrator checks
- * rt_abi_version() == RT_ABI_VERSION at start-up: a binary built against an
- * older header would otherwise link (C linkage) and mis-pass arguments. */
-#define RT_ABI_VERSION 5
+ * counters buffer grew); 5 = RtOptions.traversal; 6 = RtOptions.overlap /
+ * check_interval / debug, RtDeviations' bounded-traversal guard fields,
+ * rt_join, rt_shutdown.  An integrator checks rt_abi_version() ==
+ * RT_ABI_VERSION at start-up: a binary built against an older header would
+ * otherwise link (C linkage) and mis-pass arguments. */
+#define RT_ABI_VERSION 6
 
 /* CUDA uchar4, used for texels (rt/scene.cuh:18) */
 typedef struct RtUChar4 { uint8_t x, y, z, w; } RtUChar4;
@@ -230,6 +234,14 @@ int rt_device_count(int *count);
  * e.g. RCCL, take the hardware queues) */
 int rt_set_device(int device);
 int rt_synchronize(void);
+/* `stream` (NULL: the calling thread) waits for every rt_render's device work
+ * on the current device, including the deep-path tails that chained calls
+ * (RtOptions.overlap) leave running past their stream point */
+int rt_join(void *stream);
+/* releases the library's per-device workspaces (streams, events, device
+ * buffers) after their device work is done; registered with atexit by
+ * rt_set_device / the first render.  Renders after it create them again. */
+void rt_shutdown(void);
 void rt_host_free(void *ptr_host);  /* frees host arrays returned by this library */
 
 /* ---------------- G_Buffer (rt/screen.cuh:22-46) ---------------- */
@@ -437,11 +449,36 @@ typedef struct RtOptions {
      * _TRI, _HIT, RT_CNT_B_*; measurement: the finisher and the long-path
      * kernel are not counted; the megakernel then runs its counting KD build). */
     int traversal;
+    /* chained calls (default render only: bounded traversal, not counting).
+     * 0: the call is complete at its stream point.  1: the call's deep paths
+     * (glass loops of 10^4+ bounces, handed to the long-path kernel) may still
+     * run after its stream point, and the NEXT call of the same frame — same
+     * scene, G_Buffer, camera and frame options, sample_count != 0, overlap 1
+     * — starts at once: its pixels that are not still out run their passes,
+     * the ones still out are owed the passes and run them when they come
+     * back.  Every pixel's passes run in the reference's order, so the frame
+     * is bit-identical to unchained calls.  Whatever reads the frame in
+     * between must join first: rt_join(stream), rt_synchronize, or the
+     * library's own readers (rt_tonemap, rt_save_render, rt_gbuffer_save,
+     * rt_reduce_shards, rt_deviation_stats), which join by themselves.  The
+     * reference's render() (rt/render.cuh:62-76) has no such tail: a call is
+     * complete when its launches are (rt/main.cu:114-155). */
+    int overlap;
+    /* run-time exactness guard of the bounded traversal (default render):
+     * 1 ray in check_interval (rounded up to a power of two; 0 = 1024) of
+     * those the finisher traces is recorded with its result and traced again
+     * by the plain KD traversal after the call; disagreements are counted in
+     * RtDeviations.bounded_mismatches.  < 0: off. */
+    int check_interval;
+    int debug;           /* RT_DEBUG_* bits: stderr diagnostics of the wavefront calls */
 } RtOptions;
 
 #define RT_TRAVERSAL_BOUNDED 0
 #define RT_TRAVERSAL_KD 1
 #define RT_TRAVERSAL_BOUNDED_COUNTED 2
+#define RT_DEBUG_CALL_LOG 1  /* per call / queue iteration: counters and host times */
+#define RT_DEBUG_LONG_LOG 2  /* every deep sample's claim / end time and bounces (unchained calls) */
+#define RT_DEBUG_CHECK_FAULT 4 /* tests of the guard: every checked hit is recorded with a wrong triangle */
 
 /* Per-call kernel timing of the last rt_render on this device with
  * RtOptions.profile = 1 (wavefront kernels; HIP events on the call's stream,
@@ -476,6 +513,12 @@ typedef struct RtDeviations {
     unsigned long long max_deep_depth; /* longest path that reached depth 64 */
     unsigned long long deep_paths;     /* paths that reached depth 64 (sum of deep_hist) */
     unsigned long long deep_hist[RT_DEV_HIST_BINS];
+    /* the bounded traversal's run-time guard (RtOptions.check_interval): rays
+     * re-traced by the plain KD traversal, results that differed (a deviation
+     * from the reference; 0 expected), and the first such ray (o, d) */
+    unsigned long long bounded_checked;
+    unsigned long long bounded_mismatches;
+    float mismatch_ray[6];
 } RtDeviations;
 int rt_deviation_stats(RtDeviations *out, int reset);
 

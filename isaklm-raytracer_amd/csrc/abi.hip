@@ -12,6 +12,7 @@
 
 #include <map>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -22,9 +23,12 @@ int rt_launch_path(const RtDevScene &sc, const RtDevFrame &fr, const RtDevCamera
 int rt_launch_tonemap(const Vec3D *fb, const int *count, RtUChar4 *out, int n, hipStream_t stream);
 int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevCamera &cam, hipStream_t stream,
                         int variant, int tail, int finish_waves, int profile, int cap, int postpone, int wide,
-                        int pipes, int long_depth, int traversal);
+                        int pipes, int long_depth, int traversal, int overlap, int check_interval, int debug);
 
 int rt_wavefront_device_init();
+int rt_wavefront_join(void *stream);
+void rt_wavefront_shutdown();
+void rt_path_shutdown();
 
 static thread_local std::string g_error;
 
@@ -101,12 +105,10 @@ int upload_prepared(const rt_host::PreparedHost &h, int ntris, int nindices, rt_
     dv.bvh_bary = nullptr;
     dv.bvh_scale = h.bvh_scale;
     dv.split_vals = nullptr;
-    dv.kd_start = dv.kd_rows = nullptr;
-    dv.bvh8 = nullptr;
+    dv.kd_rows = nullptr;
     dv.kd_cell = nullptr;
     dv.kd_grid = 0;
     for (int a = 0; a < 3; ++a) dv.kd_gscale[a] = h.kd_grid_scale[a];
-    dv.kd_resume_bulk = getenv("RT_KD_RESUME") && atoi(getenv("RT_KD_RESUME")) != 0 ? 1 : 0;
     for (int a = 0; a < 4; ++a) dv.split_off[a] = h.split_off[a];
     if (h.bvh_depth >= 0 && ((rc = upload_vec(*s, h.bvh_nodes, &dv.bvh_nodes)) ||
                              (rc = upload_vec(*s, h.bvh_a, &dv.bvh_a)) ||
@@ -115,24 +117,13 @@ int upload_prepared(const rt_host::PreparedHost &h, int ntris, int nindices, rt_
         release(s);
         return rc;
     }
-    // the lone-ray traversal's tables (lone_trace.h): the 8-wide BVH and the KD descent shortcut
-    // (RT_LONE=1: wf_long's deep paths take it instead of the wide KD traversal; experiments —
-    // exact, but 26 vs 18 us per deep bounce on room2m)
-    static const bool lone = getenv("RT_LONE") && atoi(getenv("RT_LONE")) != 0;
-    if (h.bvh_depth >= 0 && !h.bvh8.empty() && (lone || dv.kd_resume_bulk) &&
-        ((rc = upload_vec(*s, h.bvh8, &dv.bvh8)) || (rc = upload_vec(*s, h.kd_start, &dv.kd_start)))) {
-        release(s);
-        return rc;
-    }
-    if (!lone) dv.bvh8 = nullptr;
-    // the root-path records (leaf and grid starts) and the grid (wf_long's deep bounces)
+    // the root-path records and the grid (wf_long's deep bounces enter at the origin's cell)
     if (!h.kd_rows.empty() && ((rc = upload_vec(*s, h.kd_rows, &dv.kd_rows)) ||
                                (h.kd_grid > 0 && (rc = upload_vec(*s, h.kd_cell, &dv.kd_cell))))) {
         release(s);
         return rc;
     }
     if (dv.kd_cell) dv.kd_grid = h.kd_grid;
-    if (h.kd_start.empty()) dv.kd_start = nullptr;
     dv.nodes = nodes;
     dv.isect_a = a;
     dv.isect_bary = bary;
@@ -175,11 +166,41 @@ unsigned long long *dev_stats_block()
 
 } // namespace
 
+// rt_shutdown at exit, registered once by rt_set_device / the first render:
+// atexit handlers run in reverse registration order, so this one (registered
+// after the HIP runtime initialised) runs before the runtime's own finalisers
+// and the library's streams, events and blobs are gone before they run
+void rt_register_shutdown()
+{
+    static std::once_flag once;
+    std::call_once(once, [] { atexit(rt_shutdown); });
+}
+
 extern "C" {
 
 const char *rt_last_error(void) { return g_error.c_str(); }
 const char *rt_version(void) { return "isaklm-raytracer_amd 0.3 (gfx950)"; }
 int rt_abi_version(void) { return RT_ABI_VERSION; }
+
+void rt_shutdown(void)
+{
+    rt_wavefront_shutdown();
+    rt_path_shutdown();
+    std::lock_guard<std::mutex> g(g_dev_mu);
+    for (auto &kv : g_dev_stats) {
+        if (hipSetDevice(kv.first) == hipSuccess) (void)hipFree(kv.second);
+    }
+    g_dev_stats.clear();
+}
+
+int rt_join(void *stream)
+{
+    if (rt_wavefront_join(stream) != 0) {
+        rt_set_error("rt_join: %s", hipGetErrorString(hipGetLastError()));
+        return RT_E_HIP;
+    }
+    return RT_OK;
+}
 
 int rt_deviation_stats(RtDeviations *out, int reset)
 {
@@ -196,6 +217,13 @@ int rt_deviation_stats(RtDeviations *out, int reset)
     for (int k = 0; k < RT_DEV_HIST_BINS; ++k) {
         out->deep_hist[k] = w[RT_DEV_HIST + k];
         out->deep_paths += w[RT_DEV_HIST + k];
+    }
+    out->bounded_checked = w[RT_DEV_CHECKED];
+    out->bounded_mismatches = w[RT_DEV_MISMATCH];
+    for (int k = 0; k < 3; ++k) {
+        const uint32_t hi = (uint32_t)(w[RT_DEV_MISRAY + 1 + k] >> 32), lo = (uint32_t)w[RT_DEV_MISRAY + 1 + k];
+        memcpy(&out->mismatch_ray[2 * k], &hi, 4);
+        memcpy(&out->mismatch_ray[2 * k + 1], &lo, 4);
     }
     if (reset) HIPCHK(hipMemset(d, 0, RT_DEV_WORDS * 8));
     return RT_OK;
@@ -224,6 +252,11 @@ int rt_download(void *dst, const void *src, size_t bytes)
 {
     if (bytes == 0) return RT_OK;
     if (!dst || !src) { rt_set_error("rt_download: null pointer"); return RT_E_INVALID; }
+    // (cudaMemcpy after a render waits for it; so does this, chained renders' tails included)
+    if (rt_wavefront_join(nullptr) != 0) {
+        rt_set_error("rt_download: join: %s", hipGetErrorString(hipGetLastError()));
+        return RT_E_HIP;
+    }
     HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
     return RT_OK;
 }
@@ -242,6 +275,7 @@ int rt_device_count(int *count)
 int rt_set_device(int device)
 {
     HIPCHK(hipSetDevice(device));
+    rt_register_shutdown();
     if (rt_wavefront_device_init() != 0) { // the pipelines' streams take their hardware queues first
         rt_set_error("rt_set_device: wavefront streams: %s", hipGetErrorString(hipGetLastError()));
         return RT_E_HIP;
@@ -735,11 +769,12 @@ int rt_render(rt_scene_t scene, G_Buffer g, Camera cam, int sample_count, const 
         if (scene->max_depth > RT_STACK_DEPTH ||
             rt_launch_wavefront(scene->dev, fr, dc, stream, o.kernel, o.wf_tail, o.wf_finish_waves, o.profile,
                                 o.wf_descent_cap, o.wf_postpone, o.wf_wide, o.wf_pipelines, o.wf_long_depth,
-                                o.traversal) != 0) {
+                                o.traversal, o.overlap, o.check_interval, o.debug) != 0) {
             rt_set_error("rt_render: wavefront launch failed: %s", hipGetErrorString(hipGetLastError()));
             return RT_E_HIP;
         }
-    } else if (rt_launch_path(scene->dev, fr, dc, scene->max_depth, stream, o.traversal) != 0) {
+    } else if (rt_wavefront_join(stream) != 0 || // (chained wavefront calls' tails first: same frame state)
+               rt_launch_path(scene->dev, fr, dc, scene->max_depth, stream, o.traversal) != 0) {
         rt_set_error("rt_render: kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
         return RT_E_HIP;
     }
@@ -753,7 +788,8 @@ int rt_tonemap(G_Buffer g, uint8_t *rgba, int w, int h, void *stream)
         rt_set_error("rt_tonemap: bad arguments");
         return RT_E_INVALID;
     }
-    if (rt_launch_tonemap(g.frame_buffer, g.sample_count, (RtUChar4 *)rgba, w * h, (hipStream_t)stream) != 0) {
+    if (rt_wavefront_join(stream) != 0 || // chained renders' deep-path tails first
+        rt_launch_tonemap(g.frame_buffer, g.sample_count, (RtUChar4 *)rgba, w * h, (hipStream_t)stream) != 0) {
         rt_set_error("rt_tonemap: launch failed");
         return RT_E_HIP;
     }

@@ -27,9 +27,8 @@
 namespace rtk {
 
 // Scene data is read-only for a kernel's lifetime: loaded through the
-// constant address space, so that a wave-uniform address (a traversal every
-// lane of the wave runs on the same ray: wf_long) becomes a scalar load
-// through the scalar cache; a divergent one stays a vector load.
+// constant address space (a wave-uniform address becomes a scalar load
+// through the scalar cache; a divergent one stays a vector load).
 // (the host pass of the single-source compile sees plain loads: these are
 // __device__ functions and never run there)
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -53,55 +52,6 @@ __device__ __forceinline__ uint4 ldc_u4(const uint32_t *p)
     const RT_CONST uint4 *q = (const RT_CONST uint4 *)p;
     return *q;
 }
-
-// A traversal stack shared by the 64 lanes of a wave that all trace the same
-// ray (entries [0, LDS_DEPTH) in the wave's LDS slice, deeper ones in its
-// spill column): popped values are made wave-uniform (readfirstlane), so the
-// loads they address stay scalar.  Same interface as Stack.
-template <int LDS_DEPTH>
-struct WaveStack {
-    uint32_t *lds_node;
-    float *lds_entry;
-    uint2 *spill;
-    int spill_stride;
-    __device__ __forceinline__ void put(int k, uint32_t node, float t)
-    {
-        if (k < LDS_DEPTH) {
-            lds_node[k] = node;
-            lds_entry[k] = t;
-        } else {
-            spill[(size_t)(k - LDS_DEPTH) * spill_stride] = make_uint2(node, __float_as_uint(t));
-        }
-    }
-    __device__ __forceinline__ void get(int k, uint32_t &node, float &entry) const
-    {
-        if (k < LDS_DEPTH) {
-            node = lds_node[k];
-            entry = lds_entry[k];
-        } else {
-            unsigned long long *p = reinterpret_cast<unsigned long long *>(spill + (size_t)(k - LDS_DEPTH) * spill_stride);
-            const unsigned long long v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-            node = (uint32_t)v;
-            entry = __uint_as_float((uint32_t)(v >> 32));
-        }
-        node = (uint32_t)__builtin_amdgcn_readfirstlane((int)node);
-        entry = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(entry)));
-    }
-    __device__ __forceinline__ uint32_t node_at(int k) const
-    {
-        uint32_t n;
-        float e;
-        get(k, n, e);
-        return n;
-    }
-    __device__ __forceinline__ float entry_at(int k) const
-    {
-        uint32_t n;
-        float e;
-        get(k, n, e);
-        return e;
-    }
-};
 
 // The tests of leaf entries [e0, e1) in order (trace_leaf_node,
 // rt/trace_ray.cuh:115-172: intersect_triangle + calculate_barycentric_
@@ -145,13 +95,10 @@ __device__ __forceinline__ int leaf_scan(const RtF4 *plane, const RtIsectBary *b
     return best;
 }
 
-// s_min of step 2: the smallest s < best of any passing test (best if none);
-// best_first: the first slot of the BVH leaf that holds it (RT_BVH_EMPTY: none)
+// s_min of step 2: the smallest s < best of any passing test (best if none)
 template <bool COUNT, typename STACK>
-__device__ __forceinline__ float bvh_bound(const RtDevScene &sc, Vec3D o, Vec3D d, float best, STACK &stk, Cnt &cn,
-                                           uint32_t &best_first)
+__device__ __forceinline__ float bvh_bound(const RtDevScene &sc, Vec3D o, Vec3D d, float best, STACK &stk, Cnt &cn)
 {
-    best_first = RT_BVH_EMPTY;
     const float m = rt_ray_margin(o.x, o.y, o.z, sc.bvh_scale);
     const Vec3D om = rt_v3(o.x + m, o.y + m, o.z + m), op = rt_v3(o.x - m, o.y - m, o.z - m);
     const Vec3D inv = rt_v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
@@ -196,72 +143,10 @@ __device__ __forceinline__ float bvh_bound(const RtDevScene &sc, Vec3D o, Vec3D 
         const uint32_t first = (cur & ~RT_BVH_LEAF) >> 3, end = first + (cur & 7u) + 1u;
         if (COUNT) cn.v[RT_CNT_B_BVH_TRI] += end - first;
         float bx, by, bz;
-        if (leaf_scan<COUNT>(sc.bvh_a, sc.bvh_bary, first, end, o, d, best, bx, by, bz, cn) >= 0) best_first = first;
+        (void)leaf_scan<COUNT>(sc.bvh_a, sc.bvh_bary, first, end, o, d, best, bx, by, bz, cn);
         cur = pop();
         if (cur == RT_BVH_EMPTY) return best;
     }
-}
-
-// The KD descent shortcut (host/scene_prepare.cpp build_kd_starts): replays
-// the bounded descent's decisions along the stored root path of the KD node
-// whose cell holds the s_min leaf's box — the same split distances, near /
-// far choice, skip rule and pushes as the descent below, from records loaded
-// independently of each other instead of node after node — checking each
-// decision against the child the path takes.  All agree: the descent's
-// state on reaching that node (node, entry, exit, stack) is returned and it
-// goes on from there.  Any difference (the hit point rounds outside the
-// box): false, and the descent starts at the root (sp = 0).
-template <bool COUNT, typename STACK>
-__device__ __forceinline__ bool kd_resume(const RtDevScene &sc, uint32_t best_first, Vec3D o, Vec3D d, float yx,
-                                          float yy, float yz, float s_min, uint32_t &node, float &entry, float &exit_,
-                                          int &sp, STACK &stk, Cnt &c)
-{
-    const uint2 st = ldc_u2(sc.kd_start + 2 * (size_t)best_first);
-    if (st.x == 0xFFFFFFFFu) return false; // (no record for this leaf)
-    const uint32_t depth = st.y & 31u;
-    const uint32_t *row = sc.kd_rows + 4 * (size_t)(st.y >> 5);
-    float en = entry, ex = exit_;
-    int k = 0;
-    for (uint32_t j = 0; j < depth; j += 4) {
-        uint4 r[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) r[i] = ldc_u4(row + 4 * (j + (j + i < depth ? i : 0)));
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            if (j + i >= depth) break;
-            if (COUNT) c.v[RT_CNT_NODE]++;
-            const uint32_t axis = r[i].y & 3u, anc = r[i].z;
-            const float split = as_float(r[i].x);
-            const float oax = axis == 0 ? o.x : (axis == 1 ? o.y : o.z);
-            const float dax = axis == 0 ? d.x : (axis == 1 ? d.y : d.z);
-            const float yax = axis == 0 ? yx : (axis == 1 ? yy : yz);
-            uint32_t near_c = anc + 1, far_c = r[i].y >> 2;
-            if (oax >= split) {
-                near_c = r[i].y >> 2;
-                far_c = anc + 1;
-            }
-            const float t = rt_div_by(split - oax, dax, yax);
-            const uint32_t taken = r[i].w ? r[i].y >> 2 : anc + 1; // the path's child
-            if (t >= ex || t < 0) {
-                if (near_c != taken) return false;
-            } else if (t <= en) {
-                if (far_c != taken) return false;
-            } else if (t <= s_min) {
-                if (far_c != taken) return false;
-                en = t;
-            } else {
-                if (near_c != taken) return false;
-                stk.put(k, far_c, t);
-                ++k;
-                ex = t;
-            }
-        }
-    }
-    node = st.x;
-    entry = en;
-    exit_ = ex;
-    sp = k;
-    return true;
 }
 
 // trace_ray with the bound: returns the triangle index or -1 and the hit's
@@ -278,19 +163,13 @@ __device__ __forceinline__ int trace_bvh(const RtDevScene &sc, const Vec3D o, co
     if (!bbox_hit(sc, o, d, entry, exit_)) return -1;
     const float root_exit = exit_;
     float s_min = -INFINITY; // (the plain KD traversal)
-    uint32_t best_first = RT_BVH_EMPTY;
     if (rt_bounded_ray(o, d, sc.split_vals, sc.split_off)) {
-        s_min = bvh_bound<COUNT>(sc, o, d, exit_, stk, c, best_first);
+        s_min = bvh_bound<COUNT>(sc, o, d, exit_, stk, c);
         if (!(s_min < root_exit)) return -1;
     }
     const float yx = rt_recip_guard(d.x), yy = rt_recip_guard(d.y), yz = rt_recip_guard(d.z);
     int sp = 0;
     uint32_t node = 0;
-    if (sc.kd_resume_bulk && sc.kd_rows && best_first != RT_BVH_EMPTY &&
-        !kd_resume<COUNT>(sc, best_first, o, d, yx, yy, yz, s_min, node, entry, exit_, sp, stk, c)) {
-        node = 0; // (a difference: the descent from the root; entry / exit untouched)
-        sp = 0;
-    }
     while (true) {
         uint2 nd = ldc_u2(sc.nodes + 2 * (size_t)node);
         if (COUNT) c.v[RT_CNT_NODE]++;

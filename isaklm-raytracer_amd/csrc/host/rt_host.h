@@ -65,24 +65,18 @@ struct PreparedHost {
     std::vector<float> split_vals;        // per axis sorted, unique (rt_bounded_ray)
     int split_off[4] = {0, 0, 0, 0};
     int bvh_depth = -1, bvh_always = 0, bvh_dropped = 0;
-    // KD descent shortcut (bvh_trace.h kd_resume): per BVH leaf, indexed by
-    // its first slot, {KD start node, row offset << 5 | depth} (0xFFFFFFFF:
-    // none), and per start node the root-to-start path, one record per
-    // ancestor {split bits, y word, ancestor index, 0 = child0 / 1 = child1}
-    // ... and per cell of a kd_grid^3 grid over the scene box (kd_cell, the
-    // same pairs; cell of a point: (p - bounds.min) * kd_grid_scale)
-    std::vector<RtF4> bvh8;               // 8-wide collapse of the BVH (lone_trace.h), 16 per node
-    std::vector<uint32_t> kd_start;
+    // wf_long's origin-cell entry (coop_trace.h kd_origin_frontier): per cell
+    // of a kd_grid^3 grid over the scene box, {KD start node, row offset << 5
+    // | depth} (0xFFFFFFFF: none; cell of a point: (p - bounds.min) *
+    // kd_grid_scale), and per start node the root-to-start path, one record
+    // per ancestor {split bits, y word, ancestor index, 0 = child0 / 1 = child1}
     std::vector<uint32_t> kd_rows;
     std::vector<uint32_t> kd_cell;
     int kd_grid = 0;
     float kd_grid_scale[3] = {0, 0, 0};
 };
-// fills the shortcut tables from the prepared KD nodes and BVH (scene_prepare.cpp)
-// (leaves: the per-BVH-leaf starts too; the grid always)
-void build_kd_starts(PreparedHost &out, const Bounding_Box &bounds, bool leaves);
-// fills bvh8 from bvh_nodes (scene_prepare.cpp)
-void build_bvh8(PreparedHost &out);
+// fills the origin-cell tables from the prepared KD nodes (scene_prepare.cpp)
+void build_kd_starts(PreparedHost &out, const Bounding_Box &bounds);
 int prepare_host(const Triangle *tris, int ntris, const KD_Tree_Node *nodes, int nnodes, const int *indices,
                  int nindices, const int *lights, int nlights, Bounding_Box bounds, PreparedHost &out);
 

@@ -38,22 +38,17 @@ static inline float bitsf(uint32_t u)
 }
 static inline RtF4 f4(float x, float y, float z, float w) { return RtF4{x, y, z, w}; }
 
-// The KD descent shortcut (bvh_trace.h kd_resume).  The bounded descent
-// goes, at every split, to the side holding the point o + d * s_min (exact
-// arithmetic: t > s_min -> near, the origin's side; t <= s_min -> far), and
-// that point lies in the box of the BVH leaf whose test set s_min — and in
-// its cell of a uniform grid over the scene box.  For each BVH leaf and each
-// grid cell, the deepest KD node whose cell holds the box is where the
-// descent passes with that s_min; its root path, stored as one record per
-// ancestor, lets the traversal replay the descent's decisions from
-// registers (independent loads) instead of fetching node after node — and
+// The origin-cell entry of wf_long's deep bounces (coop_trace.h
+// kd_origin_frontier): trace_ray descends, at every split, to the side
+// holding the ray's origin until the split separates the origin from the
+// ray's interval.  For each cell of a uniform grid over the scene box, the
+// deepest KD node whose cell holds the grid cell is where that descent passes
+// for an origin in it; its root path, stored as one record per ancestor, lets
+// the wide traversal replay those decisions from independent loads — and
 // check each against the path, falling back to the root on any difference,
-// so the shortcut never changes a result.  (The grid serves the large
-// triangles — walls — whose leaf boxes straddle the top splits.)
-void build_kd_starts(PreparedHost &out, const Bounding_Box &bounds, bool leaves)
+// so the entry never changes a result.
+void build_kd_starts(PreparedHost &out, const Bounding_Box &bounds)
 {
-    const size_t nslots = out.bvh_a.size(), nb = leaves ? out.bvh_nodes.size() / 4 : 0;
-    out.kd_start.assign(leaves ? 2 * nslots : 0, 0xFFFFFFFFu);
     out.kd_rows.clear();
     out.kd_cell.clear();
     out.kd_grid = 0;
@@ -97,20 +92,6 @@ void build_kd_starts(PreparedHost &out, const Bounding_Box &bounds, bool leaves)
         packed = off << 5 | (uint32_t)path.size();
         return true;
     };
-    for (size_t i = 0; i < nb; ++i) {
-        const RtF4 *nd = &out.bvh_nodes[4 * i];
-        uint32_t ref[2];
-        memcpy(&ref[0], &nd[3].x, 4);
-        memcpy(&ref[1], &nd[3].y, 4);
-        const float lo[2][3] = {{nd[0].x, nd[0].y, nd[0].z}, {nd[1].z, nd[1].w, nd[2].x}};
-        const float hi[2][3] = {{nd[0].w, nd[1].x, nd[1].y}, {nd[2].y, nd[2].z, nd[2].w}};
-        for (int c = 0; c < 2; ++c) {
-            if (ref[c] == RT_BVH_EMPTY || !(ref[c] & RT_BVH_LEAF)) continue;
-            const uint32_t first = (ref[c] & ~RT_BVH_LEAF) >> 3;
-            if (first >= nslots) continue;
-            (void)start_for(lo[c], hi[c], out.kd_start[2 * (size_t)first], out.kd_start[2 * (size_t)first + 1]);
-        }
-    }
     // the grid: G^3 cells over the scene box (G ~ the tree's node count^(1/3), 4..128)
     const float ext[3] = {bounds.max.x - bounds.min.x, bounds.max.y - bounds.min.y, bounds.max.z - bounds.min.z};
     if (!(ext[0] > 0 && ext[1] > 0 && ext[2] > 0 && std::isfinite(ext[0] + ext[1] + ext[2]))) return;
@@ -132,88 +113,6 @@ void build_kd_starts(PreparedHost &out, const Bounding_Box &bounds, bool leaves)
             }
     out.kd_grid = G;
     for (int a = 0; a < 3; ++a) out.kd_grid_scale[a] = (float)G / ext[a];
-}
-
-// The 8-wide collapse of the binary BVH for lone_trace.h: starting from a
-// node's two children, the inner child with the largest box surface is
-// replaced by its two children until there are 8 (or only leaves).  Child
-// boxes and leaf references are the binary tree's own (the same conservative
-// boxes, the same leaves); an inner child refers to its 8-wide node.  Layout:
-// 16 RtF4 per node, child k = {lo.x, lo.y, lo.z, hi.x}, {hi.y, hi.z,
-// ref bits, 0}; ref RT_BVH_EMPTY for unused slots.
-void build_bvh8(PreparedHost &out)
-{
-    const size_t nb = out.bvh_nodes.size() / 4;
-    out.bvh8.clear();
-    if (nb == 0) return;
-    struct Child {
-        uint32_t ref;
-        float lo[3], hi[3];
-    };
-    auto child_of = [&](uint32_t node, int c) {
-        const RtF4 *nd = &out.bvh_nodes[4 * (size_t)node];
-        Child ch;
-        memcpy(&ch.ref, c == 0 ? &nd[3].x : &nd[3].y, 4);
-        if (c == 0) {
-            ch.lo[0] = nd[0].x; ch.lo[1] = nd[0].y; ch.lo[2] = nd[0].z;
-            ch.hi[0] = nd[0].w; ch.hi[1] = nd[1].x; ch.hi[2] = nd[1].y;
-        } else {
-            ch.lo[0] = nd[1].z; ch.lo[1] = nd[1].w; ch.lo[2] = nd[2].x;
-            ch.hi[0] = nd[2].y; ch.hi[1] = nd[2].z; ch.hi[2] = nd[2].w;
-        }
-        return ch;
-    };
-    std::vector<int> idx(nb, -1);
-    std::vector<std::vector<Child>> wide; // per 8-wide node, its children (binary refs)
-    std::vector<uint32_t> order{0};
-    idx[0] = 0;
-    for (size_t q = 0; q < order.size(); ++q) {
-        const uint32_t b = order[q];
-        std::vector<Child> ch;
-        for (int c = 0; c < 2; ++c) {
-            const Child x = child_of(b, c);
-            if (x.ref != RT_BVH_EMPTY) ch.push_back(x);
-        }
-        while (ch.size() < 8) {
-            int pick = -1;
-            float area = -1.0f;
-            for (size_t k = 0; k < ch.size(); ++k) {
-                if (ch[k].ref & RT_BVH_LEAF) continue;
-                const float ex = ch[k].hi[0] - ch[k].lo[0], ey = ch[k].hi[1] - ch[k].lo[1], ez = ch[k].hi[2] - ch[k].lo[2];
-                const float a = ex * ey + ey * ez + ez * ex;
-                if (!(a <= area)) { // (NaN or larger: take it)
-                    area = a;
-                    pick = (int)k;
-                }
-            }
-            if (pick < 0) break;
-            const uint32_t inner = ch[(size_t)pick].ref;
-            ch.erase(ch.begin() + pick);
-            for (int c = 0; c < 2; ++c) {
-                const Child x = child_of(inner, c);
-                if (x.ref != RT_BVH_EMPTY) ch.push_back(x);
-            }
-        }
-        for (const Child &x : ch)
-            if (!(x.ref & RT_BVH_LEAF) && idx[x.ref] < 0) {
-                idx[x.ref] = (int)order.size();
-                order.push_back(x.ref);
-            }
-        wide.push_back(std::move(ch));
-    }
-    out.bvh8.assign(16 * wide.size(), RtF4{0, 0, 0, 0});
-    for (size_t i = 0; i < wide.size(); ++i)
-        for (int k = 0; k < 8; ++k) {
-            RtF4 *d = &out.bvh8[16 * i + 2 * (size_t)k];
-            uint32_t ref = RT_BVH_EMPTY;
-            if ((size_t)k < wide[i].size()) {
-                const Child &x = wide[i][(size_t)k];
-                ref = (x.ref & RT_BVH_LEAF) ? x.ref : (uint32_t)idx[x.ref];
-                d[0] = RtF4{x.lo[0], x.lo[1], x.lo[2], x.hi[0]};
-                d[1] = RtF4{x.hi[1], x.hi[2], 0.0f, 0.0f};
-            }
-            memcpy(&d[1].z, &ref, 4);
-        }
 }
 
 int prepare_host(const Triangle *tris, int ntris, const KD_Tree_Node *nodes, int nnodes, const int *indices,
@@ -356,11 +255,7 @@ int prepare_host(const Triangle *tris, int ntris, const KD_Tree_Node *nodes, int
     // --- the conservative BVH (bvh_build.h), records in its leaf order ----
     BvhHost bvh;
     out.bvh_depth = -1;
-    const double t0 = omp_get_wtime();
     const int brc = build_bvh(tris, ntris, ta.data(), tbary.data(), bvh);
-    if (getenv("RT_BVH_STATS"))
-        fprintf(stderr, "[bvh] rc %d tris %d nodes %zu depth %d always %d dropped %d scale %g build %.3f s\n", brc,
-                ntris, bvh.nodes.size() / 4, bvh.depth, bvh.always, bvh.dropped, bvh.scale, omp_get_wtime() - t0);
     if (brc == RT_OK && bvh.depth < RT_BVH_STACK) {
         out.bvh_nodes = std::move(bvh.nodes);
         out.bvh_a.resize(bvh.order.size());
@@ -372,15 +267,9 @@ int prepare_host(const Triangle *tris, int ntris, const KD_Tree_Node *nodes, int
         }
         out.bvh_scale = bvh.scale;
         out.bvh_depth = bvh.depth;
-        // the 8-wide BVH and the KD descent shortcut's tables, on request: the lone-ray traversal
-        // of the deep paths (RT_LONE=1, lone_trace.h) uses both, the bulk finisher the shortcut
-        // (RT_KD_RESUME=1).  Both measured slower than the defaults
-        auto on = [](const char *v) { return getenv(v) && atoi(getenv(v)) != 0; };
-        const bool leaf_starts = on("RT_LONE") || on("RT_KD_RESUME");
-        if (leaf_starts) build_bvh8(out);
-        // the grid cells' start nodes always: wf_long enters each deep bounce's KD traversal at
-        // the cell of the ray's origin (wavefront.hip kd_origin_frontier); off with RT_KD_GRID=0
-        if (leaf_starts || !getenv("RT_KD_GRID") || on("RT_KD_GRID")) build_kd_starts(out, bounds, leaf_starts);
+        // the grid cells' start nodes: wf_long enters each deep bounce's KD traversal at the cell
+        // of the ray's origin (coop_trace.h kd_origin_frontier)
+        build_kd_starts(out, bounds);
         out.bvh_always = bvh.always;
         out.bvh_dropped = bvh.dropped;
     } else if (brc != RT_OK && brc != RT_E_UNSUPPORTED) {
@@ -407,10 +296,6 @@ int prepare_host(const Triangle *tris, int ntris, const KD_Tree_Node *nodes, int
         out.split_off[3] = (int)out.split_vals.size();
         if (nan_split) out.bvh_depth = -1;
     }
-
-    if (getenv("RT_BVH_STATS") && out.bvh_depth >= 0)
-        fprintf(stderr, "[bvh] kd starts: %zu rows (%.1f MB)\n", out.kd_rows.size() / 4,
-                (out.kd_rows.size() + out.kd_start.size()) * 4e-6);
 
     // --- lights: one padding entry for the xi == 1.0 draw -----
     out.lights.assign(lights, lights + nlights);

@@ -211,28 +211,35 @@ __global__ void __launch_bounds__(256) rt_tonemap_kernel(const Vec3D *fb, const 
 
 // ---- host launchers (called by abi.hip) ----
 namespace {
-// per-device spill area of the bounded megakernel (grown on demand)
+// Per-device spill area of the bounded megakernel (grown on demand), indexed
+// by global thread id: one launch at a time may use it.  Launches are
+// serialised on it — each waits (on its stream) for the previous launch's
+// event, whatever stream that was on — and the buffer is replaced only after
+// that launch is done, all under the mutex until the launch is enqueued.
+struct MegaSpill {
+    uint2 *buf = nullptr;
+    size_t entries = 0;
+    hipEvent_t last = nullptr; // after the last launch that used buf
+    bool recorded = false;
+};
 std::mutex g_spill_mu;
-std::map<int, std::pair<uint2 *, size_t>> g_spill;
-
-uint2 *mega_spill(size_t entries)
-{
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-    std::lock_guard<std::mutex> g(g_spill_mu);
-    auto &e = g_spill[dev];
-    if (e.second < entries) {
-        if (e.first) (void)hipFree(e.first);
-        e.first = nullptr;
-        e.second = 0;
-        void *p = nullptr;
-        if (hipMalloc(&p, entries * sizeof(uint2)) != hipSuccess) return nullptr;
-        e.first = (uint2 *)p;
-        e.second = entries;
-    }
-    return e.first;
-}
+std::map<int, MegaSpill> g_spill;
 } // namespace
+
+void rt_path_shutdown()
+{
+    std::lock_guard<std::mutex> g(g_spill_mu);
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    for (auto &kv : g_spill) {
+        if (hipSetDevice(kv.first) != hipSuccess) continue;
+        if (kv.second.recorded) (void)hipEventSynchronize(kv.second.last);
+        if (kv.second.buf) (void)hipFree(kv.second.buf);
+        if (kv.second.last) (void)hipEventDestroy(kv.second.last);
+    }
+    g_spill.clear();
+    (void)hipSetDevice(cur);
+}
 
 int rt_launch_path(const RtDevScene &sc, const RtDevFrame &fr, const RtDevCamera &cam, int stack_depth,
                    hipStream_t stream, int traversal)
@@ -244,11 +251,29 @@ int rt_launch_path(const RtDevScene &sc, const RtDevFrame &fr, const RtDevCamera
         // the bounded traversal: the KD part needs <= RT_STACK_DEPTH entries, the BVH part <= RT_BVH_STACK
         const size_t threads = (size_t)tiles * RT_BLOCK;
         const int deeper = (RT_BVH_STACK > RT_STACK_DEPTH ? RT_BVH_STACK : RT_STACK_DEPTH) - RT_MEGA_BVH_LDS;
-        uint2 *spill = mega_spill(threads * (size_t)deeper);
-        if (!spill) return -1;
-        hipLaunchKernelGGL((rt_path_kernel<false, RT_MEGA_BVH_LDS, true>), grid, block, 0, stream, sc, fr, cam, spill,
+        const size_t entries = threads * (size_t)deeper;
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess) return -1;
+        std::lock_guard<std::mutex> g(g_spill_mu);
+        MegaSpill &m = g_spill[dev];
+        if (!m.last && hipEventCreateWithFlags(&m.last, hipEventDisableTiming) != hipSuccess) return -1;
+        if (m.entries < entries) {
+            if (m.recorded && hipEventSynchronize(m.last) != hipSuccess) return -1; // the old buffer's last user
+            if (m.buf) (void)hipFree(m.buf);
+            m.buf = nullptr;
+            m.entries = 0;
+            void *p = nullptr;
+            if (hipMalloc(&p, entries * sizeof(uint2)) != hipSuccess) return -1;
+            m.buf = (uint2 *)p;
+            m.entries = entries;
+        } else if (m.recorded && hipStreamWaitEvent(stream, m.last, 0) != hipSuccess) {
+            return -1; // the previous launch (maybe on another stream) leaves the spill slots first
+        }
+        hipLaunchKernelGGL((rt_path_kernel<false, RT_MEGA_BVH_LDS, true>), grid, block, 0, stream, sc, fr, cam, m.buf,
                            (int)threads);
-        return hipGetLastError() == hipSuccess ? 0 : -1;
+        if (hipGetLastError() != hipSuccess || hipEventRecord(m.last, stream) != hipSuccess) return -1;
+        m.recorded = true;
+        return 0;
     }
     if (stack_depth <= RT_STACK_SMALL) {
         if (count)

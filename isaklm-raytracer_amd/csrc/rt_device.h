@@ -49,8 +49,12 @@
 #define RT_DEV_CUT 2        // paths cut at the depth limit (watchdog or RtOptions.max_depth)
 #define RT_DEV_HIST 3       // + k: paths ending at depth in [64 * 2^k, 64 * 2^(k+1)), k < RT_DEV_HIST_BINS
                             // (isaklm_rt.h: 18 bins, 64 * 2^18 = 2^24 > RT_WATCHDOG_BOUNCES)
+#define RT_DEV_CHECKED 21   // rays of the bounded traversal re-traced by the KD traversal (wf_check)
+#define RT_DEV_MISMATCH 22  // ... whose results differed
+#define RT_DEV_MISRAY 23    // 4 words: set flag, then the first mismatching ray's o, d as packed float bits
 #define RT_DEV_WORDS 32
-static_assert(RT_DEV_HIST + RT_DEV_HIST_BINS <= RT_DEV_WORDS, "deviation block");
+static_assert(RT_DEV_HIST + RT_DEV_HIST_BINS <= RT_DEV_CHECKED && RT_DEV_MISRAY + 4 <= RT_DEV_WORDS,
+              "deviation block");
 
 struct RtDevMaterial {          // 64 B
     float albedo[3];
@@ -96,15 +100,12 @@ struct RtDevScene {
     float bvh_scale;            // largest |vertex|_1 (rt_ray_margin)
     const float *split_vals;    // the KD tree's split values, per axis sorted (rt_bounded_ray)
     int split_off[4];           // axis a: split_vals[split_off[a], split_off[a + 1])
-    // KD descent shortcut (host/scene_prepare.cpp build_kd_starts, bvh_trace.h
-    // kd_resume); nullptr: none
-    const uint32_t *kd_start;   // per BVH leaf slot (its first): {start node, row offset << 5 | depth}
+    // wf_long's origin-cell entry (host/scene_prepare.cpp build_kd_starts,
+    // coop_trace.h kd_origin_frontier); nullptr / 0: none
     const uint32_t *kd_rows;    // 4 words per ancestor: split bits, y word, ancestor index, child taken
-    int kd_resume_bulk;         // trace_bvh uses the shortcut too (RT_KD_RESUME=1; lone_trace always)
     const uint32_t *kd_cell;    // per cell of a kd_grid^3 grid over the scene box: {start node, row offset << 5 | depth}
     int kd_grid;                // cell of p: ((p - bmin) * kd_gscale), clamped to [0, kd_grid - 1]
     float kd_gscale[3];
-    const RtF4 *bvh8;           // 8-wide BVH (lone_trace.h): 16 per node, child k {lo, hi.x}, {hi.yz, ref, 0}; nullptr: none
 };
 
 // BVH child reference: an inner node's index, or RT_BVH_LEAF | first << 3 |

@@ -81,6 +81,7 @@ int rt_reduce_shards(rt_comm_t c, G_Buffer g, int width, int height, int root, v
     }
     const size_t n = (size_t)width * height;
     hipStream_t s = (hipStream_t)stream;
+    if (rt_join(stream) != RT_OK) return RT_E_HIP; // chained renders' deep-path tails first
     NCCLCHK(ncclGroupStart());
     NCCLCHK(ncclReduce(g.frame_buffer, g.frame_buffer, 3 * n, ncclFloat32, ncclSum, root, c->comm, s));
     NCCLCHK(ncclReduce(g.squared_luminance, g.squared_luminance, n, ncclFloat32, ncclSum, root, c->comm, s));

@@ -16,6 +16,8 @@
 #include <hip/hip_runtime.h>
 
 #include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
 #include <time.h>
 
 #include <algorithm>
@@ -27,7 +29,6 @@
 #include <vector>
 
 #include "bvh_trace.h"
-#include "lone_trace.h"
 #include "rt_kernels.h"
 
 using namespace rtk;
@@ -111,9 +112,22 @@ static_assert(WF_BLOCK % WF_TBLOCK == 0 && WF_TBLOCK % 64 == 0, "WF_TBLOCK must 
 #define WF_MAX_PIPES 6                // concurrent pipelines (RtOptions.wf_pipelines); more than 3 need GPU_MAX_HW_QUEUES > 4
 #define WF_PIPES_DEFAULT 3
 #define WF_LONG_DEPTH_DEFAULT 64      // RtOptions.wf_long_depth: paths deeper than this go to wf_long
-#define WF_LONG_CUS_DEFAULT 0         // whole-call mode: CUs of wf_long's own (long_cus; 0: shared)
 #define WF_LONG_BLOCKS 64             // wf_long grid (4 waves each, one path per wave at a time)
-#define WF_LONG_IDLE 2000000000ull   // s_memrealtime ticks (100 MHz): 20 s without a claim ends a wf_long wave
+// safety nets (s_memrealtime ticks, 100 MHz), never reached by a working
+// protocol: a wf_long slice wave leaves after 20 s without a claim; a
+// persistent wf_long wave (whole-call mode) after 600 s without a claim.
+// Either strands pixels instead of hanging the GPU.
+#define WF_LONG_IDLE 2000000000ull
+#define WF_LONG_IDLE_PERSIST 60000000000ull
+#define WF_CHECK_INTERVAL_DEFAULT 1024u // RtOptions.check_interval: 1 ray in this many re-traced by the KD traversal
+#define WF_CHECK_CAP (1u << 20)         // cross-check records per call (more are dropped, not counted)
+// per-pixel hand-off word (WfState.pxo): a pixel handed to wf_long is OUT
+// until a finisher takes it back or wf_long finishes it (LONGDONE: its state
+// was written by the concurrently running wf_long, so the next reader
+// acquires first); the low bits count passes that later chained calls owe it
+#define RT_PX_OUT 0x80000000u
+#define RT_PX_LONGDONE 0x40000000u
+#define RT_PX_PASSES 0x3FFFFFFFu
 
 struct WfState {
     int *passes_left;
@@ -129,32 +143,48 @@ struct WfState {
     uint2 *spill;      // traversal stack spill
     int spill_threads;
     // long-path hand-off (wf_long): a path deeper than long_depth leaves its
-    // pipeline for the concurrently running wf_long kernel
-    uint32_t *long_flag;  // per entry: slot + 1 once published (agent-scope store after a release fence)
-    RtF4 *long_ray;       // 2 per entry
+    // pipeline for the concurrently running wf_long kernel through a ring of
+    // long_cap entries: entry e (counted from the last reset) lives at e %
+    // long_cap, published as long_ent = (e + 1) << 32 | slot after its ray
     uint32_t *long_ctr;   // [0] entries reserved, [1] entries claimed, [3] paths running in wf_long
+    unsigned long long *long_ent;
+    RtF4 *long_ray;       // 2 per ring slot
     int long_depth;       // 0 = off
-    uint32_t long_cap;    // entries of long_flag / long_ray (the pixels)
+    uint32_t long_cap;    // ring slots (the pixels)
     // whole-call finisher (bounded traversal): wf_long runs a handed-over path
     // only to the end of its SAMPLE and returns the pixel through this ring to
     // the finishers, whose lanes run its remaining passes
     int long_return;
     unsigned long long *ret_ring; // entry e at e % long_cap: (e + 1) << 32 | slot once published
-    unsigned long long *long_log; // debug (RT_WF_LONG_LOG): [0] call start, then per claim {claim, end, bounces, slot}
+    unsigned long long *long_log; // debug (RT_DEBUG_LONG_LOG): [0] call start, then per claim {claim, end, bounces, slot}
     // ret_ctr: u64 [0] = finisher waves alive << 32 | returns reserved (wf_long
     // reserves only while a finisher wave is alive; a wave leaves only when
     // every reserved return is claimed: no pixel is stranded, and neither
     // kernel ever waits for the other — they may share a hardware queue);
     // u32 [2] = returns claimed, u32 [3] = pixels out (handed to wf_long, not
     // yet returned or done): an idle finisher wave lingers (s_sleep) while
-    // pixels are out — for at most WF_FIN_LINGER ticks, so that it never
-    // depends on wf_long making progress
+    // pixels are out — for at most `linger` ticks (0 for chained calls, whose
+    // successor takes the returns), so that it never depends on wf_long
     uint32_t *ret_ctr;
+    unsigned long long linger;
+    // per pixel: RT_PX_OUT | passes owed by later chained calls, RT_PX_LONGDONE, or 0
+    uint32_t *pxo;
+    // the persistent wf_long's producers: finisher waves of its call not yet
+    // past their last hand-off (nullptr: wf_long runs in host-kicked slices)
+    uint32_t *fin_live;
     // pixels whose path went to wf_long in the previous call run first (their
     // passes are the call's longest chains): wf_start puts them on path list 1,
     // the whole-call finisher takes list 1 before list 0
     uint8_t *heavy;
     int heavy_first;
+    // run-time exactness guard of the bounded traversal: the finisher records
+    // every ray whose hash of (pixel, pass, depth, kind) hits chk_mask (3 RtF4:
+    // {o, hit bits}, {d, bx}, {by, bz, -, -}); wf_check re-traces them with the
+    // plain KD traversal (nullptr: off)
+    RtF4 *chk;
+    uint32_t *chk_ctr;
+    uint32_t chk_mask;
+    int chk_fault; // (RT_DEBUG_CHECK_FAULT, tests: record a wrong triangle for every checked hit)
 };
 
 namespace {
@@ -193,32 +223,46 @@ __device__ __forceinline__ void enqueue_path(const WfState &st, int q, bool want
     if (want) st.q_slot[q][i] = slot;
 }
 
-// hand `to_long` lanes' paths (state already stored) to wf_long: reserve an
-// entry, store the ray, drain this wave's stores, release (write back the
-// XCD's L2: MI355X_MICROARCH.md hand-off rules), then publish the entry with
-// an agent-scope store that wf_long's claims check
+// publish ring entry e of the long-path hand-off: the ray, then (after this
+// wave's stores are drained and released: the XCD's L2 written back,
+// MI355X_MICROARCH.md hand-off rules) the tag wf_long's claims check
+__device__ __forceinline__ void long_publish(const WfState &st, bool to_long, uint32_t e, uint32_t slot, Vec3D o,
+                                             Vec3D d)
+{
+    const uint32_t k = e % st.long_cap;
+    if (to_long) {
+        st.long_ray[2 * (size_t)k] = RtF4{o.x, o.y, o.z, 0.0f};
+        st.long_ray[2 * (size_t)k + 1] = RtF4{d.x, d.y, d.z, 0.0f};
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (to_long) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(st.long_ent + k, ((unsigned long long)(e + 1u) << 32) | slot, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// hand `to_long` lanes' paths (state already stored) to wf_long (queue
+// kernels: a pixel is handed over at most once per call, and the ring is
+// reset per call, so its long_cap = pixels entries never wrap)
 __device__ __forceinline__ void publish_long(const WfState &st, bool to_long, uint32_t slot, Vec3D o, Vec3D d)
 {
     uint32_t e = 0;
     if (to_long) {
         st.heavy[slot] = st.heavy[slot] | 1u;
         e = __hip_atomic_fetch_add(st.long_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        st.long_ray[2 * (size_t)e] = RtF4{o.x, o.y, o.z, 0.0f};
-        st.long_ray[2 * (size_t)e + 1] = RtF4{d.x, d.y, d.z, 0.0f};
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (to_long) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(st.long_flag + e, slot + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    long_publish(st, to_long, e, slot, o, d);
 }
 
 // the finisher's hand-off: as publish_long, but the wave reserves its entries
-// with one compare-and-swap that never passes long_cap (a pixel can be handed
-// over several times per call when wf_long returns it after each deep
-// sample).  Returns false (wave-uniform) when the entries would not fit: the
-// lanes then keep their paths.  The path state is stored by the caller first.
+// with one compare-and-swap that never laps an unclaimed entry (a pixel can be
+// handed over several times per call when wf_long returns it after each deep
+// sample, and chained calls keep the ring running).  Returns false
+// (wave-uniform) when the entries would not fit: the lanes then keep their
+// paths.  The path state is stored by the caller first; the pixel is OUT
+// (pxo) from here until a finisher takes it back or wf_long finishes it.
 __device__ __forceinline__ bool publish_long_capped(const WfState &st, bool to_long, uint32_t slot, Vec3D o, Vec3D d)
 {
     const unsigned long long m = __ballot(to_long);
@@ -228,7 +272,9 @@ __device__ __forceinline__ bool publish_long_capped(const WfState &st, bool to_l
     uint32_t base = 0xffffffffu;
     if (lane == leader) {
         uint32_t r = __hip_atomic_load(st.long_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        while (r + k <= st.long_cap) {
+        while (true) {
+            const uint32_t c = __hip_atomic_load(st.long_ctr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (r + k - c > st.long_cap) break; // (c may be stale-low: conservative)
             if (__hip_atomic_compare_exchange_strong(st.long_ctr, &r, r + k, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                      __HIP_MEMORY_SCOPE_AGENT)) {
                 base = r;
@@ -243,15 +289,9 @@ __device__ __forceinline__ bool publish_long_capped(const WfState &st, bool to_l
     const uint32_t e = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
     if (to_long) {
         st.heavy[slot] = st.heavy[slot] | 1u;
-        st.long_ray[2 * (size_t)e] = RtF4{o.x, o.y, o.z, 0.0f};
-        st.long_ray[2 * (size_t)e + 1] = RtF4{d.x, d.y, d.z, 0.0f};
+        if (st.long_return) __hip_atomic_store(st.pxo + slot, RT_PX_OUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (to_long) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(st.long_flag + e, slot + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    long_publish(st, to_long, e, slot, o, d);
     return true;
 }
 
@@ -295,7 +335,25 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_start(RtDevFrame fr, RtDevCamera 
     const int slot = valid ? y * fr.width + x : 0;
     bool want = false;
     Vec3D ro = rt_v3(0, 0, 0), rd = rt_v3(0, 0, 0);
-    if (valid && slot < n) {
+    // whole-call mode: a pixel still OUT in wf_long (a chained call's deep
+    // sample, still running) is left to whoever holds it: its passes are
+    // owed (pxo), and the holder runs them.  One that wf_long finished
+    // concurrently (LONGDONE) is read after an acquire.
+    bool owned = valid && slot < n;
+    if (st.long_return && owned) {
+        uint32_t x = __hip_atomic_load(st.pxo + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        while (x & RT_PX_OUT) {
+            if (__hip_atomic_compare_exchange_strong(st.pxo + slot, &x, x + (uint32_t)fr.passes, __ATOMIC_RELAXED,
+                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                owned = false;
+                break;
+            }
+        }
+        const bool acq = owned && x == RT_PX_LONGDONE;
+        if (__any(acq)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        if (acq) __hip_atomic_store(st.pxo + slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (owned) {
         Vec3D fb = rt_v3(0.0f, 0.0f, 0.0f);
         float sq = 0.0f;
         int count = 0;
@@ -321,7 +379,7 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_start(RtDevFrame fr, RtDevCamera 
     }
     if (st.heavy_first) { // the whole-call finisher: no ray queue; heavy pixels on list 1
         bool h = false;
-        if (valid && slot < n) {
+        if (owned) {
             const uint8_t v = st.heavy[slot];
             h = v != 0;
             if (v & 1u) st.heavy[slot] = v & 2u; // bit 0: set again by this call's hand-offs (bit 1 stays)
@@ -1020,6 +1078,10 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_FIN_BVH_WAVES) wf_finish_bvh(RtDe
                     __hip_atomic_fetch_sub(st.ret_ctr + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     active = true;
                     first_ray(st, fr, (uint32_t)v, p);
+                    // back from wf_long: no longer OUT; plus the passes chained calls queued meanwhile
+                    const uint32_t owed = __hip_atomic_exchange(st.pxo + (uint32_t)v, 0u, __ATOMIC_RELAXED,
+                                                                __HIP_MEMORY_SCOPE_AGENT);
+                    p.passes_left += (int)(owed & RT_PX_PASSES);
                 }
             }
         }
@@ -1030,7 +1092,8 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_FIN_BVH_WAVES) wf_finish_bvh(RtDe
             int leave = 0;
             if (lane == 0) {
                 if (idle_since == 0) idle_since = __builtin_amdgcn_s_memrealtime();
-                bool out = __hip_atomic_load(st.ret_ctr + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+                bool out = st.linger != 0 &&
+                           __hip_atomic_load(st.ret_ctr + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
                 // only WF_FIN_LINGER_WAVES waves linger (a seat each, kept until they leave): the
                 // others leave their slots to wf_long, which the deep paths are waiting for
                 if (out && !seated) {
@@ -1042,7 +1105,7 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_FIN_BVH_WAVES) wf_finish_bvh(RtDe
                 }
                 unsigned long long w = __hip_atomic_load(ret_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 const uint32_t cl = __hip_atomic_load(ret_claimed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if ((uint32_t)w == cl && (!out || __builtin_amdgcn_s_memrealtime() - idle_since > WF_FIN_LINGER) &&
+                if ((uint32_t)w == cl && (!out || __builtin_amdgcn_s_memrealtime() - idle_since > st.linger) &&
                     __hip_atomic_compare_exchange_strong(ret_word, &w, w - (1ull << 32), __ATOMIC_RELAXED,
                                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
                     leave = 1;
@@ -1056,6 +1119,25 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_FIN_BVH_WAVES) wf_finish_bvh(RtDe
         if (active) {
             float bx = 0.0f, by = 0.0f, bz = 0.0f;
             const int hit = trace_bvh<COUNT>(sc, p.ro, p.rd, bx, by, bz, stk, c);
+            // run-time exactness guard: a deterministic sample of the rays, with the
+            // bounded result, is queued for wf_check's plain KD re-trace
+            if (!COUNT && st.chk) {
+                uint32_t h = p.slot * 0x9E3779B1u ^ (uint32_t)p.passes_left * 0x85EBCA77u ^
+                             (uint32_t)p.depth * 0xC2B2AE3Du ^ (p.shadow ? 0x27D4EB2Fu : 0u);
+                h ^= h >> 15;
+                h *= 0x2C1B3C6Du;
+                h ^= h >> 12;
+                const bool rec = (h & st.chk_mask) == 0u;
+                if (__any(rec)) {
+                    const uint32_t i = wave_append(st.chk_ctr, rec);
+                    if (rec && i < WF_CHECK_CAP) {
+                        st.chk[3 * (size_t)i] =
+                            RtF4{p.ro.x, p.ro.y, p.ro.z, __int_as_float(st.chk_fault && hit >= 0 ? hit ^ 1 : hit)};
+                        st.chk[3 * (size_t)i + 1] = RtF4{p.rd.x, p.rd.y, p.rd.z, bx};
+                        st.chk[3 * (size_t)i + 2] = RtF4{by, bz, 0.0f, 0.0f};
+                    }
+                }
+            }
             const bool cam_ray = !p.shadow && p.depth == 1;
             const bool want = shade_step<COUNT>(sc, fr, cam, p, hit, bx, by, bz, limit, c);
             // heavy-first ordering: a pixel whose camera ray enters glass (where the
@@ -1069,6 +1151,57 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_FIN_BVH_WAVES) wf_finish_bvh(RtDe
         if (__any(to_long) && publish_long_capped(st, to_long, p.slot, p.ro, p.rd) && to_long) active = false;
     }
     if (COUNT) flush_counters(c, fr.counters);
+    if (st.fin_live) { // this wave's hand-offs are published: the persistent wf_long may stop once all are past here
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        if (lane == 0) __hip_atomic_fetch_sub(st.fin_live, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// The run-time exactness guard's second half: every ray wf_finish_bvh
+// recorded is traced again with the plain KD traversal (trace(), i.e.
+// trace_ray, rt/trace_ray.cuh:244-318) and compared bit for bit with the
+// bounded result (triangle, barycentrics).  Counts checks and mismatches in
+// the deviation statistics and keeps the first mismatching ray.  One ray per
+// lane, grid-stride within the spill area (grid blocks).
+__global__ void __launch_bounds__(WF_BLOCK) wf_check(RtDevScene sc, WfState st, unsigned long long *dev)
+{
+    __shared__ uint32_t s_node[WF_LDS_STACK * WF_BLOCK];
+    __shared__ float s_entry[WF_LDS_STACK * WF_BLOCK];
+    const int tid = threadIdx.x;
+    const int gtid = blockIdx.x * WF_BLOCK + tid;
+    Stack<WF_LDS_STACK> stk{s_node + tid, s_entry + tid, WF_BLOCK, st.spill + gtid, st.spill_threads};
+    Cnt c;
+    uint32_t n = *st.chk_ctr;
+    n = n < WF_CHECK_CAP ? n : WF_CHECK_CAP;
+    unsigned long long checked = 0, bad = 0;
+    for (uint32_t e = gtid; e < n; e += gridDim.x * WF_BLOCK) {
+        const RtF4 a = st.chk[3 * (size_t)e], b = st.chk[3 * (size_t)e + 1], q = st.chk[3 * (size_t)e + 2];
+        const Vec3D o = rt_v3(a.x, a.y, a.z), d = rt_v3(b.x, b.y, b.z);
+        float bx = 0.0f, by = 0.0f, bz = 0.0f;
+        const int hit = trace<false>(sc, o, d, bx, by, bz, stk, c);
+        ++checked;
+        const bool same = hit == __float_as_int(a.w) &&
+                          (hit < 0 || (__float_as_uint(bx) == __float_as_uint(b.w) &&
+                                       __float_as_uint(by) == __float_as_uint(q.x) &&
+                                       __float_as_uint(bz) == __float_as_uint(q.y)));
+        if (!same) {
+            ++bad;
+            if (atomicCAS(dev + RT_DEV_MISRAY, 0ull, 1ull) == 0ull) { // the first mismatch: its ray
+                dev[RT_DEV_MISRAY + 1] = (unsigned long long)__float_as_uint(o.x) << 32 | __float_as_uint(o.y);
+                dev[RT_DEV_MISRAY + 2] = (unsigned long long)__float_as_uint(o.z) << 32 | __float_as_uint(d.x);
+                dev[RT_DEV_MISRAY + 3] = (unsigned long long)__float_as_uint(d.y) << 32 | __float_as_uint(d.z);
+            }
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        checked += __shfl_xor(checked, off);
+        bad += __shfl_xor(bad, off);
+    }
+    if ((tid & 63) == 0) {
+        if (checked) atomicAdd(dev + RT_DEV_CHECKED, checked);
+        if (bad) atomicAdd(dev + RT_DEV_MISMATCH, bad);
+    }
 }
 
 // Cooperative finisher: runs queued paths to the end of their passes in
@@ -1190,31 +1323,34 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_FIN_OCC) wf_finish_coop(RtDevScen
 }
 
 // Long paths (total internal reflection in glass runs to 10^4 bounces and
-// more) would otherwise advance one bounce per queue iteration and then hold
-// up the end of the call in the finisher.  wf_shade hands every path deeper
-// than st.long_depth to this kernel, launched on the caller's stream (idle
-// during the call) in slices beside the pipelines: each wave claims the next
+// more) would otherwise hold up the end of the call one bounce per queue
+// iteration or one lane at a time.  Paths deeper than st.long_depth are handed
+// to this kernel through the hand-off ring; each wave claims the next
 // PUBLISHED entry in order (compare-and-swap on the claim counter, never an
-// entry whose publication is still in flight) and runs that path to the end
-// of its pixel's passes, every ray traced by all 64 lanes (wide_trace), lane 0
-// shading.  A wave with nothing to claim keeps polling only while another
-// wave of this slice still runs a path (new paths keep arriving meanwhile),
-// then leaves; the host launches the next slice when this one is over.  The
-// slice never waits on work another queue must do, so it cannot deadlock
-// when the runtime maps the caller's stream and a pipeline stream to one
-// hardware queue.  The final slice (every producer done, all entries
-// published) drains what is left.
+// entry whose publication is still in flight) and runs that path with every
+// ray traced by all 64 lanes (wide_trace), lane 0 shading.
+//
+// Two launch forms:
+//  * whole-call mode (st.fin_live != nullptr): ONE persistent launch per call
+//    on its own stream, beside the finisher; a wave leaves once every finisher
+//    wave of its call is past its last hand-off (fin_live == 0) and every
+//    reserved entry is claimed.  It runs a path only to the end of its deep
+//    SAMPLE, then returns the pixel to a live finisher (return ring) or, with
+//    none alive, runs the pixel's remaining passes itself — including passes
+//    that later chained calls owe it (pxo) — and releases it (LONGDONE).
+//  * queue mode (fin_live == nullptr): slices on the caller's stream, kicked
+//    by the pipelines' host threads; a wave with nothing to claim waits only
+//    while another path is running, the final slice drains the rest; a path
+//    runs to the end of its pixel's passes.
+// Neither form ever waits on work another queue must do, so neither can
+// deadlock when the runtime maps two of these streams onto one hardware queue.
 template <bool COUNT>
 __global__ void __launch_bounds__(WF_BLOCK, WF_LONG_WAVES) wf_long(RtDevScene sc, RtDevFrame fr, RtDevCamera cam, WfState st,
-                                                    int final_slice, int bounded)
+                                                    int final_slice)
 {
-    __shared__ uint32_t s_wnode[(WF_BLOCK / 64) * WF_BVH_LDS]; // bounded: one stack per wave (WaveStack)
-    __shared__ float s_wentry[(WF_BLOCK / 64) * WF_BVH_LDS];
     __shared__ WideItem s_wide[(WF_BLOCK / 64) * WIDE_CAP];
     __shared__ unsigned long long s_key[(WF_BLOCK / 64) * 4];
     __shared__ int s_mark[2 * WF_BLOCK]; // 128 per wave: chunk_owner marks + junk slots
-    __shared__ uint32_t s_lnode[(WF_BLOCK / 64) * LONE_STACK]; // lone_trace: one stack per wave
-    __shared__ float s_lkey[(WF_BLOCK / 64) * LONE_STACK];
     if (WF_LONG_PRIO > 0) __builtin_amdgcn_s_setprio(WF_LONG_PRIO);
     const int lane = __lane_id();
     const int wave = threadIdx.x >> 6;
@@ -1224,52 +1360,70 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_LONG_WAVES) wf_long(RtDevScene sc
     if (COUNT) c.zero();
     const int limit = fr.max_depth > 0 ? fr.max_depth : RT_WATCHDOG_BOUNCES;
     uint32_t *const reserved = st.long_ctr, *const claimed = st.long_ctr + 1, *const running = st.long_ctr + 3;
+    const bool persist = st.fin_live != nullptr;
     unsigned long long t_idle = __builtin_amdgcn_s_memrealtime();
     while (true) {
-        // ---- claim the next published entry (lane 0)
-        uint32_t e = 0, flag = 0;
+        // ---- claim the next published entry (lane 0): its tag and ray are read
+        // before the claim (a claimed ring slot may be reused at once)
+        uint32_t e = 0, slot = 0;
+        RtF4 ro4{0, 0, 0, 0}, rd4{0, 0, 0, 0};
         int quit = 0;
         if (lane == 0) {
             while (true) {
+                // (producers first: once they are all past their last hand-off,
+                // `reserved` read after this acquire holds every entry)
+                const bool done = persist && __hip_atomic_load(st.fin_live, __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_AGENT) == 0u;
+                if (done) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                 e = __hip_atomic_load(claimed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 const uint32_t r = __hip_atomic_load(reserved, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                flag = e < r ? __hip_atomic_load(st.long_flag + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-                if (flag) {
-                    uint32_t expect = e;
-                    if (__hip_atomic_compare_exchange_strong(claimed, &expect, e + 1u, __ATOMIC_RELAXED,
-                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                        __hip_atomic_fetch_add(running, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (e < r) {
+                    const uint32_t k = e % st.long_cap;
+                    const unsigned long long v =
+                        __hip_atomic_load(st.long_ent + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if ((uint32_t)(v >> 32) == e + 1u) { // published: acquire, read, then claim
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                        ro4 = ldf4(st.long_ray + 2 * (size_t)k);
+                        rd4 = ldf4(st.long_ray + 2 * (size_t)k + 1);
+                        slot = (uint32_t)v;
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        uint32_t expect = e;
+                        if (__hip_atomic_compare_exchange_strong(claimed, &expect, e + 1u, __ATOMIC_RELAXED,
+                                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                            __hip_atomic_fetch_add(running, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            break;
+                        }
+                        continue; // another wave took it: try the next one
+                    }
+                    // reserved, its publication still in flight: wait for it
+                } else {
+                    // nothing claimable.  Persistent: done once the producers are; slices: the
+                    // final one once every entry is claimed, the others unless a path still runs.
+                    const bool others = __hip_atomic_load(running, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+                    if (persist ? done : (final_slice || !others)) {
+                        quit = 1;
                         break;
                     }
-                    continue; // another wave took it: try the next one
                 }
-                // nothing claimable now.  Final slice: done once every entry is claimed.  Otherwise wait
-                // only while a path of this slice is still running.  Safety net: WF_LONG_IDLE ticks idle.
-                const bool others = __hip_atomic_load(running, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
-                if ((final_slice ? e >= r : !others) ||
-                    __builtin_amdgcn_s_memrealtime() - t_idle > WF_LONG_IDLE) {
-                    quit = 1;
+                if (__builtin_amdgcn_s_memrealtime() - t_idle > (persist ? WF_LONG_IDLE_PERSIST : WF_LONG_IDLE)) {
+                    quit = 1; // safety net (see WF_LONG_IDLE)
                     break;
                 }
                 __builtin_amdgcn_s_sleep(16);
             }
-            if (!quit) { // acquire: this lane's loads below see the producer's stores
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
+            if (!quit) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         // (lane 0's values, wave-uniform: readfirstlane — every lane is active here)
         if (__builtin_amdgcn_readfirstlane(quit)) break;
         e = (uint32_t)__builtin_amdgcn_readfirstlane((int)e);
-        flag = (uint32_t)__builtin_amdgcn_readfirstlane((int)flag);
-        // ---- run the path (state in lane 0) to the end of its pixel's passes
+        // ---- run the path (state in lane 0)
         PathRegs p;
         p.slot = 0;
         p.ro = p.rd = rt_v3(0, 0, 0);
         if (lane == 0) {
-            load_regs(st, fr, flag - 1u, p);
-            p.ro = ld3(ldf4(st.long_ray + 2 * (size_t)e));
-            p.rd = ld3(ldf4(st.long_ray + 2 * (size_t)e + 1));
+            load_regs(st, fr, slot, p);
+            p.ro = ld3(ro4);
+            p.rd = ld3(rd4);
         }
         int want = 0; // after the loop: 0 the pixel's passes are done, 2 returned to the finishers
         uint32_t ret_e = 0;
@@ -1279,25 +1433,6 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_LONG_WAVES) wf_long(RtDevScene sc
             ++bounces;
             int hit = -1;
             float bx = 0.0f, by = 0.0f, bz = 0.0f;
-            if (!COUNT && bounded == 2) {
-                // the deep path's ray with the lone-ray traversal (lone_trace.h): every lane on it
-                auto uni = [](float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); };
-                const Vec3D o = rt_v3(uni(p.ro.x), uni(p.ro.y), uni(p.ro.z));
-                const Vec3D d = rt_v3(uni(p.rd.x), uni(p.rd.y), uni(p.rd.z));
-                const LoneLds L{s_lnode + wave * LONE_STACK, s_lkey + wave * LONE_STACK};
-                WaveStack<WF_BVH_LDS> ws{s_wnode + wave * WF_BVH_LDS, s_wentry + wave * WF_BVH_LDS,
-                                         st.spill + blockIdx.x * (WF_BLOCK / 64) + wave, st.spill_threads};
-                hit = lone_trace(sc, o, d, bx, by, bz, L, ws, c);
-            } else if (!COUNT && bounded) {
-                // every lane traces lane 0's ray with the bounded traversal: wave-uniform
-                // addresses, so its node and record loads are scalar loads
-                auto uni = [](float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); };
-                const Vec3D o = rt_v3(uni(p.ro.x), uni(p.ro.y), uni(p.ro.z));
-                const Vec3D d = rt_v3(uni(p.rd.x), uni(p.rd.y), uni(p.rd.z));
-                WaveStack<WF_BVH_LDS> ws{s_wnode + wave * WF_BVH_LDS, s_wentry + wave * WF_BVH_LDS,
-                                         st.spill + blockIdx.x * (WF_BLOCK / 64) + wave, st.spill_threads};
-                hit = trace_bvh<false>(sc, o, d, bx, by, bz, ws, c);
-            } else {
             CoopRay r;
             coop_idle(r);
             if (lane == 0) {
@@ -1313,10 +1448,39 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_LONG_WAVES) wf_long(RtDevScene sc
                 if (nf > 0) wide_trace_from<COUNT>(sc, o, d, nf, W, lane == 0, hit, bx, by, bz, c);
                 else wide_trace<COUNT>(sc, o, d, en, ex, W, lane == 0, hit, bx, by, bz, c);
             }
-            }
             want = 0;
             if (lane == 0) {
                 want = shade_step<COUNT>(sc, fr, cam, p, hit, bx, by, bz, limit, c) ? 1 : 0;
+                if (!want && st.long_return) {
+                    // the pixel's passes are done: run the passes chained calls owe it, or
+                    // release it — its state stored and released before the word says so
+                    while (true) {
+                        store_regs(st, fr, p);
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                        uint32_t x = RT_PX_OUT;
+                        if (__hip_atomic_compare_exchange_strong(st.pxo + p.slot, &x, RT_PX_LONGDONE, __ATOMIC_RELAXED,
+                                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                            break;
+                        x = __hip_atomic_exchange(st.pxo + p.slot, RT_PX_OUT, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+                        p.passes_left = (int)(x & RT_PX_PASSES);
+                        const Vec3D fb = fr.fb[p.slot];
+                        const float sq = fr.sq[p.slot];
+                        const int count = fr.count[p.slot];
+                        if (start_sample<COUNT>(fr, cam, (int)p.slot, p.passes_left, p.rng, fb, sq, count, p.ro, p.rd,
+                                                c)) { // as shade_step's next pass
+                            p.T = rt_v3(1.0f, 1.0f, 1.0f);
+                            p.L = rt_v3(0.0f, 0.0f, 0.0f);
+                            p.inside = false;
+                            p.prev_type = PRIMARY;
+                            p.depth = 1;
+                            p.shadow = false;
+                            want = 1;
+                            break;
+                        }
+                    }
+                }
                 // return mode: the deep sample is over once the pixel's next one starts (depth 1);
                 // the pixel goes back to the finishers if one is still alive to take it
                 if (want && st.long_return && p.depth == 1 && !p.shadow) {
@@ -1343,8 +1507,8 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_LONG_WAVES) wf_long(RtDevScene sc
                 L[2] = bounces;
                 L[3] = p.slot;
             }
-            store_regs(st, fr, p);
-            if (want == 2) { // back to the finishers: its next ray, then its ring entry
+            if (want == 2) { // back to the finishers: its state and next ray, then its ring entry
+                store_regs(st, fr, p);
                 st.ro[p.slot] = p.ro;
                 st.cont[p.slot] = p.rd;
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1352,8 +1516,10 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_LONG_WAVES) wf_long(RtDevScene sc
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __hip_atomic_store(st.ret_ring + ret_e % st.long_cap, ((unsigned long long)(ret_e + 1u) << 32) | p.slot,
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            } else if (st.long_return) { // the pixel's passes are done: no longer out
+            } else if (st.long_return) { // done and released above (its state may already be another's)
                 __hip_atomic_fetch_sub(st.ret_ctr + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                store_regs(st, fr, p);
             }
             __hip_atomic_fetch_sub(running, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -1363,6 +1529,8 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_LONG_WAVES) wf_long(RtDevScene sc
 }
 
 // ---------------------------------------------------------------- launcher
+void rt_register_shutdown(); // abi.hip: rt_shutdown at exit, before the HIP runtime's finalisers
+
 namespace {
 
 // One pipeline = its own ray queues, hits, counters, stack spill area and
@@ -1370,6 +1538,9 @@ namespace {
 // pipelines run concurrently (one host thread each), so the latency-bound
 // tail of one pipeline's trace launches and its finisher overlap the other
 // pipelines' bulk work.  Per-pixel path state is shared (pixels are disjoint).
+// The whole-call mode uses pipeline 0 and runs its persistent wf_long on
+// pipeline 1's or 2's stream (alternating per call: a chained call's wf_long
+// may start while the previous one still runs deep paths).
 struct Pipe {
     std::vector<std::pair<float, float>> trace_iv; // profiled trace launches: [start, end] ms after the call's start
     WfState st{};
@@ -1378,8 +1549,19 @@ struct Pipe {
     hipEvent_t ev[6] = {};   // RtOptions.profile
     hipEvent_t join = nullptr;
     hipEvent_t fin_done = nullptr; // after the finisher (the host polls it while kicking wf_long slices)
+    hipEvent_t long_done = nullptr; // whole-call mode: after a persistent wf_long on this stream
     bool joined = false; // join recorded by a previous call
+    bool long_rec = false; // long_done recorded by a previous call
     RtProfile prof{};
+};
+
+// the frame a chained call continues (RtOptions.overlap): everything a pixel's
+// passes depend on besides its own G_Buffer state
+struct ChainKey {
+    const void *nodes, *bvh, *fb, *sq, *count, *rng;
+    int width, height, adaptive, min_samples, max_depth, shard_id, num_shards, long_depth;
+    float tolerance;
+    RtDevCamera cam;
 };
 
 struct Workspace {
@@ -1389,19 +1571,28 @@ struct Workspace {
     void *blob = nullptr;
     Pipe pipe[WF_MAX_PIPES];
     bool streams_ok = false;
-    hipEvent_t fork = nullptr, ev0 = nullptr, ev1 = nullptr;
-    hipEvent_t long_ev = nullptr; // after the last wf_long slice on the caller's stream
+    hipEvent_t fork = nullptr, ev0 = nullptr, ev1 = nullptr, fin_ready = nullptr;
+    hipEvent_t long_ev = nullptr; // after the last wf_long slice on the caller's stream (queue mode)
     bool recorded = false;   // long_ev recorded by a previous call
-    // CU partition of the whole-call finisher mode: wf_long on `long_cus` CUs of
-    // its own, the finisher pipeline on the rest (0: shared CUs, the caller's stream)
-    int long_cus = 0;
-    int total_cus = 0;
-    hipStream_t long_stream = nullptr, fin_stream = nullptr;
-    hipEvent_t part_ev = nullptr;
+    uint32_t *fin_live = nullptr; // 8 producer words (whole-call mode, one per call in flight: call % 8)
+    RtF4 *chk = nullptr;          // the exactness guard's records (WF_CHECK_CAP x 3 RtF4) and their counter
+    uint32_t *chk_ctr = nullptr;
+    unsigned long long call_seq = 0;
+    bool chain_open = false; // the last call was a whole-call call with RtOptions.overlap
+    ChainKey key{};
     RtProfile prof{};        // last profiled call
 };
 
-std::map<int, Workspace> g_ws; // per device
+std::mutex g_ws_mu;
+std::map<int, Workspace *> g_ws; // per device (owned; released by rt_shutdown)
+
+Workspace &workspace(int dev)
+{
+    std::lock_guard<std::mutex> g(g_ws_mu);
+    Workspace *&w = g_ws[dev];
+    if (!w) w = new Workspace();
+    return *w;
+}
 
 __global__ void wf_bind_stream() {}
 
@@ -1413,6 +1604,7 @@ int ensure_streams(Workspace &w, int npipes)
 {
     if (!w.streams_ok) {
         if (hipEventCreateWithFlags(&w.fork, hipEventDisableTiming) != hipSuccess) return -1;
+        if (hipEventCreateWithFlags(&w.fin_ready, hipEventDisableTiming) != hipSuccess) return -1;
         if (hipEventCreateWithFlags(&w.long_ev, hipEventDisableTiming) != hipSuccess) return -1;
         if (hipEventCreate(&w.ev0) != hipSuccess || hipEventCreate(&w.ev1) != hipSuccess) return -1;
         w.streams_ok = true;
@@ -1424,6 +1616,7 @@ int ensure_streams(Workspace &w, int npipes)
         if (hipHostMalloc((void **)&p.host_count, 64) != hipSuccess) return -1;
         if (hipEventCreateWithFlags(&p.join, hipEventDisableTiming) != hipSuccess) return -1;
         if (hipEventCreateWithFlags(&p.fin_done, hipEventDisableTiming) != hipSuccess) return -1;
+        if (hipEventCreateWithFlags(&p.long_done, hipEventDisableTiming) != hipSuccess) return -1;
         for (auto &e : p.ev)
             if (hipEventCreate(&e) != hipSuccess) return -1;
         hipLaunchKernelGGL(wf_bind_stream, dim3(1), dim3(64), 0, p.stream);
@@ -1432,57 +1625,16 @@ int ensure_streams(Workspace &w, int npipes)
     return 0;
 }
 
-// CUs of wf_long's own in the whole-call mode (RT_WF_LONG_CUS, default 0:
-// shared CUs).  Measured per 256-pass room2m call (median of 5 calls, two
-// rounds, tools/gpu_r03_cu.sh): 0 / 8 / 16 / 32 CUs 1.54-1.78 / 1.51-1.53 /
-// 1.49-1.51 / 1.59-2.00 s, but the driver-style 20-step bench equal within
-// its noise (325.5 vs 325.1 Msamples/s), and a process holding CU-masked
-// queues crashes in rocprofv3's exit (--pmc and --kernel-trace: SIGSEGV in
-// __cxa_finalize, the trace summary not written) — so not by default
-int long_cus()
-{
-    static const int k = getenv("RT_WF_LONG_CUS") ? atoi(getenv("RT_WF_LONG_CUS")) : WF_LONG_CUS_DEFAULT;
-    return k;
-}
-
-// the CU-partitioned streams (created once, on the first whole-call launch that
-// asks for them): wf_long's stream on `cus` CUs spread over the chip, the
-// finisher's on the others.  Returns 0 with no partition when the runtime
-// refuses a CU-masked stream.
-int ensure_partition(Workspace &w, int cus)
-{
-    if (w.long_stream || cus <= 0) return 0;
-    int dev = 0;
-    hipDeviceProp_t prop;
-    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return -1;
-    const int n = prop.multiProcessorCount;
-    if (cus >= n) return 0;
-    std::vector<uint32_t> lm((size_t)(n + 31) / 32, 0u), fm((size_t)(n + 31) / 32, 0u);
-    for (int k = 0; k < cus; ++k) {
-        const int cu = (int)(((long long)k * n) / cus);
-        lm[(size_t)cu / 32] |= 1u << (cu % 32);
-    }
-    for (int cu = 0; cu < n; ++cu)
-        if (!(lm[(size_t)cu / 32] >> (cu % 32) & 1u)) fm[(size_t)cu / 32] |= 1u << (cu % 32);
-    if (hipExtStreamCreateWithCUMask(&w.long_stream, (uint32_t)lm.size(), lm.data()) != hipSuccess ||
-        hipExtStreamCreateWithCUMask(&w.fin_stream, (uint32_t)fm.size(), fm.data()) != hipSuccess) {
-        (void)hipGetLastError();
-        w.long_stream = w.fin_stream = nullptr;
-        return 0;
-    }
-    if (hipEventCreateWithFlags(&w.part_ev, hipEventDisableTiming) != hipSuccess) return -1;
-    w.long_cus = cus;
-    w.total_cus = n;
-    return 0;
-}
-
 int ensure(Workspace &w, size_t slots, int grid, int npipes)
 {
-    if (ensure_streams(w, npipes) != 0) return -1;
+    if (ensure_streams(w, npipes > WF_PIPES_DEFAULT ? npipes : WF_PIPES_DEFAULT) != 0) return -1;
     if (w.slots >= slots && w.grid >= grid && w.spill_pipes >= npipes) return 0;
     // traversal stack spill for the pipelines in use (at least the default 3)
     const int spill_pipes = npipes > WF_PIPES_DEFAULT ? npipes : WF_PIPES_DEFAULT;
-    if (w.blob) (void)hipFree(w.blob);
+    if (w.blob) {
+        (void)hipDeviceSynchronize(); // (a chained call's wf_long may still use the old blob)
+        (void)hipFree(w.blob);
+    }
     w.blob = nullptr;
     const size_t spill_threads = (size_t)grid * WF_BLOCK;
     size_t off = 0;
@@ -1494,10 +1646,11 @@ int ensure(Workspace &w, size_t slots, int grid, int npipes)
     // per pixel
     const size_t o_pl = take(slots * 4), o_fl = take(slots * 4), o_T = take(slots * 12), o_L = take(slots * 12),
                  o_c = take(slots * 12), o_n = take(slots * 12), o_rp = take(slots * 12), o_li = take(slots * 4),
-                 o_ro = take(slots * 12), o_es = take(slots * 4), o_ee = take(slots * 4);
-    // long-path hand-off (shared by the pipelines), wf_long's stack-free wide traversal needs no spill
-    const size_t o_lf = take(slots * 4), o_lr = take(slots * 32), o_lc = take(256), o_rr = take(slots * 8),
-                 o_rc = take(256), o_hv = take(slots);
+                 o_ro = take(slots * 12), o_es = take(slots * 4), o_ee = take(slots * 4), o_px = take(slots * 4);
+    // long-path hand-off (shared by the pipelines), wf_long's stack-free wide traversal needs no spill;
+    // the cross-check records
+    const size_t o_le = take(slots * 8), o_lr = take(slots * 32), o_lc = take(256), o_rr = take(slots * 8),
+                 o_rc = take(256), o_hv = take(slots), o_ctl = take(256), o_chk = take((size_t)WF_CHECK_CAP * 48);
     // per pipeline (path lists sized for every pixel: a pipeline never holds
     // more; ray queues for two rays per path: a shadow and an extension ray)
     size_t o_qs0[WF_MAX_PIPES], o_qs1[WF_MAX_PIPES], o_qr0[WF_MAX_PIPES], o_qr1[WF_MAX_PIPES], o_h[WF_MAX_PIPES],
@@ -1517,6 +1670,12 @@ int ensure(Workspace &w, size_t slots, int grid, int npipes)
     }
     char *b = (char *)w.blob;
     if (hipMemset(b + o_hv, 0, slots) != hipSuccess) return -1; // no history yet
+    if (hipMemset(b + o_px, 0, slots * 4) != hipSuccess) return -1; // no pixel out
+    if (hipMemset(b + o_ctl, 0, 256) != hipSuccess) return -1;
+    w.fin_live = (uint32_t *)(b + o_ctl);
+    w.chk = (RtF4 *)(b + o_chk);
+    w.chk_ctr = (uint32_t *)(b + o_ctl + 64);
+    w.chain_open = false;
     for (int i = 0; i < WF_MAX_PIPES; ++i) {
         WfState &st = w.pipe[i].st;
         st.passes_left = (int *)(b + o_pl);
@@ -1538,16 +1697,23 @@ int ensure(Workspace &w, size_t slots, int grid, int npipes)
         st.counts = (uint32_t *)(b + o_cnt[i]);
         st.spill = i < spill_pipes ? (uint2 *)(b + o_sp[i]) : nullptr;
         st.spill_threads = (int)spill_threads;
-        st.long_flag = (uint32_t *)(b + o_lf);
-        st.long_ray = (RtF4 *)(b + o_lr);
         st.long_ctr = (uint32_t *)(b + o_lc);
+        st.long_ent = (unsigned long long *)(b + o_le);
+        st.long_ray = (RtF4 *)(b + o_lr);
         st.long_depth = 0;
         st.long_cap = (uint32_t)slots;
         st.long_return = 0;
         st.ret_ring = (unsigned long long *)(b + o_rr);
         st.ret_ctr = (uint32_t *)(b + o_rc);
+        st.linger = WF_FIN_LINGER;
+        st.pxo = (uint32_t *)(b + o_px);
+        st.fin_live = nullptr;
         st.heavy = (uint8_t *)(b + o_hv);
         st.heavy_first = 0;
+        st.chk = nullptr; // (whole-call mode only: launch_whole)
+        st.chk_ctr = nullptr;
+        st.chk_mask = 0;
+        st.chk_fault = 0;
     }
     w.slots = slots;
     w.grid = grid;
@@ -1561,17 +1727,260 @@ float elapsed_ms(hipEvent_t a, hipEvent_t b)
     return hipEventElapsedTime(&ms, a, b) == hipSuccess ? ms : 0.0f;
 }
 
+// `stream` waits for every call's device work on this workspace (the
+// pipelines' last launches and every wf_long) — stream NULL: the host does
+int join_all(Workspace &w, hipStream_t stream)
+{
+    for (int pi = 0; pi < WF_MAX_PIPES; ++pi) {
+        Pipe &p = w.pipe[pi];
+        if (p.joined && hipStreamWaitEvent(stream, p.join, 0) != hipSuccess) return -1;
+        if (p.long_rec && hipStreamWaitEvent(stream, p.long_done, 0) != hipSuccess) return -1;
+    }
+    if (w.recorded && hipStreamWaitEvent(stream, w.long_ev, 0) != hipSuccess) return -1;
+    return 0;
+}
+
+int debug_long_log(Workspace &w, unsigned long long *buf);
+
+// The whole call in one persistent finisher (bounded traversal, the default):
+// wf_start seeds every pixel's first ray, wf_finish_bvh runs every pixel to
+// the end of its passes (one path per lane), deep paths go to ONE persistent
+// wf_long beside it, and wf_check re-traces the guard's sample.  Nothing here
+// waits on the host: the call is enqueued and returns.
+//
+// RtOptions.overlap (chained calls): a call of the same frame as the previous
+// overlapping call does not wait for that call's wf_long — pixels still out
+// in it are skipped by wf_start and owed this call's passes (pxo), which the
+// finisher that takes them back (or wf_long itself) runs — and its own
+// wf_long is left running past the call's stream point: rt_join and the
+// library's readers of the frame wait for it.  Results are bit-identical to
+// unchained calls: a pixel's passes run in order whoever runs them.
+int launch_whole(Workspace &w, int dev, const RtDevScene &sc, const RtDevFrame &fr, const RtDevCamera &cam,
+                 hipStream_t stream, int long_depth, bool prof, bool overlap, uint32_t check_mask, int debug)
+{
+    (void)dev;
+    const size_t slots = (size_t)fr.width * fr.height;
+    const int grid = 1536; // every wave slot at the finisher's 6 waves/SIMD (1,536 blocks of 4 waves)
+    if (ensure(w, slots, grid, 1) != 0) return -1;
+    ChainKey key;
+    memset(&key, 0, sizeof key);
+    key.nodes = sc.nodes;
+    key.bvh = sc.bvh_nodes;
+    key.fb = fr.fb;
+    key.sq = fr.sq;
+    key.count = fr.count;
+    key.rng = fr.rng;
+    key.width = fr.width;
+    key.height = fr.height;
+    key.adaptive = fr.adaptive;
+    key.min_samples = fr.min_samples;
+    key.max_depth = fr.max_depth;
+    key.shard_id = fr.shard_id;
+    key.num_shards = fr.num_shards;
+    key.long_depth = long_depth;
+    key.tolerance = fr.tolerance;
+    key.cam = cam;
+    const bool chained = overlap && w.chain_open && !fr.reset && memcmp(&key, &w.key, sizeof key) == 0;
+    Pipe &pp = w.pipe[0];
+    WfState st = pp.st;
+    const int long_return = long_depth > 0 ? 1 : 0;
+    st.long_depth = long_depth;
+    st.long_return = long_return;
+    st.heavy_first = long_return;
+    st.linger = overlap ? 0ull : WF_FIN_LINGER;
+    st.chk_mask = check_mask;
+    st.chk = check_mask == 0xFFFFFFFFu ? nullptr : w.chk;
+    st.chk_ctr = w.chk_ctr;
+    st.chk_fault = (debug & RT_DEBUG_CHECK_FAULT) ? 1 : 0;
+    // debug (RT_DEBUG_LONG_LOG): every deep sample's claim / end time and bounces
+    static unsigned long long *long_log_buf = nullptr;
+    if ((debug & RT_DEBUG_LONG_LOG) && !long_log_buf && hipMalloc((void **)&long_log_buf, 8 * 4 * 65536) != hipSuccess)
+        return -1;
+    st.long_log = (debug & RT_DEBUG_LONG_LOG) ? long_log_buf : nullptr;
+    // the finisher: every wave slot but wf_long's blocks, at most one lane per pixel
+    int fgrid = (int)((slots + WF_BLOCK - 1) / WF_BLOCK);
+    const int fmax = long_return ? grid - WF_LONG_BLOCKS : grid;
+    fgrid = fgrid > fmax ? fmax : fgrid;
+    const uint32_t k = (uint32_t)(w.call_seq % 8);
+    st.fin_live = long_return ? w.fin_live + k : nullptr;
+    if (!chained) {
+        // a fresh call: every earlier call's work on the workspace first, then
+        // the hand-off state from zero (nothing of it is in flight now)
+        if (join_all(w, stream) != 0) return -1;
+        if (long_return) {
+            if (hipMemsetAsync(st.long_ctr, 0, 256, stream) != hipSuccess) return -1;
+            if (hipMemsetAsync(st.long_ent, 0, slots * 8, stream) != hipSuccess) return -1;
+            if (hipMemsetAsync(st.ret_ring, 0, slots * 8, stream) != hipSuccess) return -1;
+            if (hipMemsetAsync(st.ret_ctr, 0, 256, stream) != hipSuccess) return -1;
+        }
+        if (st.long_log && hipMemsetAsync(long_log_buf, 0, 8 * 4 * 65536, stream) != hipSuccess) return -1;
+    }
+    ++w.call_seq;
+    // fork: the pipeline stream starts after the caller's stream
+    const hipStream_t s = pp.stream;
+    if (hipEventRecord(w.fork, stream) != hipSuccess || hipStreamWaitEvent(s, w.fork, 0) != hipSuccess) return -1;
+    if (prof && hipEventRecord(w.ev0, stream) != hipSuccess) return -1;
+    auto mark = [&](int i) { return !prof || hipEventRecord(pp.ev[i], s) == hipSuccess; };
+    if (!mark(0)) return -1;
+    if (hipMemsetAsync(st.counts, 0, 256, s) != hipSuccess) return -1;
+    if (st.fin_live && hipMemsetD32Async((hipDeviceptr_t)st.fin_live, (int)(fgrid * (WF_BLOCK / 64)), 1, s) != hipSuccess)
+        return -1;
+    if (st.chk && hipMemsetAsync(st.chk_ctr, 0, 4, s) != hipSuccess) return -1;
+    const int tiles = ((fr.width + 15) / 16) * ((fr.height + 15) / 16);
+    hipLaunchKernelGGL(wf_start<false>, dim3(tiles), dim3(WF_BLOCK), 0, s, fr, cam, st, 0, 1);
+    if (!mark(1) || !mark(2)) return -1;
+    if (hipEventRecord(w.fin_ready, s) != hipSuccess) return -1;
+    // (the finisher is launched before its wf_long: on a shared hardware queue
+    // it then completes first, and wf_long finds its producers done)
+    hipLaunchKernelGGL(wf_finish_bvh<false>, dim3(fgrid), dim3(WF_BLOCK), 0, s, sc, fr, cam, st, 0);
+    if (hipGetLastError() != hipSuccess || !mark(3)) return -1;
+    Pipe *lp = nullptr;
+    if (long_return) {
+        lp = &w.pipe[1 + (int)(w.call_seq & 1)];
+        if (hipStreamWaitEvent(lp->stream, w.fin_ready, 0) != hipSuccess) return -1;
+        hipLaunchKernelGGL(wf_long<false>, dim3(WF_LONG_BLOCKS), dim3(WF_BLOCK), 0, lp->stream, sc, fr, cam, st, 1);
+        if (hipGetLastError() != hipSuccess) return -1;
+        if (hipEventRecord(lp->long_done, lp->stream) != hipSuccess) return -1;
+        lp->long_rec = true;
+    }
+    if (st.chk) {
+        hipLaunchKernelGGL(wf_check, dim3(grid), dim3(WF_BLOCK), 0, s, sc, st, fr.dev_stats);
+        if (hipGetLastError() != hipSuccess) return -1;
+    }
+    if (!mark(4)) return -1;
+    if (hipEventRecord(pp.join, s) != hipSuccess) return -1;
+    pp.joined = true;
+    // join: the caller's stream continues after the finisher — and, unless the
+    // call overlaps the next one, after its wf_long
+    if (hipStreamWaitEvent(stream, pp.join, 0) != hipSuccess) return -1;
+    if (!overlap && lp && hipStreamWaitEvent(stream, lp->long_done, 0) != hipSuccess) return -1;
+    w.chain_open = overlap;
+    w.key = key;
+    if (prof) {
+        if (hipEventRecord(w.ev1, stream) != hipSuccess || hipEventSynchronize(pp.ev[4]) != hipSuccess ||
+            hipEventSynchronize(w.ev1) != hipSuccess)
+            return -1;
+        RtProfile P{};
+        P.iterations = 0;
+        P.finish_launches = 1;
+        P.start_ms = elapsed_ms(pp.ev[0], pp.ev[1]);
+        P.finish_ms = elapsed_ms(pp.ev[2], pp.ev[3]);
+        P.call_ms = elapsed_ms(w.ev0, w.ev1);
+        P.pipelines = 1;
+        w.prof = P;
+    }
+    if (debug & RT_DEBUG_CALL_LOG) {
+        (void)hipStreamSynchronize(s);
+        timespec ts;
+        clock_gettime(CLOCK_MONOTONIC, &ts);
+        uint32_t lc[4] = {}, rc4[5] = {};
+        (void)hipMemcpy(lc, st.long_ctr, sizeof lc, hipMemcpyDeviceToHost);
+        (void)hipMemcpy(rc4, st.ret_ctr, sizeof rc4, hipMemcpyDeviceToHost);
+        fprintf(stderr,
+                "[wf] call %llu%s finisher done t %.4f; long entries %u claimed %u running %u; returns reserved %u "
+                "claimed %u, finisher waves alive %u, pixels out %u\n",
+                w.call_seq, chained ? " (chained)" : "", ts.tv_sec + ts.tv_nsec * 1e-9, lc[0], lc[1], lc[3], rc4[0],
+                rc4[2], rc4[1], rc4[3]);
+    }
+    if (st.long_log && !overlap) return debug_long_log(w, long_log_buf);
+    return 0;
+}
+
+int debug_long_log(Workspace &w, unsigned long long *buf)
+{
+    (void)w;
+    (void)hipDeviceSynchronize();
+    std::vector<unsigned long long> L(4 * 65536);
+    (void)hipMemcpy(L.data(), buf, 8 * L.size(), hipMemcpyDeviceToHost);
+    struct Rec { double start, end; unsigned long long bounces, slot; };
+    std::vector<Rec> v;
+    double last = 0;
+    for (size_t e = 1; e < 65536; ++e)
+        if (L[4 * e + 1]) {
+            v.push_back({(L[4 * e] - L[0]) * 1e-5, (L[4 * e + 1] - L[0]) * 1e-5, L[4 * e + 2], L[4 * e + 3]});
+            last = std::max(last, v.back().end);
+        }
+    std::sort(v.begin(), v.end(), [](const Rec &a, const Rec &b) { return a.end > b.end; });
+    fprintf(stderr, "[wf long log] %zu deep samples, last end %.1f ms; latest 12 (start ms, end ms, bounces, us/bounce, slot):\n",
+            v.size(), last);
+    for (size_t i = 0; i < v.size() && i < 12; ++i)
+        fprintf(stderr, "  %.1f %.1f %llu %.2f %llu\n", v[i].start, v[i].end, v[i].bounces,
+                (v[i].end - v[i].start) * 1e3 / (double)(v[i].bounces ? v[i].bounces : 1), v[i].slot);
+    std::sort(v.begin(), v.end(), [](const Rec &a, const Rec &b) { return a.bounces > b.bounces; });
+    fprintf(stderr, "[wf long log] longest 8:\n");
+    for (size_t i = 0; i < v.size() && i < 8; ++i)
+        fprintf(stderr, "  %.1f %.1f %llu %.2f %llu\n", v[i].start, v[i].end, v[i].bounces,
+                (v[i].end - v[i].start) * 1e3 / (double)(v[i].bounces ? v[i].bounces : 1), v[i].slot);
+    return 0;
+}
+
 } // namespace
 
-// rt_set_device: the default pipelines' streams (and the CU-partitioned ones
-// of the whole-call mode) take their hardware queues before anything else in
-// the process (RCCL's streams in a multi-GPU run)
+// rt_set_device: the default pipelines' streams take their hardware queues
+// before anything else in the process (RCCL's streams in a multi-GPU run)
 int rt_wavefront_device_init()
 {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return -1;
-    if (ensure_streams(g_ws[dev], WF_PIPES_DEFAULT) != 0) return -1;
-    return long_cus() > 0 ? ensure_partition(g_ws[dev], long_cus()) : 0;
+    rt_register_shutdown();
+    return ensure_streams(workspace(dev), WF_PIPES_DEFAULT);
+}
+
+// rt_join: `stream` (NULL: the host) waits for every rt_render's device work
+// on the current device, chained calls' deep-path tails included
+int rt_wavefront_join(void *stream)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return -1;
+    Workspace *w = nullptr;
+    {
+        std::lock_guard<std::mutex> g(g_ws_mu);
+        auto it = g_ws.find(dev);
+        if (it == g_ws.end() || !it->second) return 0;
+        w = it->second;
+    }
+    if (!stream) {
+        for (int pi = 0; pi < WF_MAX_PIPES; ++pi) {
+            Pipe &p = w->pipe[pi];
+            if (p.joined && hipEventSynchronize(p.join) != hipSuccess) return -1;
+            if (p.long_rec && hipEventSynchronize(p.long_done) != hipSuccess) return -1;
+        }
+        if (w->recorded && hipEventSynchronize(w->long_ev) != hipSuccess) return -1;
+        return 0;
+    }
+    return join_all(*w, (hipStream_t)stream);
+}
+
+// rt_shutdown: every stream, event and device blob of every device's
+// workspace, in reverse creation order, after the device work is done
+void rt_wavefront_shutdown()
+{
+    std::lock_guard<std::mutex> g(g_ws_mu);
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    for (auto &kv : g_ws) {
+        Workspace *w = kv.second;
+        if (!w) continue;
+        if (hipSetDevice(kv.first) != hipSuccess) continue;
+        (void)hipDeviceSynchronize();
+        if (w->blob) (void)hipFree(w->blob);
+        for (int i = WF_MAX_PIPES - 1; i >= 0; --i) {
+            Pipe &p = w->pipe[i];
+            for (auto &e : p.ev)
+                if (e) (void)hipEventDestroy(e);
+            if (p.long_done) (void)hipEventDestroy(p.long_done);
+            if (p.fin_done) (void)hipEventDestroy(p.fin_done);
+            if (p.join) (void)hipEventDestroy(p.join);
+            if (p.host_count) (void)hipHostFree(p.host_count);
+            if (p.stream) (void)hipStreamDestroy(p.stream);
+        }
+        for (hipEvent_t e : {w->ev1, w->ev0, w->long_ev, w->fin_ready, w->fork})
+            if (e) (void)hipEventDestroy(e);
+        delete w;
+        kv.second = nullptr;
+    }
+    g_ws.clear();
+    (void)hipSetDevice(cur);
 }
 
 extern "C" int rt_last_profile(RtProfile *out)
@@ -1579,67 +1988,71 @@ extern "C" int rt_last_profile(RtProfile *out)
     if (!out) return RT_E_INVALID;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return RT_E_HIP;
+    std::lock_guard<std::mutex> g(g_ws_mu);
     auto it = g_ws.find(dev);
-    *out = it == g_ws.end() ? RtProfile{} : it->second.prof;
+    *out = it == g_ws.end() || !it->second ? RtProfile{} : it->second->prof;
     return RT_OK;
 }
 
 int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevCamera &cam, hipStream_t stream,
                         int variant, int tail_opt, int finish_waves_opt, int profile, int cap_opt, int postpone_opt,
-                        int wide_opt, int pipes_opt, int long_opt, int traversal)
+                        int wide_opt, int pipes_opt, int long_opt, int traversal, int overlap, int check_interval,
+                        int debug)
 {
     // 1: wave-cooperative leaves (entries packed as k << 6 | lane: needs < 2^26 entries), 2: static, 3: per-lane fetch
     int trace_kind = variant;
     if (trace_kind == 1 && sc.index_count >= (1 << 26)) trace_kind = 3;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return -1;
-    Workspace &w = g_ws[dev];
+    Workspace &w = workspace(dev);
+    rt_register_shutdown();
     const size_t slots = (size_t)fr.width * fr.height;
     const bool count = fr.counters != nullptr;
     // the queue trace launches run the BVH-bounded traversal (counting calls: the KD one, whose counters are the reference's)
     const bool bounded = sc.bvh_nodes != nullptr && ((traversal == RT_TRAVERSAL_BOUNDED && !count) ||
                                                      traversal == RT_TRAVERSAL_BOUNDED_COUNTED);
-    // ... and the tail finisher too (RT_WF_FIN_BVH=0: the cooperative KD finisher; experiments)
-    static const bool fin_bvh = !getenv("RT_WF_FIN_BVH") || atoi(getenv("RT_WF_FIN_BVH")) != 0;
-    // bounded traversal: the whole call in the finisher by default — one path
-    // per lane to the end of its passes beats queue iterations once a ray
-    // query is ~30 dependent loads: 1.22 vs 1.61 s per 256-pass room2m call
-    // with deep paths cut (profiles/r03).  It runs as ONE pipeline whose
+    // paths deeper than this leave their pipeline for wf_long (cooperative trace only)
+    const int long_depth = trace_kind == 1 && long_opt >= 0 ? (long_opt > 0 ? long_opt : WF_LONG_DEPTH_DEFAULT) : 0;
+    // bounded traversal, not counting: the whole call in the finisher by default
+    // — one path per lane to the end of its passes beats queue iterations once
+    // a ray query is ~30 dependent loads: 1.22 vs 1.61 s per 256-pass room2m
+    // call with deep paths cut (profiles/r03).  It runs as ONE pipeline whose
     // finisher spans the chip: three pipelines' fixed pixel sets finished up
     // to 0.7 s apart, each leaving its third of the chip idle.
-    const bool whole = bounded && fin_bvh && trace_kind == 1 && (tail_opt <= 0 || (size_t)tail_opt > slots);
-    // persistent-ish grid for trace/shade (grid-stride over the queue); RT_WF_GRID overrides (experiments)
-    static const int grid_env = getenv("RT_WF_GRID") ? atoi(getenv("RT_WF_GRID")) : 0;
-    // 512 blocks = 2,048 waves = a third of the chip's 6,144 wave slots at the
+    const bool whole = bounded && !count && trace_kind == 1 && (tail_opt <= 0 || (size_t)tail_opt > slots);
+    if (whole) {
+        // the run-time exactness guard: 1 ray in check_interval (a power of two) re-traced by the KD traversal
+        uint32_t mask = 0xFFFFFFFFu;
+        if (check_interval >= 0) {
+            uint32_t iv = check_interval > 0 ? (uint32_t)check_interval : WF_CHECK_INTERVAL_DEFAULT;
+            uint32_t p2 = 1;
+            while (p2 < iv && p2 < (1u << 30)) p2 <<= 1;
+            mask = p2 - 1;
+        }
+        return launch_whole(w, dev, sc, fr, cam, stream, long_depth, profile != 0, overlap != 0, mask, debug);
+    }
+    // persistent-ish grid for trace/shade (grid-stride over the queue).  512
+    // blocks = 2,048 waves = a third of the chip's 6,144 wave slots at the
     // trace kernel's 6 waves/SIMD: the 3 pipelines' launches share the chip,
     // and a launch's ~465k rays are ~3.5 per lane, so the lanes stay busy past
     // the launch's first round of rays (1,536 blocks: ~1.2 rays per lane, most
     // of the launch was its tail).  Measured 512 / 704 / 1,536: 37.5 / 37.6 /
     // 33.1 Msamples/s on room2m 1080p (tools/gpu_sweep.sh, profiles/r02).
-    // The whole-call finisher: 1,536 blocks = every slot at 6 waves/SIMD.
-    const int grid = grid_env >= 64 && grid_env <= 16384 ? grid_env : (whole ? 1536 : 512);
+    const int grid = 512;
     const int tgrid = grid * (WF_BLOCK / WF_TBLOCK); // the same waves in WF_TBLOCK-thread blocks
     // wf_shade: half the trace grid (~2 paths per lane per launch).  Measured
     // per 256-pass room2m call (2 rounds each): 64 / 128 / 256 / 384 / 512 /
     // 1,024 / 2,048 blocks: 13.27 / 12.82 / 12.78 / 12.78 / 12.87 / 13.01 /
-    // 13.21 s.  RT_WF_SHADE_GRID overrides (experiments)
-    static const int sgrid_env = getenv("RT_WF_SHADE_GRID") ? atoi(getenv("RT_WF_SHADE_GRID")) : 0;
-    const int sgrid = sgrid_env >= 16 && sgrid_env <= 16384 ? sgrid_env : (tgrid / 2 > 16 ? tgrid / 2 : 16);
+    // 13.21 s
+    const int sgrid = tgrid / 2 > 16 ? tgrid / 2 : 16;
     const bool prof = profile != 0;
-    // wf_long: RT_WF_LONG_UNI=1 runs the bounded traversal wave-uniformly (every lane on the path's ray,
-    // scalar node loads) instead of the 64-lane wide KD traversal — experiments: per bounce no faster on
-    // the light guide (9.5 us either way: a lone path is bound by its dependent instruction chain, not by
-    // load latency) and 25 % slower per room2m call (profiles/r03/deep_paths.md)
-    static const bool long_uni = getenv("RT_WF_LONG_UNI") && atoi(getenv("RT_WF_LONG_UNI")) != 0;
-    // (RT_WF_HEAVY_FIRST=0: the whole-call finisher takes pixels in tile order only; experiments)
-    static const bool heavy_first_opt = !getenv("RT_WF_HEAVY_FIRST") || atoi(getenv("RT_WF_HEAVY_FIRST")) != 0;
     const int tiles = ((fr.width + 15) / 16) * ((fr.height + 15) / 16);
-    int npipes = pipes_opt > 0 ? pipes_opt : (whole ? 1 : WF_PIPES_DEFAULT);
+    int npipes = pipes_opt > 0 ? pipes_opt : WF_PIPES_DEFAULT;
     npipes = npipes > WF_MAX_PIPES ? WF_MAX_PIPES : npipes;
     npipes = npipes > tiles ? tiles : npipes;
     if (ensure(w, slots, grid, npipes) != 0) return -1;
     // below this many live paths the rest of the call runs in one finisher launch
-    const uint32_t tail = whole ? (uint32_t)slots + 1u : tail_opt > 0 ? (uint32_t)tail_opt : WF_TAIL_DEFAULT;
+    const uint32_t tail = tail_opt > 0 ? (uint32_t)tail_opt : WF_TAIL_DEFAULT;
     // the cooperative finisher runs on at most this many waves (up to 64 paths in flight each)
     // (small trees: rays are short, so more paths per finisher wave keep its
     // cooperative rounds full — the 36-triangle Cornell box at 256x256 runs
@@ -1659,52 +2072,30 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
     // cheaper, and only a lone ray goes wide.  Measured: room2m / cornell_blob
     // finisher time -18 % / -30 % at 32, the Cornell box 2x slower)
     const int wide = sc.index_count >= WF_FIN_WIDE_MIN_ENTRIES ? wide_lanes : (wide_lanes > 0 ? 1 : 0);
-    static const bool trace_iters = getenv("RT_WF_TRACE_ITERS") != nullptr; // debug: per-iteration queue sizes
-    // paths deeper than this leave their pipeline for wf_long (cooperative trace only)
-    const int long_depth = trace_kind == 1 && long_opt >= 0 ? (long_opt > 0 ? long_opt : WF_LONG_DEPTH_DEFAULT) : 0;
-    for (int pi = 0; pi < WF_MAX_PIPES; ++pi) w.pipe[pi].st.long_depth = long_depth;
-    const WfState &lst = w.pipe[0].st;
-    // in the whole-call mode wf_long runs on long_cus() CUs of its own and the finisher on the
-    // others (streams created by rt_set_device): a deep path's bounces do not wait behind the
-    // bulk's waves on its CU
-    if (whole && long_depth > 0 && long_cus() > 0 && ensure_partition(w, long_cus()) != 0) return -1;
-    const bool part = whole && long_depth > 0 && w.long_stream != nullptr;
-    // RT_WF_LONG_LOG=1 (debug): log every deep sample's claim / end time and bounces, printed after the call
-    static const bool long_log = getenv("RT_WF_LONG_LOG") != nullptr;
-    static unsigned long long *long_log_buf = nullptr;
-    if (long_log && !long_log_buf && hipMalloc((void **)&long_log_buf, 8 * 4 * 65536) != hipSuccess) return -1;
-    for (int pi = 0; pi < WF_MAX_PIPES; ++pi) w.pipe[pi].st.long_log = long_log ? long_log_buf : nullptr;
-    if (long_log && hipMemsetAsync(long_log_buf, 0, 8 * 4 * 65536, stream) != hipSuccess) return -1;
-    hipStream_t const lstream = part ? w.long_stream : stream; // wf_long's slices
+    const bool trace_iters = (debug & RT_DEBUG_CALL_LOG) != 0; // per-iteration queue sizes
+    for (int pi = 0; pi < WF_MAX_PIPES; ++pi) {
+        WfState &st = w.pipe[pi].st;
+        st.long_depth = long_depth;
+        st.long_return = 0;
+        st.heavy_first = 0;
+        st.fin_live = nullptr;
+        st.long_log = nullptr;
+    }
+    const WfState lst = w.pipe[0].st;
 
     // the workspace (per-pixel path state, long-path hand-off) is shared by every
-    // call on this device: a call on another stream than the previous one must
-    // not start before that call's last wf_long slice and pipelines are done
-    // (every pipeline the previous call used, whatever this call's pipeline
-    // count: pixels may move to another pipeline while the previous call's
-    // finisher still writes their path state; the wf_long wait only if a
-    // slice was ever launched)
-    if (w.recorded && hipStreamWaitEvent(stream, w.long_ev, 0) != hipSuccess) return -1;
-    for (int pi = 0; pi < WF_MAX_PIPES; ++pi)
-        if (w.pipe[pi].joined && hipStreamWaitEvent(stream, w.pipe[pi].join, 0) != hipSuccess) return -1;
-    // the whole call in the bounded finisher: wf_long returns pixels after their deep sample
-    const int long_return = long_depth > 0 && bounded && fin_bvh && trace_kind == 1 && tail > slots ? 1 : 0;
-    for (int pi = 0; pi < WF_MAX_PIPES; ++pi) {
-        w.pipe[pi].st.long_return = long_return;
-        w.pipe[pi].st.heavy_first = long_return && heavy_first_opt;
-    }
+    // call on this device: a call must not start before every earlier call's
+    // pipelines and wf_long work are done (pixels may move to another pipeline
+    // while the previous call's finisher still writes their path state)
+    if (join_all(w, stream) != 0) return -1;
+    w.chain_open = false;
     if (long_depth > 0) {
-        // (every entry of the arrays: in return mode a pixel may be handed over more than once per call)
-        if (hipMemsetAsync(lst.long_flag, 0, (size_t)lst.long_cap * 4, stream) != hipSuccess) return -1;
+        // (the ring from zero: a pixel is handed over at most once per call here)
+        if (hipMemsetAsync(lst.long_ent, 0, slots * 8, stream) != hipSuccess) return -1;
         if (hipMemsetAsync(lst.long_ctr, 0, 256, stream) != hipSuccess) return -1;
-    }
-    if (long_return) {
-        if (hipMemsetAsync(lst.ret_ring, 0, (size_t)lst.long_cap * 8, stream) != hipSuccess) return -1;
-        if (hipMemsetAsync(lst.ret_ctr, 0, 256, stream) != hipSuccess) return -1;
     }
     // fork: every pipeline stream starts after the caller's stream
     if (hipEventRecord(w.fork, stream) != hipSuccess) return -1;
-    if (part && hipStreamWaitEvent(lstream, w.fork, 0) != hipSuccess) return -1;
     if (prof && hipEventRecord(w.ev0, stream) != hipSuccess) return -1;
     std::mutex long_mu;
     bool long_final = false;
@@ -1722,14 +2113,13 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
         }
         const int fin = final ? 1 : 0;
         if (count)
-            hipLaunchKernelGGL(wf_long<true>, dim3(WF_LONG_BLOCKS), dim3(WF_BLOCK), 0, lstream, sc, fr, cam, lst, fin, 0);
+            hipLaunchKernelGGL(wf_long<true>, dim3(WF_LONG_BLOCKS), dim3(WF_BLOCK), 0, stream, sc, fr, cam, lst, fin);
         else
-            hipLaunchKernelGGL(wf_long<false>, dim3(WF_LONG_BLOCKS), dim3(WF_BLOCK), 0, lstream, sc, fr, cam, lst, fin,
-                               !bounded ? 0 : long_uni ? 1 : sc.bvh8 ? 2 : 0);
+            hipLaunchKernelGGL(wf_long<false>, dim3(WF_LONG_BLOCKS), dim3(WF_BLOCK), 0, stream, sc, fr, cam, lst, fin);
         if (hipGetLastError() != hipSuccess) return -1;
         long_final = final;
         ++n_slices;
-        if (hipEventRecord(w.long_ev, lstream) != hipSuccess) return -1;
+        if (hipEventRecord(w.long_ev, stream) != hipSuccess) return -1;
         w.recorded = true;
         return 0;
     };
@@ -1750,7 +2140,7 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
         Pipe &pp = w.pipe[pi];
         pp.trace_iv.clear();
         WfState &st = pp.st;
-        hipStream_t s = part && pi == 0 ? w.fin_stream : pp.stream;
+        hipStream_t s = pp.stream;
         if (hipStreamWaitEvent(s, w.fork, 0) != hipSuccess) return -1;
         RtProfile P{};
         auto mark = [&](int i) { return !prof || hipEventRecord(pp.ev[i], s) == hipSuccess; };
@@ -1762,18 +2152,10 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
         // run the `live` paths of queue qq to the end of the call in the finisher
         auto finish = [&](int qq, uint32_t live) -> int {
             if (!mark(2)) return -1;
-            if (bounded && fin_bvh) {
-                // one path per lane (lanes refill from the list), within the spill area (grid blocks),
-                // leaving the wf_long slices their blocks: the pipelines' finishers together would
-                // otherwise hold every wave slot until they end, and the deep paths they hand over
-                // would start only then
+            if (bounded) {
+                // one path per lane (lanes refill from the list), within the spill area (grid blocks)
                 int fgrid = (int)((live + WF_BLOCK - 1) / WF_BLOCK);
-                int fmax = long_depth > 0 ? grid - (WF_LONG_BLOCKS + npipes - 1) / npipes : grid;
-                if (part) { // the finisher's CUs at its occupancy (every block resident)
-                    const int pmax = (w.total_cus - w.long_cus) * 4 * WF_FIN_BVH_WAVES / (WF_BLOCK / 64);
-                    fmax = pmax < grid ? pmax : grid;
-                }
-                fgrid = fgrid > fmax ? fmax : fgrid;
+                fgrid = fgrid > grid ? grid : fgrid;
                 if (hipMemsetAsync(st.counts + 4, 0, 4, s) != hipSuccess) return -1;
                 if (count) hipLaunchKernelGGL(wf_finish_bvh<true>, dim3(fgrid), dim3(WF_BLOCK), 0, s, sc, fr, cam, st, qq);
                 else hipLaunchKernelGGL(wf_finish_bvh<false>, dim3(fgrid), dim3(WF_BLOCK), 0, s, sc, fr, cam, st, qq);
@@ -1810,7 +2192,7 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
         // is a producer until the finisher is done (meanwhile wf_long slices are
         // kicked as they end; the last producer queues the final slice)
         auto finish_and_release = [&](int qq, uint32_t live) -> int {
-            const bool publishes = bounded && fin_bvh && long_depth > 0;
+            const bool publishes = bounded && long_depth > 0;
             if (!publishes && producer_done(pi) != 0) return -1;
             if (finish(qq, live) != 0) return -1;
             if (!publishes) return 0;
@@ -1822,81 +2204,65 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
                 if (kick_long(false) != 0) return -1;
                 std::this_thread::sleep_for(std::chrono::microseconds(200));
             }
+            return producer_done(pi);
+        };
+        for (int it = 0;; ++it) {
+            const int q = it & 1;
+            if (hipMemsetAsync(st.counts + (q ^ 1), 0, 4, s) != hipSuccess) return -1;     // next ray queue
+            if (hipMemsetAsync(st.counts + 6 + (q ^ 1), 0, 4, s) != hipSuccess) return -1; // next path list
+            if (hipMemsetAsync(st.counts + 2 + q, 0, 4, s) != hipSuccess) return -1; // fetch cursor
+            if (!mark(4)) return -1;
+            if (bounded) {
+                if (count)
+                    hipLaunchKernelGGL(wf_trace_bvh<true>, dim3(grid), dim3(WF_BLOCK), 0, s, sc, st, q, fr.counters);
+                else
+                    hipLaunchKernelGGL(wf_trace_bvh<false>, dim3(grid), dim3(WF_BLOCK), 0, s, sc, st, q, nullptr);
+            } else if (trace_kind == 1) {
+                const int li = it * npipes + pi;
+                unsigned long long *tl = fr.wave_times && li < WF_TIMELINE_LAUNCHES ? fr.wave_times + 3 * li : nullptr;
+                if (count)
+                    hipLaunchKernelGGL(wf_trace_coop<true>, dim3(tgrid), dim3(WF_TBLOCK), 0, s, sc, st, q,
+                                       fr.counters, cap, postpone, wide_lanes, tl);
+                else
+                    hipLaunchKernelGGL(wf_trace_coop<false>, dim3(tgrid), dim3(WF_TBLOCK), 0, s, sc, st, q,
+                                       fr.counters, cap, postpone, wide_lanes, tl);
+            } else if (trace_kind == 3) {
+                if (count) hipLaunchKernelGGL(wf_trace_dyn<true>, dim3(grid), dim3(WF_BLOCK), 0, s, sc, st, q, fr.counters);
+                else hipLaunchKernelGGL(wf_trace_dyn<false>, dim3(grid), dim3(WF_BLOCK), 0, s, sc, st, q, fr.counters);
+            } else {
+                if (count) hipLaunchKernelGGL(wf_trace<true>, dim3(grid), dim3(WF_BLOCK), 0, s, sc, st, q, fr.counters);
+                else hipLaunchKernelGGL(wf_trace<false>, dim3(grid), dim3(WF_BLOCK), 0, s, sc, st, q, fr.counters);
+            }
+            if (!mark(5)) return -1;
+            if (count) hipLaunchKernelGGL(wf_shade<true>, dim3(sgrid), dim3(WF_TBLOCK), 0, s, sc, fr, cam, st, q);
+            else hipLaunchKernelGGL(wf_shade<false>, dim3(sgrid), dim3(WF_TBLOCK), 0, s, sc, fr, cam, st, q);
+            if (hipGetLastError() != hipSuccess) return -1;
+            if (!mark(2)) return -1;
+            if (hipMemcpyAsync(pp.host_count, st.counts, 32, hipMemcpyDeviceToHost, s) != hipSuccess)
+                return -1;
+            if (hipStreamSynchronize(s) != hipSuccess) return -1;
+            const uint32_t live = pp.host_count[6 + (q ^ 1)]; // paths with rays in the next queue
+            P.iterations = it + 1;
+            if (prof) {
+                P.trace_ms += elapsed_ms(pp.ev[4], pp.ev[5]);
+                P.shade_ms += elapsed_ms(pp.ev[5], pp.ev[2]);
+                pp.trace_iv.emplace_back(elapsed_ms(w.ev0, pp.ev[4]), elapsed_ms(w.ev0, pp.ev[5]));
+            }
             if (trace_iters) {
                 timespec ts;
                 clock_gettime(CLOCK_MONOTONIC, &ts);
-                fprintf(stderr, "[wf] pipe %d finisher done t %.4f\n", pi, ts.tv_sec + ts.tv_nsec * 1e-9);
+                fprintf(stderr, "[wf] pipe %d it %d live %u t %.4f\n", pi, it, live, ts.tv_sec + ts.tv_nsec * 1e-9);
             }
-            return producer_done(pi);
-        };
-        if (trace_kind == 1 && tail > slots) {
-            // wf_tail above the frame size: the whole call runs in the finisher (no queue iterations)
-            rc = finish_and_release(0, (uint32_t)slots);
-        } else {
-            for (int it = 0;; ++it) {
-                const int q = it & 1;
-                if (hipMemsetAsync(st.counts + (q ^ 1), 0, 4, s) != hipSuccess) return -1;     // next ray queue
-                if (hipMemsetAsync(st.counts + 6 + (q ^ 1), 0, 4, s) != hipSuccess) return -1; // next path list
-                if (hipMemsetAsync(st.counts + 2 + q, 0, 4, s) != hipSuccess) return -1; // fetch cursor
-                if (!mark(4)) return -1;
-                if (bounded) {
-                    if (count)
-                        hipLaunchKernelGGL(wf_trace_bvh<true>, dim3(grid), dim3(WF_BLOCK), 0, s, sc, st, q, fr.counters);
-                    else
-                        hipLaunchKernelGGL(wf_trace_bvh<false>, dim3(grid), dim3(WF_BLOCK), 0, s, sc, st, q, nullptr);
-                } else if (trace_kind == 1) {
-                    const int li = it * npipes + pi;
-                    unsigned long long *tl = fr.wave_times && li < WF_TIMELINE_LAUNCHES ? fr.wave_times + 3 * li : nullptr;
-                    if (count)
-                        hipLaunchKernelGGL(wf_trace_coop<true>, dim3(tgrid), dim3(WF_TBLOCK), 0, s, sc, st, q,
-                                           fr.counters, cap, postpone, wide_lanes, tl);
-                    else
-                        hipLaunchKernelGGL(wf_trace_coop<false>, dim3(tgrid), dim3(WF_TBLOCK), 0, s, sc, st, q,
-                                           fr.counters, cap, postpone, wide_lanes, tl);
-                } else if (trace_kind == 3) {
-                    if (count) hipLaunchKernelGGL(wf_trace_dyn<true>, dim3(grid), dim3(WF_BLOCK), 0, s, sc, st, q, fr.counters);
-                    else hipLaunchKernelGGL(wf_trace_dyn<false>, dim3(grid), dim3(WF_BLOCK), 0, s, sc, st, q, fr.counters);
-                } else {
-                    if (count) hipLaunchKernelGGL(wf_trace<true>, dim3(grid), dim3(WF_BLOCK), 0, s, sc, st, q, fr.counters);
-                    else hipLaunchKernelGGL(wf_trace<false>, dim3(grid), dim3(WF_BLOCK), 0, s, sc, st, q, fr.counters);
-                }
-                if (!mark(5)) return -1;
-                if (count) hipLaunchKernelGGL(wf_shade<true>, dim3(sgrid), dim3(WF_TBLOCK), 0, s, sc, fr, cam, st, q);
-                else hipLaunchKernelGGL(wf_shade<false>, dim3(sgrid), dim3(WF_TBLOCK), 0, s, sc, fr, cam, st, q);
-                if (hipGetLastError() != hipSuccess) return -1;
-                if (!mark(2)) return -1;
-                if (hipMemcpyAsync(pp.host_count, st.counts, 32, hipMemcpyDeviceToHost, s) != hipSuccess)
-                    return -1;
-                if (hipStreamSynchronize(s) != hipSuccess) return -1;
-                const uint32_t live = pp.host_count[6 + (q ^ 1)]; // paths with rays in the next queue
-                P.iterations = it + 1;
-                if (prof) {
-                    P.trace_ms += elapsed_ms(pp.ev[4], pp.ev[5]);
-                    P.shade_ms += elapsed_ms(pp.ev[5], pp.ev[2]);
-                    pp.trace_iv.emplace_back(elapsed_ms(w.ev0, pp.ev[4]), elapsed_ms(w.ev0, pp.ev[5]));
-                }
-                if (trace_iters) {
-                    timespec ts;
-                    clock_gettime(CLOCK_MONOTONIC, &ts);
-                    fprintf(stderr, "[wf] pipe %d it %d live %u t %.4f\n", pi, it, live, ts.tv_sec + ts.tv_nsec * 1e-9);
-                }
-                if (kick_long(false) != 0) return -1; // paths published by this shade launch
-                if (live == 0 || live < tail) {
-                    if (live != 0) rc = finish_and_release(q ^ 1, live);
-                    else if (producer_done(pi) != 0) return -1;
-                    break;
-                }
+            if (kick_long(false) != 0) return -1; // paths published by this shade launch
+            if (live == 0 || live < tail) {
+                if (live != 0) rc = finish_and_release(q ^ 1, live);
+                else if (producer_done(pi) != 0) return -1;
+                break;
             }
         }
         if (rc != 0) return rc;
         if (hipEventRecord(pp.join, s) != hipSuccess) return -1;
         pp.joined = true;
-        if (trace_iters) {
-            (void)hipStreamSynchronize(s);
-            timespec ts;
-            clock_gettime(CLOCK_MONOTONIC, &ts);
-            fprintf(stderr, "[wf] pipe %d finished t %.4f\n", pi, ts.tv_sec + ts.tv_nsec * 1e-9);
-        }
         if (prof) {
             if (!mark(4) || hipEventSynchronize(pp.ev[4]) != hipSuccess) return -1;
             P.trace_launches = P.shade_launches = P.iterations;
@@ -1915,53 +2281,19 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
     for (int pi = 1; pi < npipes; ++pi) threads[pi].join();
     if (!long_final) (void)kick_long(true); // a pipeline failed early: drain the published paths anyway
     if (trace_iters) {
-        for (int pi = 0; pi < npipes; ++pi) (void)hipStreamSynchronize(w.pipe[pi].stream);
-        timespec ts;
-        clock_gettime(CLOCK_MONOTONIC, &ts);
-        fprintf(stderr, "[wf] pipelines done t %.4f\n", ts.tv_sec + ts.tv_nsec * 1e-9);
-        uint32_t lc[4] = {};
         (void)hipStreamSynchronize(stream);
+        uint32_t lc[4] = {};
         (void)hipMemcpy(lc, lst.long_ctr, sizeof lc, hipMemcpyDeviceToHost);
+        timespec ts;
         clock_gettime(CLOCK_MONOTONIC, &ts);
         fprintf(stderr, "[wf] long paths %u claimed %u running %u; slices %d; caller stream done t %.4f\n", lc[0],
                 lc[1], lc[3], n_slices, ts.tv_sec + ts.tv_nsec * 1e-9);
-        if (long_return) {
-            uint32_t rc4[4] = {};
-            (void)hipMemcpy(rc4, lst.ret_ctr, sizeof rc4, hipMemcpyDeviceToHost);
-            fprintf(stderr, "[wf] returns reserved %u claimed %u, finisher waves alive %u, pixels out %u\n", rc4[0],
-                    rc4[2], rc4[1], rc4[3]);
-        }
-    }
-    if (long_log) {
-        (void)hipDeviceSynchronize();
-        std::vector<unsigned long long> L(4 * 65536);
-        (void)hipMemcpy(L.data(), long_log_buf, 8 * L.size(), hipMemcpyDeviceToHost);
-        struct Rec { double start, end; unsigned long long bounces, slot; };
-        std::vector<Rec> v;
-        double last = 0;
-        for (size_t e = 1; e < 65536; ++e)
-            if (L[4 * e + 1]) {
-                v.push_back({(L[4 * e] - L[0]) * 1e-5, (L[4 * e + 1] - L[0]) * 1e-5, L[4 * e + 2], L[4 * e + 3]});
-                last = std::max(last, v.back().end);
-            }
-        std::sort(v.begin(), v.end(), [](const Rec &a, const Rec &b) { return a.end > b.end; });
-        fprintf(stderr, "[wf long log] %zu deep samples, last end %.1f ms; latest 12 (start ms, end ms, bounces, us/bounce, slot):\n",
-                v.size(), last);
-        for (size_t i = 0; i < v.size() && i < 12; ++i)
-            fprintf(stderr, "  %.1f %.1f %llu %.2f %llu\n", v[i].start, v[i].end, v[i].bounces,
-                    (v[i].end - v[i].start) * 1e3 / (double)(v[i].bounces ? v[i].bounces : 1), v[i].slot);
-        std::sort(v.begin(), v.end(), [](const Rec &a, const Rec &b) { return a.bounces > b.bounces; });
-        fprintf(stderr, "[wf long log] longest 8:\n");
-        for (size_t i = 0; i < v.size() && i < 8; ++i)
-            fprintf(stderr, "  %.1f %.1f %llu %.2f %llu\n", v[i].start, v[i].end, v[i].bounces,
-                    (v[i].end - v[i].start) * 1e3 / (double)(v[i].bounces ? v[i].bounces : 1), v[i].slot);
     }
     for (int pi = 0; pi < npipes; ++pi)
         if (rcs[pi] != 0) return rcs[pi];
-    // join: the caller's stream continues after every pipeline (and wf_long's own stream)
+    // join: the caller's stream continues after every pipeline
     for (int pi = 0; pi < npipes; ++pi)
         if (hipStreamWaitEvent(stream, w.pipe[pi].join, 0) != hipSuccess) return -1;
-    if (part && hipStreamWaitEvent(stream, w.long_ev, 0) != hipSuccess) return -1;
     if (prof) {
         RtProfile P{};
         for (int pi = 0; pi < npipes; ++pi) { // kernel times summed over the (concurrent) pipelines

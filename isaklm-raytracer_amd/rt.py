@@ -56,7 +56,8 @@ class RtOptions(ctypes.Structure):
                 ("wf_tail", ctypes.c_int), ("wf_finish_waves", ctypes.c_int), ("profile", ctypes.c_int),
                 ("wf_descent_cap", ctypes.c_int), ("wf_postpone", ctypes.c_int), ("wf_wide", ctypes.c_int),
                 ("shard_id", ctypes.c_int), ("num_shards", ctypes.c_int), ("wf_pipelines", ctypes.c_int),
-                ("wf_long_depth", ctypes.c_int), ("traversal", ctypes.c_int)]
+                ("wf_long_depth", ctypes.c_int), ("traversal", ctypes.c_int), ("overlap", ctypes.c_int),
+                ("check_interval", ctypes.c_int), ("debug", ctypes.c_int)]
 
 
 class RtProfile(ctypes.Structure):
@@ -79,7 +80,9 @@ DEV_HIST_BINS = 18
 class RtDeviations(ctypes.Structure):
     _fields_ = [("watchdog_paths", ctypes.c_ulonglong), ("cut_paths", ctypes.c_ulonglong),
                 ("max_deep_depth", ctypes.c_ulonglong), ("deep_paths", ctypes.c_ulonglong),
-                ("deep_hist", ctypes.c_ulonglong * DEV_HIST_BINS)]
+                ("deep_hist", ctypes.c_ulonglong * DEV_HIST_BINS),
+                ("bounded_checked", ctypes.c_ulonglong), ("bounded_mismatches", ctypes.c_ulonglong),
+                ("mismatch_ray", ctypes.c_float * 6)]
 
 
 def deviation_stats(reset=False):
@@ -89,10 +92,18 @@ def deviation_stats(reset=False):
     d = RtDeviations()
     check(lib().rt_deviation_stats(ctypes.byref(d), int(reset)))
     return {"watchdog_paths": d.watchdog_paths, "cut_paths": d.cut_paths, "max_deep_depth": d.max_deep_depth,
-            "deep_paths": d.deep_paths, "deep_hist": [int(v) for v in d.deep_hist]}
+            "deep_paths": d.deep_paths, "deep_hist": [int(v) for v in d.deep_hist],
+            "bounded_checked": int(d.bounded_checked), "bounded_mismatches": int(d.bounded_mismatches),
+            "mismatch_ray": [float(v) for v in d.mismatch_ray]}
 
 
-ABI_VERSION = 5  # RT_ABI_VERSION of include/isaklm_rt.h
+def join(stream=None):
+    """rt_join: `stream` (None: the host) waits for every render's device work,
+    chained calls' deep-path tails included."""
+    check(lib().rt_join(stream))
+
+
+ABI_VERSION = 6  # RT_ABI_VERSION of include/isaklm_rt.h
 TRIANGLE_BYTES = 152
 NODE_BYTES = 20
 COUNTER_NAMES = ["node", "tri", "hit", "texel", "nee", "sample", "skip", "ray", "watchdog", "maxdepth"]
@@ -157,6 +168,8 @@ def lib():
         L.rt_tonemap.argtypes = [G_Buffer, vp, i, i, vp]
         L.rt_save_render.argtypes = [G_Buffer, i, i, ctypes.c_char_p]
         L.rt_deviation_stats.argtypes = [ctypes.POINTER(RtDeviations), i]
+        L.rt_join.argtypes = [vp]
+        L.rt_shutdown.restype = None
         L.rt_abi_version.restype = i
         if L.rt_abi_version() != ABI_VERSION:
             raise RtError(f"{LIB_PATH}: ABI version {L.rt_abi_version()}, this binding expects {ABI_VERSION} "
@@ -355,9 +368,11 @@ TRAVERSAL_BOUNDED_COUNTED = 2  # measurement: the bounded queue trace kernel cou
 def options(width, height, passes=1, adaptive=True, min_samples=100, tolerance=0.05, max_depth=0, stream=None,
             counters=None, kernel=KERNEL_MEGA, wf_tail=0, wf_finish_waves=0, profile=False, wf_descent_cap=0,
             wf_postpone=0, wf_wide=0, shard_id=0, num_shards=1, wave_times=None, wf_pipelines=0, wf_long_depth=0,
-            traversal=None):
+            traversal=None, overlap=False, check_interval=0, debug=0):
     """RtOptions; traversal: TRAVERSAL_BOUNDED / TRAVERSAL_KD (None: the
-    library default, or RT_TRAVERSAL from the environment)."""
+    library default, or RT_TRAVERSAL from the environment); overlap: chained
+    calls (RtOptions.overlap: join before reading the frame); check_interval:
+    the bounded traversal's run-time guard (0: 1 ray in 1024, < 0: off)."""
     o = RtOptions()
     lib().rt_default_options(ctypes.byref(o))
     o.width, o.height, o.passes = width, height, passes
@@ -371,6 +386,7 @@ def options(width, height, passes=1, adaptive=True, min_samples=100, tolerance=0
     o.wave_times_device = wave_times
     o.wf_pipelines = wf_pipelines
     o.wf_long_depth = wf_long_depth
+    o.overlap, o.check_interval, o.debug = int(overlap), check_interval, debug
     if traversal is None and os.environ.get("RT_TRAVERSAL"):
         traversal = {"bounded": TRAVERSAL_BOUNDED, "kd": TRAVERSAL_KD,
                      "bounded_counted": TRAVERSAL_BOUNDED_COUNTED}[os.environ["RT_TRAVERSAL"]]

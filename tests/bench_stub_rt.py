@@ -146,7 +146,8 @@ class DeviceCounters:
 
 
 def deviation_stats(reset=False):
-    return {"watchdog_paths": 0, "cut_paths": 0, "max_deep_depth": 0, "deep_paths": 0, "deep_hist": [0] * 18}
+    return {"watchdog_paths": 0, "cut_paths": 0, "max_deep_depth": 0, "deep_paths": 0, "deep_hist": [0] * 18,
+            "bounded_checked": 0, "bounded_mismatches": 0, "mismatch_ray": [0.0] * 6}
 
 
 class Comm:

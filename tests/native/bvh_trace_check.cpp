@@ -26,7 +26,6 @@
 namespace {
 
 bool g_debug = false;
-bool g_no_grid = false;
 
 float bitsf(uint32_t u)
 {
@@ -36,13 +35,12 @@ float bitsf(uint32_t u)
 }
 
 struct Work {
-    long long nodes = 0, tests = 0, bvh_nodes = 0, bvh_tests = 0, leaves = 0, resumed = 0, resume_failed = 0,
-              rows = 0;
+    long long nodes = 0, tests = 0, bvh_nodes = 0, bvh_tests = 0, leaves = 0, rows = 0;
 };
 
 struct E { uint32_t node; float entry; };
 
-// the state the descent resumes from (kd_resume): node, interval, stack
+// the state the descent resumes from (the origin-cell replay): node, interval, stack
 struct Resume {
     uint32_t node = 0;
     float entry = 0, exit_ = 0;
@@ -142,9 +140,8 @@ Hit kd_trace(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, float entry, floa
     }
 }
 
-float bvh_bound(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, float best, Work &w, uint32_t *best_first = nullptr)
+float bvh_bound(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, float best, Work &w)
 {
-    if (best_first) *best_first = RT_BVH_EMPTY;
     const float m = rt_ray_margin(o.x, o.y, o.z, h.bvh_scale);
     const Vec3D om = rt_v3(o.x + m, o.y + m, o.z + m), op = rt_v3(o.x - m, o.y - m, o.z - m);
     const Vec3D inv = rt_v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
@@ -181,7 +178,6 @@ float bvh_bound(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, float best, Wo
                 ++w.bvh_tests;
                 if (test(h.bvh_a.data(), h.bvh_bary.data(), e, o, d, best, s, b)) {
                     best = s;
-                    if (best_first) *best_first = first;
                 }
             }
         }
@@ -198,74 +194,10 @@ float bvh_bound(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, float best, Wo
     }
 }
 
-// s_min over the 8-wide collapse (h.bvh8, lone_trace.h lone_bound): the
-// same smallest passing s as the binary query, whatever the visiting order
-float bvh8_bound(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, float best)
-{
-    const float m = rt_ray_margin(o.x, o.y, o.z, h.bvh_scale);
-    const Vec3D om = rt_v3(o.x + m, o.y + m, o.z + m), op = rt_v3(o.x - m, o.y - m, o.z - m);
-    const Vec3D inv = rt_v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-    std::vector<std::pair<uint32_t, float>> stk{{0u, -INFINITY}};
-    while (!stk.empty()) {
-        const auto top = stk.back();
-        stk.pop_back();
-        if (!(top.second <= best)) continue;
-        const RtF4 *nd = &h.bvh8[16 * (size_t)top.first];
-        for (int k = 0; k < 8; ++k) {
-            uint32_t ref;
-            memcpy(&ref, &nd[2 * k + 1].z, 4);
-            if (ref == RT_BVH_EMPTY) continue;
-            float tn;
-            if (!rt_bvh_box(nd[2 * k].x, nd[2 * k].y, nd[2 * k].z, nd[2 * k].w, nd[2 * k + 1].x, nd[2 * k + 1].y, om, op,
-                            inv, best, tn))
-                continue;
-            if (ref & RT_BVH_LEAF) {
-                const uint32_t f = (ref & ~RT_BVH_LEAF) >> 3, e1 = f + (ref & 7u) + 1u;
-                for (uint32_t e = f; e < e1; ++e) {
-                    float s, b[3];
-                    if (test(h.bvh_a.data(), h.bvh_bary.data(), e, o, d, best, s, b)) best = s;
-                }
-            } else {
-                stk.push_back({ref, tn});
-            }
-        }
-    }
-    return best;
-}
-
-long long g_bvh8_mism = 0;
 long long g_origin_mism = 0;
 
-// restatement of bvh_trace.h kd_resume: replay the bounded descent along the
-// stored root path of the leaf's start node, each decision checked
-// the start record of the ray: the deeper of its s_min leaf's and of the grid
-// cell of o + d * s_min (bvh_trace.h kd_pick)
-void kd_pick(const rt_host::PreparedHost &h, uint32_t best_first, Vec3D o, Vec3D d, float s_min, uint32_t &start,
-             uint32_t &packed)
-{
-    start = packed = 0xFFFFFFFFu;
-    if (best_first != RT_BVH_EMPTY) {
-        start = h.kd_start[2 * (size_t)best_first];
-        packed = h.kd_start[2 * (size_t)best_first + 1];
-    }
-    if (h.kd_grid > 0 && !g_no_grid) {
-        const int G = h.kd_grid;
-        const float p[3] = {o.x + d.x * s_min, o.y + d.y * s_min, o.z + d.z * s_min};
-        const float bmin[3] = {h.bounds.min.x, h.bounds.min.y, h.bounds.min.z};
-        int c[3];
-        for (int a = 0; a < 3; ++a) {
-            const float f = (p[a] - bmin[a]) * h.kd_grid_scale[a];
-            c[a] = f >= 0.0f ? (f < (float)(G - 1) ? (int)f : G - 1) : 0; // (NaN: 0)
-        }
-        const size_t k = ((size_t)c[2] * G + c[1]) * G + c[0];
-        const uint32_t cs = h.kd_cell[2 * k], cp = h.kd_cell[2 * k + 1];
-        if (cs != 0xFFFFFFFFu && (start == 0xFFFFFFFFu || (cp & 31u) > (packed & 31u))) {
-            start = cs;
-            packed = cp;
-        }
-    }
-}
-
+// restatement of coop_trace.h kd_origin_frontier's replay: the descent along
+// the stored root path of a grid cell's start node, each decision checked
 bool kd_resume(const rt_host::PreparedHost &h, uint32_t start, uint32_t packed, Vec3D o, Vec3D d, float entry,
                float exit_, float s_min, Resume &r, Work &w)
 {
@@ -306,33 +238,13 @@ bool kd_resume(const rt_host::PreparedHost &h, uint32_t start, uint32_t packed, 
     return true;
 }
 
-bool g_resume = true;
-
 Hit bounded_trace(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, Work &w)
 {
     float t1, t2;
     if (!scene_box(h, o, d, t1, t2)) return Hit{};
     if (!rt_bounded_ray(o, d, h.split_vals.data(), h.split_off)) return kd_trace(h, o, d, t1, t2, -INFINITY, w);
-    uint32_t bf;
-    const float s_min = bvh_bound(h, o, d, t2, w, &bf);
-    if (!h.bvh8.empty()) {
-        const float s8 = bvh8_bound(h, o, d, t2);
-        if (memcmp(&s8, &s_min, 4) != 0) {
-#pragma omp atomic
-            ++g_bvh8_mism;
-        }
-    }
+    const float s_min = bvh_bound(h, o, d, t2, w);
     if (!(s_min < t2)) return Hit{};
-    if (g_resume && !h.kd_start.empty()) {
-        Resume r;
-        uint32_t start, packed;
-        kd_pick(h, bf, o, d, s_min, start, packed);
-        if (kd_resume(h, start, packed, o, d, t1, t2, s_min, r, w)) {
-            ++w.resumed;
-            return kd_trace(h, o, d, t1, t2, s_min, w, &r);
-        }
-        ++w.resume_failed;
-    }
     return kd_trace(h, o, d, t1, t2, s_min, w);
 }
 
@@ -380,9 +292,6 @@ int main(int argc, char **argv)
         return 2;
     }
     const long long rays = argc > 2 ? atoll(argv[2]) : 200000;
-    g_resume = !getenv("RT_KD_RESUME") || atoi(getenv("RT_KD_RESUME")) != 0;
-    setenv("RT_KD_RESUME", g_resume ? "1" : "0", 1); // prepare_host builds the shortcut's tables
-    if (getenv("RT_KD_NO_GRID")) g_no_grid = true;
     std::mt19937_64 rng(argc > 3 ? strtoull(argv[3], nullptr, 10) : 7);
     RtHostScene scene;
     Camera cam;
@@ -515,9 +424,6 @@ int main(int argc, char **argv)
             wb.leaves += lb.leaves;
             wb.bvh_nodes += lb.bvh_nodes;
             wb.bvh_tests += lb.bvh_tests;
-            wb.resumed += lb.resumed;
-            wb.resume_failed += lb.resume_failed;
-            wb.rows += lb.rows;
         }
     }
     (void)unit;
@@ -526,9 +432,6 @@ int main(int argc, char **argv)
     printf("kd-only per ray: nodes %.1f leaves %.1f tests %.1f\n", wp.nodes / R, wp.leaves / R, wp.tests / R);
     printf("bounded per ray: bvh nodes %.1f bvh tests %.1f kd nodes %.1f leaves %.2f tests %.1f\n", wb.bvh_nodes / R,
            wb.bvh_tests / R, wb.nodes / R, wb.leaves / R, wb.tests / R);
-    printf("kd resume: %lld resumed, %lld fell back to the root, %.1f path records per ray (%zu rows)\n", wb.resumed,
-           wb.resume_failed, wb.rows / R, h.kd_rows.size() / 4);
-    printf("8-wide BVH: %zu nodes, s_min mismatches vs the binary query %lld\n", h.bvh8.size() / 16, g_bvh8_mism);
     printf("origin-cell entry: %lld resumed, mismatches vs the plain traversal %lld\n", g_origin_resumed, g_origin_mism);
-    return mism == 0 && g_bvh8_mism == 0 && g_origin_mism == 0 ? 0 : 1;
+    return mism == 0 && g_origin_mism == 0 ? 0 : 1;
 }

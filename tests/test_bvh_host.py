@@ -90,16 +90,12 @@ def test_bounded_equals_kd_hazard_scenes(trace_check, tmp_path):
     assert "mismatches 0" in _run_trace_check(trace_check, path, 500_000, cam=on[:3])
 
 
-@pytest.mark.parametrize("grid", [True, False])
-def test_descent_shortcut_and_bvh8_host(trace_check, tmp_path, grid):
-    """The opt-in traversal tables (RT_KD_RESUME / RT_LONE): the KD descent
-    shortcut resumed from the s_min leaf's start node alone (the GPU's
-    lone_trace) or the deeper of it and the grid cell's, and the 8-wide BVH's
-    s_min, all equal to the plain KD traversal / the binary query."""
-    env = {} if grid else {"RT_KD_NO_GRID": "1"}
+def test_origin_cell_entry_host(trace_check, tmp_path):
+    """wf_long's deep bounces enter the KD traversal at the grid cell holding
+    the ray's origin (coop_trace.h kd_origin_frontier): the replayed root path,
+    checked decision by decision, gives the plain traversal's result."""
     for path in (helpers.scene_path("cornell_blob"), helpers.make_trap_scene(str(tmp_path / "t"))):
-        out = _run_trace_check(trace_check, path, 300_000, seed=11, env=env)
+        out = _run_trace_check(trace_check, path, 300_000, seed=11)
         assert "rays 300000" in out and " mismatches 0\n" in out, out
-        assert "s_min mismatches vs the binary query 0" in out, out
-        resumed = int(out.split("kd resume: ")[1].split(" resumed")[0])
-        assert resumed > 0, out
+        line = out.split("origin-cell entry: ")[1]
+        assert int(line.split(" resumed")[0]) > 0 and line.split("traversal ")[1].startswith("0"), out

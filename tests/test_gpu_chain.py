@@ -1,0 +1,135 @@
+"""Chained calls (RtOptions.overlap) and the bounded traversal's run-time
+guard (RtOptions.check_interval), both on the default render (the bounded
+traversal, one persistent finisher per call, deep paths in wf_long).
+
+Chained calls let a call's deep-path tail (glass loops of 10^4+ bounces,
+SURVEY H8) run on while the next call of the same frame starts; pixels still
+out are owed the new call's passes.  A pixel's passes still run in order, so
+the frame must be bit-identical to unchained calls and to the oracle — over
+back-to-back calls on one stream, with the frame read (joined) in between,
+with adaptive sampling, and with calls that change the camera (which must not
+chain).  The guard re-traces a deterministic sample of the finisher's rays
+with the plain KD traversal (trace_ray, rt/trace_ray.cuh:244-318): its
+counters must show checks and no mismatch, and a deliberately corrupted
+record must be caught.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+import helpers
+import rt
+
+pytestmark = pytest.mark.gpu
+WF = rt.KERNEL_WAVEFRONT
+
+
+_HIP = None
+_STREAMS = []
+
+
+def _stream():
+    """a raw hipStream_t (kept for the session: the library may still hold events on it)"""
+    global _HIP
+    if _HIP is None:
+        _HIP = ctypes.CDLL("libamdhip64.so")
+    s = ctypes.c_void_p()
+    assert _HIP.hipStreamCreate(ctypes.byref(s)) == 0
+    _STREAMS.append(s)
+    return s
+
+
+def _render_calls(run, W, H, passes, stream=None, overlap=True, **kw):
+    return run.render(W, H, passes, kernel=WF, overlap=overlap, stream=stream, **kw)[0]
+
+
+@pytest.mark.parametrize("name,W,H,split", [("room2m", 1920, 1080, [16, 16, 16, 16]),
+                                            ("cornell_blob", 640, 360, [1, 2, 5, 8])])
+def test_chained_calls_equal_one_call(name, W, H, split):
+    run = helpers.GpuRun(name)
+    one = _render_calls(run, W, H, [sum(split)], overlap=False)
+    s = _stream()
+    chained = _render_calls(run, W, H, split, stream=s)
+    helpers.assert_bitwise(chained, one, what=f"{name} {len(split)} chained calls vs one call")
+    assert int(chained[2].sum()) == W * H * sum(split)
+
+
+def test_chained_deep_paths_vs_oracle(tmp_path):
+    """The glass light guide: hundreds of bounces per path, most pixels' samples
+    handed to wf_long; 1-pass chained calls (the reference's granularity,
+    rt/main.cu:114-155) must give the oracle's frame."""
+    trap = helpers.make_trap_scene(str(tmp_path / "t"))
+    run = helpers.GpuRun(trap)
+    W, H = 96, 64
+    split = [1] * 6 + [3]
+    rt.deviation_stats(reset=True)
+    gpu = _render_calls(run, W, H, split, wf_long_depth=8)
+    dev = rt.deviation_stats(reset=False)
+    ref, _ = helpers.oracle_render(trap, W, H, split)
+    helpers.assert_bitwise(gpu, ref, what="light guide, chained 1-pass calls")
+    assert dev["deep_paths"] > 0, dev  # the hand-off really ran
+
+
+def test_chained_adaptive_and_reads_between(tmp_path):
+    """Adaptive sampling over chained calls, the frame read (tonemap: joins) in
+    between, and a camera change (must not chain) — equal to plain calls."""
+    run = helpers.GpuRun("room_small")
+    W, H = 480, 270
+    ref = _render_calls(run, W, H, [6, 6, 6, 6], overlap=False, adaptive=True, min_samples=8)
+    g = rt.GBuffer(W, H)
+    for c in range(4):
+        opt = rt.options(W, H, 6, adaptive=True, min_samples=8, kernel=WF, overlap=True)
+        rt.render(run.dev, g, run.camera, 0 if c == 0 else 1, opt)
+        if c == 1:
+            rt.tonemap(g)  # reads the frame: joins the chained tail first
+    helpers.assert_bitwise(g.download(), ref, what="adaptive chained with a read between")
+    # a call with another camera does not chain onto the previous one
+    cam2 = rt.Camera()
+    ctypes.memmove(ctypes.byref(cam2), ctypes.byref(run.camera), ctypes.sizeof(rt.Camera))
+    cam2.yaw += 0.05
+    g1, g2 = rt.GBuffer(W, H), rt.GBuffer(W, H)
+    for g_, ov in ((g1, True), (g2, False)):
+        rt.render(run.dev, g_, run.camera, 0, rt.options(W, H, 4, adaptive=False, kernel=WF, overlap=ov))
+        rt.render(run.dev, g_, cam2, 1, rt.options(W, H, 4, adaptive=False, kernel=WF, overlap=ov))
+    helpers.assert_bitwise(g1.download(), g2.download(), what="camera change between chained calls")
+
+
+def test_guard_counts_checks_and_no_mismatch():
+    run = helpers.GpuRun("room2m")
+    rt.deviation_stats(reset=True)
+    _render_calls(run, 960, 540, [8, 8], check_interval=64)
+    dev = rt.deviation_stats(reset=True)
+    # ~960*540*16 samples x ~3 rays / 64
+    assert dev["bounded_checked"] > 200_000, dev
+    assert dev["bounded_mismatches"] == 0, dev
+
+
+def test_guard_catches_a_corrupted_result():
+    """RT_DEBUG_CHECK_FAULT records every checked hit with a wrong triangle:
+    the KD re-trace must flag each of them (and only hits: misses stay)."""
+    run = helpers.GpuRun("cornell")
+    rt.deviation_stats(reset=True)
+    _render_calls(run, 128, 128, [4], check_interval=16, debug=4)
+    dev = rt.deviation_stats(reset=True)
+    assert dev["bounded_checked"] > 1000, dev
+    # the closed box: every ray hits something
+    assert dev["bounded_mismatches"] == dev["bounded_checked"], dev
+    assert any(v != 0.0 for v in dev["mismatch_ray"]), dev
+
+
+def test_megakernel_two_streams_equal_serial():
+    """two bounded megakernel calls on different streams share the
+    per-device spill area; the library serialises them on it."""
+    run = helpers.GpuRun("room_small")
+    W, H = 320, 180
+    ga, gb = rt.GBuffer(W, H), rt.GBuffer(W, H, W * H)
+    s1, s2 = _stream(), _stream()
+    for g_, s in ((ga, s1), (gb, s2)):
+        rt.render(run.dev, g_, run.camera, 0, rt.options(W, H, 4, adaptive=False, kernel=rt.KERNEL_MEGA,
+                                                         stream=s))
+    rt.check(rt.lib().rt_synchronize())
+    ra, _, _ = run.render(W, H, 4, kernel=rt.KERNEL_MEGA)
+    rb, _, _ = run.render(W, H, 4, kernel=rt.KERNEL_MEGA, seed_skip=W * H)
+    helpers.assert_bitwise(ga.download(), ra, what="megakernel stream 1")
+    helpers.assert_bitwise(gb.download(), rb, what="megakernel stream 2")
