@@ -60,6 +60,76 @@ inline float tri_margin(Vec3D p1, Vec3D v0, Vec3D v1, float rd, float nx, float 
 
 // (the per-ray margin, rt_ray_margin, is in bvh_common.h: the traversal adds it)
 
+// A proven bound (DESIGN.md §5 "The margin, derived") on the inf-norm
+// distance from the triangle's vertex box of the EXACT point o + s*d of any
+// passing test (rt_tri_plane + rt_tri_bary, the reference's arithmetic on
+// these precomputed floats) of a ray with |o|_1 <= on1 (any direction), plus
+// the slab test's own rounding at a box whose corners have |.|_1 <= box1 (so
+// that tri_margin + rt_ray_margin
+// >= this value means the culling never drops a passing test).  Standard
+// rounding-error analysis (gamma_k = k u / (1 - k u), u = 2^-24, every float
+// operation of the test and of the precomputation), evaluated in double and
+// inflated by 1e-6 relative; +inf when its conditioning premise fails.  Not
+// used by the build: tests/native/bvh_margin_check.cpp and bvh_trace_check.cpp
+// check tri_margin + rt_ray_margin against it for every triangle they see.
+inline double tri_margin_bound(Vec3D p1, Vec3D v0, Vec3D v1, float rd, double on1, double box1)
+{
+    const double u = 0x1p-24;
+    auto gam = [&](double k) { return k * u / (1.0 - k * u); };
+    const double g2 = gam(2), g3 = gam(3);
+    const double l0 = sqrt((double)v0.x * v0.x + (double)v0.y * v0.y + (double)v0.z * v0.z);
+    const double l1 = sqrt((double)v1.x * v1.x + (double)v1.y * v1.y + (double)v1.z * v1.z);
+    const double L = l0 > l1 ? l0 : l1;
+    if (!(L > 0.0) || !isfinite(rd)) return INFINITY;
+    const double kappa = L * L * L * L * fabs((double)rd); // ~ 1 / sin^2 of the triangle's angles
+    // |d_ij - v_i.v_j| <= g3 L^2, product / difference roundings: the Cramer
+    // numerators and den = d00 d11 - d01^2 are off by at most a1 R L^3 / a1 L^4
+    const double a1 = 2.0 * g3 * (2.0 + g3) + 2.0 * g2 * (1.0 + g3) * (1.0 + g3);
+    const double b = u + a1 * kappa * (1.0 + u) * (1.0 + u); // |rd * det G - 1|
+    if (!(b < 0.25)) return INFINITY;
+    const double bp = b + u * (1.0 + b);
+    const double c = (1.0 + u) * a1 * kappa;
+    const double D = 1.0 - bp - 2.0 * c;
+    if (!(D > 0.5)) return INFINITY;
+    // angle of the stored normal n = normalize(cross(v0, v1)) to the exact one
+    const double tau = 1.5708 * g2 * sqrt(2.0 * kappa / (1.0 - b)) + 4.0 * u;
+    const double p1n = fabs((double)p1.x) + fabs((double)p1.y) + fabs((double)p1.z);
+    const double s3 = 1.7320508075688772;
+    // R = |v2| (v2 = fl(P - p1)): R <= 2 (1 + delta) L + h', where delta bounds
+    // the barycentric error and h' the distance of p1 + v2 from the plane;
+    // F below is that bound as a (monotone, contracting) function of R
+    double hp = 0, eP = 0, eV = 0, delta = 0;
+    auto F = [&](double R) {
+        // |X|_1 <= |p1|_1 + sqrt3 |X - p1|, |X - p1| <= R (1 + 3u) + e_P; e_P = |P - X| (P = fl(o + fl(d s)))
+        double e = 0.0;
+        for (int it = 0; it < 4; ++it) {
+            const double xn = p1n + s3 * (R * (1.0 + 3.0 * u) + e);
+            const double sdn = xn + on1; // |s| |d|_1 = |X - o|_1
+            e = g2 * (sdn + xn) * (1.0 + 1e-9);
+        }
+        eP = e;
+        const double xn = p1n + s3 * (R * (1.0 + 3.0 * u) + eP), sdn = xn + on1;
+        eV = u * R * (1.0 + 3.0 * u); // v2 = fl(P - p1)
+        // n.(X - p1) for the plane test's s: the roundings of w = n.p1, n.o, d.n, num and num / dn
+        const double A0 = g2 * (1.0 + g3) * (1.0 + 4.0 * u) * (p1n + on1) +
+                          g3 * (1.0 + 4.0 * u) * (on1 + p1n + sdn);
+        hp = A0 + tau * (R * (1.0 + 3.0 * u) + eP) + eP + eV;
+        delta = (c * (2.0 + hp / L) + bp) / D;
+        return 2.0 * (1.0 + delta) * L + hp;
+    };
+    double R = 2.0 * L;
+    for (int it = 0; it < 200; ++it) R = F(R);
+    R = R * (1.0 + 1e-9) + 1e-30;
+    if (!(F(R) <= R)) return INFINITY; // (no contraction: the premise fails)
+    (void)F(R);
+    // Q = p1 + cy v0 + cz v1 lies in the triangle grown by u (cy, cz >= 0,
+    // cy + cz <= 1 + u), whose vertex box is within u L of the real one
+    const double dist = 2.0 * u * L + eP + eV + hp + 2.0 * delta * L;
+    // the slab test's rounding at a box within box1 (|corner|_1) of the origin
+    const double slab = 3.0 * u * (box1 + on1);
+    return (dist + slab) * (1.0 + 1e-6) + 1e-30;
+}
+
 struct BvhHost {
     std::vector<RtF4> nodes;       // 4 per node (bvh_trace.h layout)
     std::vector<uint32_t> order;   // BVH leaf slot -> triangle index

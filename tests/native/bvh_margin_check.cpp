@@ -6,7 +6,12 @@
 // the same float operations as the GPU: bvh_common.h) must NOT be culled by
 // the slab test of the triangle's grown box with best = s.  Reports the
 // largest fraction of the margin a hit point actually used (the slack), and
-// checks that triangles left out (NaN margin) never pass.
+// checks that triangles left out (NaN margin) never pass.  Also checks the
+// written-out bound (bvh_build.h tri_margin_bound): every exact
+// hit point lies within it (the derivation holds on these cases), and the
+// shipped margins — tri_margin + rt_ray_margin — are at least that bound for
+// every finite-margin triangle and any origin (the culling is proven safe,
+// not only sampled); reports the smallest ratio shipped / proven.
 //
 // Build: g++ -O2 -std=c++17 -ffp-contract=off -fno-fast-math -I include -I csrc ...
 // Usage: bvh_margin_check [pairs_millions] [seed]; exit 0 = no violation.
@@ -45,6 +50,11 @@ Rec prepare(Vec3D p1, Vec3D p2, Vec3D p3) // scene_prepare.cpp's per-triangle co
 struct Stats {
     long long pairs = 0, passes = 0, violations = 0, nan_tris = 0, nan_passes = 0, inf_tris = 0, tris = 0;
     double max_used = 0.0; // largest (distance of the exact hit point outside the vertex box) / (margin + ray margin)
+    long long bound_fails = 0;    // exact hit points outside the proven bound (must be 0)
+    long long margin_short = 0;   // triangles whose shipped margin is below the proven bound (must be 0)
+    long long bound_inf = 0;      // finite shipped margin but no proven bound (must be 0)
+    double min_ratio = INFINITY;  // smallest (tri_margin + rt_ray_margin) / proven bound
+    double max_bound_used = 0.0;  // largest (distance outside the vertex box) / proven bound
 };
 
 std::mt19937_64 rng;
@@ -84,6 +94,22 @@ void check_triangle(Vec3D p1, Vec3D p2, Vec3D p3, int rays, Stats &st)
     if (U(0, 1) < 0.3) scale *= logU(1.0, 50.0);
     const float fscale = (float)scale;
     const double L = fmax(fmax(fabs((double)hi[0] - lo[0]), fabs((double)hi[1] - lo[1])), fabs((double)hi[2] - lo[2]));
+    // the shipped margins against the proven bound, for origins from 0 to far beyond the scene
+    // (both sides are affine in |o|_1: the ends and the scene's own range decide)
+    if (m == m) {
+        for (double on1 : {0.0, (double)fscale, 3.0 * fscale, 1e3 * fscale, 1e6 * fscale + 1.0}) {
+            const double pb = rt_host::tri_margin_bound(p1, p2 - p1, p3 - p1, r.rd, on1, 3.0 * fscale);
+            if (isinf(pb)) {
+                ++st.bound_inf;
+                continue;
+            }
+            // the per-ray margin as the traversal computes it for an origin with |o|_1 = on1
+            const float of = (float)(on1 / 3.0);
+            const double shipped = (double)m + (double)rt_ray_margin(of, of, of, fscale);
+            st.min_ratio = fmin(st.min_ratio, shipped / pb);
+            if (shipped < pb) ++st.margin_short;
+        }
+    }
     for (int k = 0; k < rays; ++k) {
         ++st.pairs;
         // target: a point near the triangle (barycentrics slightly outside [0, 1] too)
@@ -138,6 +164,15 @@ void check_triangle(Vec3D p1, Vec3D p2, Vec3D p3, int rays, Stats &st)
         for (int a = 0; a < 3; ++a) out = fmax(out, fmax(lo[a] - P[a], P[a] - hi[a]));
         const double used = out / ((double)m + mr);
         if (used > st.max_used) st.max_used = used;
+        const double on1 = fabs((double)o.x) + fabs((double)o.y) + fabs((double)o.z);
+        const double pb = rt_host::tri_margin_bound(p1, r.C.x == r.C.x ? rt_v3(r.C.x, r.C.y, r.C.z) : p2 - p1,
+                                                    rt_v3(r.D.x, r.D.y, r.D.z), r.rd, on1, 3.0 * fscale);
+        if (!isinf(pb)) {
+            st.max_bound_used = fmax(st.max_bound_used, out / pb);
+            if (out > pb && ++st.bound_fails <= 10)
+                fprintf(stderr, "BOUND FAIL: tri (%a %a %a) (%a %a %a) (%a %a %a) o (%a %a %a) d (%a %a %a) out %g bound %g\n",
+                        p1.x, p1.y, p1.z, p2.x, p2.y, p2.z, p3.x, p3.y, p3.z, o.x, o.y, o.z, d.x, d.y, d.z, out, pb);
+        }
         if (!kept) {
             if (++st.violations <= 10)
                 fprintf(stderr,
@@ -195,7 +230,12 @@ int main(int argc, char **argv)
         }
         check_triangle(p1, p2, p3, rays, st);
     }
-    printf("pairs %lld passes %lld violations %lld tris %lld nan_tris %lld nan_passes %lld inf_tris %lld max_used %.3g\n",
-           st.pairs, st.passes, st.violations, st.tris, st.nan_tris, st.nan_passes, st.inf_tris, st.max_used);
-    return st.violations == 0 && st.nan_passes == 0 ? 0 : 1;
+    printf("pairs %lld passes %lld violations %lld tris %lld nan_tris %lld nan_passes %lld inf_tris %lld max_used %.3g "
+           "bound_fails %lld margin_short %lld bound_inf %lld min_ratio %.4g max_bound_used %.4g\n",
+           st.pairs, st.passes, st.violations, st.tris, st.nan_tris, st.nan_passes, st.inf_tris, st.max_used,
+           st.bound_fails, st.margin_short, st.bound_inf, st.min_ratio, st.max_bound_used);
+    return st.violations == 0 && st.nan_passes == 0 && st.bound_fails == 0 && st.margin_short == 0 &&
+                   st.bound_inf == 0
+               ? 0
+               : 1;
 }

@@ -347,6 +347,40 @@ int main(int argc, char **argv)
     }
     printf("tris %d kd_nodes %zu bvh_nodes %zu bvh_depth %d always %d dropped %d\n", n, nodes.size(),
            h.bvh_nodes.size() / 4, h.bvh_depth, h.bvh_always, h.bvh_dropped);
+    {
+        // every triangle's shipped margin (tri_margin + rt_ray_margin, for origins from the scene's
+        // centre to far outside it) against the proven bound (bvh_build.h tri_margin_bound)
+        const Bounding_Box &b = h.bounds;
+        const double box1 = fmax(fabs((double)b.min.x), fabs((double)b.max.x)) +
+                            fmax(fabs((double)b.min.y), fabs((double)b.max.y)) +
+                            fmax(fabs((double)b.min.z), fabs((double)b.max.z));
+        long long shorts = 0, unproven = 0, finite = 0;
+        double min_ratio = INFINITY;
+#pragma omp parallel for reduction(+ : shorts, unproven, finite) reduction(min : min_ratio)
+        for (long long k = 0; k < (long long)h.bvh_bary.size(); ++k) {
+            const RtIsectBary &r = h.bvh_bary[(size_t)k];
+            const RtF4 &A = h.bvh_a[(size_t)k];
+            const Vec3D p1 = rt_v3(r.b.x, r.b.y, r.b.z), v0 = rt_v3(r.c.x, r.c.y, r.c.z), v1 = rt_v3(r.d.x, r.d.y, r.d.z);
+            const float rd = bitsf(r.rd);
+            const float m = rt_host::tri_margin(p1, v0, v1, rd, A.x, A.y, A.z);
+            if (!(m == m) || isinf(m)) continue; // (whole-scene box / left out)
+            ++finite;
+            for (double on1 : {0.0, box1, 1e3 * box1, 1e6 * box1 + 1.0}) {
+                const double pb = rt_host::tri_margin_bound(p1, v0, v1, rd, on1, box1);
+                if (isinf(pb)) {
+                    ++unproven;
+                    continue;
+                }
+                const float of = (float)(on1 / 3.0);
+                const double shipped = (double)m + (double)rt_ray_margin(of, of, of, h.bvh_scale);
+                min_ratio = fmin(min_ratio, shipped / pb);
+                if (shipped < pb) ++shorts;
+            }
+        }
+        printf("margins: %lld finite, shipped below the proven bound %lld, unproven %lld, min ratio %.4g\n", finite,
+               shorts, unproven, min_ratio);
+        if (shorts || unproven) return 1;
+    }
     std::uniform_real_distribution<float> U(0.0f, 1.0f);
     auto unit = [&]() {
         while (true) {

@@ -60,6 +60,10 @@ def test_margins_never_cull_a_passing_test(margin_check, seed):
     assert int(stats["passes"]) > 1_000_000 and int(stats["violations"]) == 0 and int(stats["nan_passes"]) == 0
     # the margins are generous: a hit point never used more than a small part of them
     assert float(stats["max_used"]) < 0.05, stats
+    # the written-out bound (bvh_build.h tri_margin_bound): every exact hit point lies within it, and
+    # the shipped margins are at least it for every finite-margin triangle and any origin
+    assert int(stats["bound_fails"]) == 0 and int(stats["margin_short"]) == 0 and int(stats["bound_inf"]) == 0, stats
+    assert float(stats["min_ratio"]) >= 1.0, stats
 
 
 def _run_trace_check(exe, scene, rays=1_000_000, seed=7, cam=None, env=None):
@@ -74,6 +78,8 @@ def _run_trace_check(exe, scene, rays=1_000_000, seed=7, cam=None, env=None):
 def test_bounded_equals_kd_host(trace_check, name):
     out = _run_trace_check(trace_check, helpers.scene_path(name))
     assert "mismatches 0" in out, out
+    # every triangle of the scene: shipped margin >= the proven bound
+    assert "shipped below the proven bound 0, unproven 0" in out, out
 
 
 def test_bounded_equals_kd_hazard_scenes(trace_check, tmp_path):

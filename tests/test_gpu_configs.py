@@ -133,3 +133,54 @@ def test_room2m_headline_budget_1024spp():
     assert np.all(gpu[2] == 1024)
     assert st["watchdog_paths"] == 0 and st["cut_paths"] == 0, st
     assert st["deep_paths"] > 0 and st["max_deep_depth"] >= rcnt["maxdepth"], (st, rcnt)
+
+
+# ------------------------------------------------ configs[4]: adaptive at the reference's constants
+REF_MIN_SAMPLES, REF_TOLERANCE = 100, 0.05  # rt/macros.h:13,17 (the test of rt/path_tracing.cuh:352-376)
+
+
+@pytest.mark.timeout(500)
+@pytest.mark.parametrize("shard", [0, 7])
+def test_configs4_room2m_glass_adaptive_reference_constants(shard):
+    """configs[4]: the dielectric stress scene at 1920x1080 with adaptive
+    sampling at the reference's own MIN_SAMPLES 100 / MAX_TOLERANCE 0.05 and
+    depth 32, on the bench kernel as the bench calls it (a 64-pass call that
+    resets, then a chained 192-pass call), so pixels cross 100 samples and the
+    test starts stopping them.  Every 3001st pixel bit-identical to the
+    oracle; shard 7's seed window is the 8-GPU configuration's (each GPU
+    evaluates adaptivity on its own slice's statistics)."""
+    run = helpers.GpuRun("room2m_glass")
+    W, H = 1920, 1080
+    calls = [64, 192]
+    skip = shard * W * H
+    gpu, _, _ = run.render(W, H, calls, adaptive=True, min_samples=REF_MIN_SAMPLES, tolerance=REF_TOLERANCE,
+                           max_depth=32, seed_skip=skip, kernel=rt.KERNEL_WAVEFRONT, overlap=True)
+    pixels = np.arange(0, W * H, 3001, dtype=np.int32)
+    ref, rcnt = helpers.oracle_render(run.path, W, H, calls, adaptive=True, min_samples=REF_MIN_SAMPLES,
+                                      tolerance=REF_TOLERANCE, max_depth=32, seed_skip=skip, pixels=pixels)
+    helpers.assert_bitwise(gpu, ref, pixels=pixels, what=f"configs[4] seed window {shard}")
+    cnt = gpu[2]
+    # the adaptive test stopped pixels after their 100th sample, and only then
+    assert rcnt["skip"] > 0 and cnt.min() >= REF_MIN_SAMPLES and (cnt < sum(calls)).sum() > W * H // 100, \
+        (rcnt["skip"], int(cnt.min()), int((cnt < sum(calls)).sum()))
+
+
+@pytest.mark.timeout(400)
+def test_configs4_regime_full_frame_cut_paths():
+    """The same regime (MIN_SAMPLES 100, tolerance 0.05, depth 32, 64 + 192
+    chained passes) on a whole 128x72 frame: every pixel bit-identical, and
+    the paths cut at depth 32 counted by the non-counting bench kernels equal
+    the oracle's over the same frame."""
+    run = helpers.GpuRun("room2m_glass")
+    W, H = 128, 72
+    calls = [64, 192]
+    _stats_reset()
+    gpu, _, _ = run.render(W, H, calls, adaptive=True, min_samples=REF_MIN_SAMPLES, tolerance=REF_TOLERANCE,
+                           max_depth=32, kernel=rt.KERNEL_WAVEFRONT, overlap=True)
+    st = rt.deviation_stats(reset=True)
+    dev = {}
+    ref, rcnt = helpers.oracle_render(run.path, W, H, calls, adaptive=True, min_samples=REF_MIN_SAMPLES,
+                                      tolerance=REF_TOLERANCE, max_depth=32, deviations=dev)
+    helpers.assert_bitwise(gpu, ref, what="configs[4] regime 128x72")
+    assert rcnt["skip"] > 0, rcnt
+    assert st["cut_paths"] == dev["cut"] > 0 and st["watchdog_paths"] == 0, (st, dev)
