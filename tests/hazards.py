@@ -144,3 +144,101 @@ def _mt(n):
     import oracle
 
     return oracle.mt19937(n)
+
+
+# ------------------------------------------------------------ adversarial geometry
+ADV_MAT = ("material white\nalbedo 0.73 0.73 0.73\nroughness 0.5\nn 1.5\n\n"
+           "material red\nalbedo 0.65 0.05 0.05\nroughness 0.5\nn 1.5\n\n"
+           "material gold\nalbedo 0.9 0.7 0.3\nroughness 0.15\nn 1.2\nk 3.0\n\n"
+           "material glass\nalbedo 0.99 0.99 0.99\nroughness 0.01\nn 1.5\ntransparent\n\n"
+           "material light\nalbedo 0.78 0.78 0.78\nemittance 15.0 15.0 15.0\nroughness 0.5\nn 1.5\n")
+
+
+def _adversarial_obj(seed):
+    """A closed room (y in [0, 2]) holding the cases the BVH margins are
+    hardest on: slivers (a vertex 1e-7..1e-2 of the edge length off the
+    opposite edge), needles (two vertices 1e-7..1e-3 apart), near-degenerate
+    fans sharing a vertex, and a dense cluster of tiny triangles — in every
+    orientation, some axis-aligned."""
+    rng = np.random.default_rng(seed)
+    lines = ["# adversarial room"]
+    vs = []
+
+    def quad(mat, a, b, c, d):
+        base = len(vs) + 1
+        vs.extend([a, b, c, d])
+        lines.append(f"usemtl {mat}")
+        lines.append(f"f {base} {base + 1} {base + 2} {base + 3}")
+
+    def tri(mat, a, b, c):
+        base = len(vs) + 1
+        vs.extend([a, b, c])
+        lines.append(f"usemtl {mat}")
+        lines.append(f"f {base} {base + 1} {base + 2}")
+
+    quad("white", (-1, 0, -1), (1, 0, -1), (1, 0, 1), (-1, 0, 1))
+    quad("white", (-1, 2, -1), (-1, 2, 1), (1, 2, 1), (1, 2, -1))
+    quad("white", (-1, 0, 1), (1, 0, 1), (1, 2, 1), (-1, 2, 1))
+    quad("red", (-1, 0, -1), (-1, 0, 1), (-1, 2, 1), (-1, 2, -1))
+    quad("white", (1, 0, -1), (1, 2, -1), (1, 2, 1), (1, 0, 1))
+    quad("light", (-0.3, 1.98, -0.3), (0.3, 1.98, -0.3), (0.3, 1.98, 0.3), (-0.3, 1.98, 0.3))
+
+    def unit():
+        v = rng.normal(size=3)
+        return v / np.linalg.norm(v)
+
+    mats = ["white", "gold", "glass", "red"]
+    for k in range(300):  # slivers
+        c = rng.uniform([-0.8, 0.2, -0.8], [0.8, 1.8, 0.8])
+        u, w = unit(), unit()
+        if k % 5 == 0:  # axis-aligned edge and offset
+            u, w = np.eye(3)[k % 3], np.eye(3)[(k + 1) % 3]
+        L = 10 ** rng.uniform(-2.5, -0.5)
+        eps = L * 10 ** rng.uniform(-7, -2)
+        p1, p2 = c, c + L * u
+        p3 = c + L * rng.uniform(0, 1) * u + eps * w
+        tri(mats[k % 4], p1, p2, p3)
+    for k in range(300):  # needles
+        c = rng.uniform([-0.8, 0.2, -0.8], [0.8, 1.8, 0.8])
+        u, w = unit(), unit()
+        L = 10 ** rng.uniform(-2, -0.3)
+        p2 = c + L * u
+        tri(mats[(k + 1) % 4], c, p2, p2 + L * 10 ** rng.uniform(-7, -3) * w)
+    for k in range(20):  # fans of thin wedges around a shared vertex
+        c = rng.uniform([-0.6, 0.4, -0.6], [0.6, 1.6, 0.6])
+        u, w = unit(), unit()
+        w = w - np.dot(w, u) * u
+        w /= np.linalg.norm(w)
+        L = 10 ** rng.uniform(-1.5, -0.7)
+        angs = np.sort(rng.uniform(0, 2 * np.pi, 24))
+        for a0, a1 in zip(angs[:-1], angs[1:]):
+            tri(mats[k % 4], c, c + L * (np.cos(a0) * u + np.sin(a0) * w), c + L * (np.cos(a1) * u + np.sin(a1) * w))
+    cl = np.array([0.2, 0.9, 0.1])  # a cloud of tiny triangles (1e-4..1e-3 of the room)
+    for k in range(400):
+        c = cl + rng.normal(scale=0.05, size=3)
+        s = 2 * 10 ** rng.uniform(-4, -3)
+        tri(mats[k % 3], c, c + s * unit(), c + s * unit())
+    out = [lines[0]] + [f"v {x:.9g} {y:.9g} {z:.9g}" for x, y, z in vs] + lines[1:]
+    return "\n".join(out) + "\n"
+
+
+def adversarial_scene(d, variant="far", seed=1):
+    """The adversarial room (_adversarial_obj) placed where float rounding is
+    coarsest relative to its features:
+      far   — translated to x = 1.2e4, z = -8e3 (|x| ~ 10^4, 1 ulp ~ 1e-3 m);
+      tiny  — scaled to 2 cm and placed 100 units from the origin, so its
+              cloud triangles are sub-millimetre (0.2-2 um .. 20 um) 100 m away;
+      near  — at the origin (reference)."""
+    os.makedirs(d, exist_ok=True)
+    with open(os.path.join(d, "adv.obj"), "w") as f:
+        f.write(_adversarial_obj(seed))
+    with open(os.path.join(d, "adv.mat"), "w") as f:
+        f.write(ADV_MAT)
+    ox, oy, oz, sc = {"far": (12000.0, 1.0, -8000.0, 1.0), "tiny": (100.0, 0.01, 0.0, 0.01),
+                      "near": (0.0, 1.0, 0.0, 1.0)}[variant]
+    cam = (ox - 0.3458 * sc, oy, oz - 3.5834 * sc)
+    p = os.path.join(d, "scene.txt")
+    with open(p, "w") as f:
+        f.write(f"mesh adv.obj adv.mat {ox!r} {oy!r} {oz!r} 0.1 0 {sc!r} 0\n"
+                f"camera {cam[0]!r} {cam[1]!r} {cam[2]!r} 0.1 0 0.8 0.0001\n")
+    return p

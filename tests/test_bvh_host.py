@@ -105,3 +105,16 @@ def test_origin_cell_entry_host(trace_check, tmp_path):
         assert "rays 300000" in out and " mismatches 0\n" in out, out
         line = out.split("origin-cell entry: ")[1]
         assert int(line.split(" resumed")[0]) > 0 and line.split("traversal ")[1].startswith("0"), out
+
+
+@pytest.mark.parametrize("variant", ["far", "tiny", "near"])
+def test_bounded_equals_kd_adversarial_host(trace_check, tmp_path, variant):
+    """Slivers, needles, thin fans and a cloud of tiny triangles, at the origin,
+    translated to |x| ~ 10^4, and scaled to sub-millimetre triangles 100 units
+    away (hazards.adversarial_scene): the bounded traversal equals the KD
+    traversal on every ray, and every triangle's margin is at least the proven
+    bound."""
+    path = hazards.adversarial_scene(str(tmp_path / variant), variant)
+    out = _run_trace_check(trace_check, path, 1_000_000, seed=3)
+    assert "rays 1000000" in out and " mismatches 0\n" in out, out
+    assert "shipped below the proven bound 0, unproven 0" in out, out

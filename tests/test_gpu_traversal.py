@@ -86,3 +86,27 @@ def test_bounded_hazard_scenes(tmp_path):
         rng = rng0.copy()
         sc.render(np.asarray(cam_arr, np.float32), fb, sq, ct, rng, W, H, P, sample_count_arg=0, adaptive=False)
         helpers.assert_bitwise(g.download(), (fb.reshape(n, 3), sq, ct, rng), what=path)
+
+
+@pytest.mark.parametrize("variant", ["far", "tiny", "near"])
+def test_bounded_equals_kd_adversarial_full_frame(tmp_path, variant):
+    """slivers (a vertex 1e-7..1e-2 of the edge off the
+    opposite edge), needles, thin fans and a cloud of tiny triangles in glass,
+    gold and diffuse materials — at the origin, translated to |x| ~ 10^4, and
+    shrunk to sub-millimetre triangles 100 units from the origin
+    (hazards.adversarial_scene).  Whole frames, the bounded traversal (the
+    product path, with its run-time guard on every 16th ray) against the KD
+    traversal, bit for bit; the guard sees no mismatch; pixel samples
+    against the oracle."""
+    path = hazards.adversarial_scene(str(tmp_path / variant), variant)
+    run = helpers.GpuRun(path)
+    W, H = 320, 240
+    rt.deviation_stats(reset=True)
+    a, _, _ = run.render(W, H, [4, 4], kernel=rt.KERNEL_WAVEFRONT, traversal=W_BOUNDED, check_interval=16)
+    dev = rt.deviation_stats(reset=True)
+    b, _, _ = run.render(W, H, [4, 4], kernel=rt.KERNEL_WAVEFRONT, traversal=W_KD)
+    helpers.assert_bitwise(a, b, what=f"adversarial {variant}: bounded vs kd")
+    assert dev["bounded_checked"] > 10_000 and dev["bounded_mismatches"] == 0, dev
+    pixels = np.arange(0, W * H, 97)
+    ref, _ = helpers.oracle_render(path, W, H, [4, 4], pixels=pixels)
+    helpers.assert_bitwise(a, ref, pixels=pixels, what=f"adversarial {variant}: bounded vs oracle")
