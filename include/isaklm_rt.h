@@ -478,7 +478,7 @@ typedef struct RtOptions {
 #define RT_TRAVERSAL_BOUNDED_COUNTED 2
 #define RT_DEBUG_CALL_LOG 1  /* per call / queue iteration: counters and host times */
 #define RT_DEBUG_LONG_LOG 2  /* every deep sample's claim / end time and bounces (unchained calls) */
-#define RT_DEBUG_CHECK_FAULT 4 /* tests of the guard: every checked hit is recorded with a wrong triangle */
+#define RT_DEBUG_CHECK_FAULT 4 /* tests of the guard: every checked ray is recorded with a wrong result */
 
 /* Per-call kernel timing of the last rt_render on this device with
  * RtOptions.profile = 1 (wavefront kernels; HIP events on the call's stream,

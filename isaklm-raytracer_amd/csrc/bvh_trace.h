@@ -26,6 +26,17 @@
 
 namespace rtk {
 
+#ifdef RT_PHASE_PROF
+// phase profile (a -DRT_PHASE_PROF build, tools/phase_profile.py): per wave,
+// the s_memtime at which trace_bvh's BVH query ends (the KD phase starts)
+__device__ unsigned long long g_phase_mid[16384];
+__device__ unsigned long long g_phase_acc[8]; // wf_finish_bvh's per-phase sums (wavefront.hip)
+#define RT_PHASE_MID()                                                                                              \
+    g_phase_mid[((blockIdx.x * blockDim.x + threadIdx.x) >> 6) & 16383] = __builtin_amdgcn_s_memtime()
+#else
+#define RT_PHASE_MID()
+#endif
+
 // Scene data is read-only for a kernel's lifetime: loaded through the
 // constant address space (a wave-uniform address becomes a scalar load
 // through the scalar cache; a divergent one stays a vector load).
@@ -165,6 +176,7 @@ __device__ __forceinline__ int trace_bvh(const RtDevScene &sc, const Vec3D o, co
     float s_min = -INFINITY; // (the plain KD traversal)
     if (rt_bounded_ray(o, d, sc.split_vals, sc.split_off)) {
         s_min = bvh_bound<COUNT>(sc, o, d, exit_, stk, c);
+        RT_PHASE_MID();
         if (!(s_min < root_exit)) return -1;
     }
     const float yx = rt_recip_guard(d.x), yy = rt_recip_guard(d.y), yz = rt_recip_guard(d.z);

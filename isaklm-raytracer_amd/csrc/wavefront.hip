@@ -184,7 +184,7 @@ struct WfState {
     RtF4 *chk;
     uint32_t *chk_ctr;
     uint32_t chk_mask;
-    int chk_fault; // (RT_DEBUG_CHECK_FAULT, tests: record a wrong triangle for every checked hit)
+    int chk_fault; // (RT_DEBUG_CHECK_FAULT, tests: record a wrong result for every checked ray)
 };
 
 namespace {
@@ -1022,6 +1022,12 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_FIN_BVH_WAVES) wf_finish_bvh(RtDe
     uint32_t *const ret_claimed = st.ret_ctr + 2;
     if (st.long_return && lane == 0) // this wave is alive: wf_long may return pixels to it
         __hip_atomic_fetch_add(ret_word, 1ull << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#ifdef RT_PHASE_PROF
+    // wave-time per phase (s_memtime, scalar): loop overhead, BVH query, KD phase, shading + guard + hand-off;
+    // iterations and active lanes at the ray query
+    unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const int wid = ((blockIdx.x * blockDim.x + threadIdx.x) >> 6) & 16383;
+#endif
     PathRegs p;
     p.slot = 0;
     p.ro = p.rd = rt_v3(0, 0, 0);
@@ -1029,6 +1035,9 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_FIN_BVH_WAVES) wf_finish_bvh(RtDe
     unsigned long long idle_since = 0;      // (lane 0) when the wave first had nothing to do
     bool seated = false;                    // (lane 0) holds a linger seat
     while (true) {
+#ifdef RT_PHASE_PROF
+        const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+#endif
         const bool need = !active && !exhausted;
         const unsigned long long m = __ballot(need);
         if (m) {
@@ -1116,9 +1125,27 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_FIN_BVH_WAVES) wf_finish_bvh(RtDe
         }
         idle_since = 0;
         bool to_long = false;
+#ifdef RT_PHASE_PROF
+        const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+        ph[0] += t1 - t0;
+        ph[4] += 1;
+        ph[5] += (unsigned long long)__popcll(__ballot(active));
+        g_phase_mid[wid] = 0;
+#endif
         if (active) {
             float bx = 0.0f, by = 0.0f, bz = 0.0f;
             const int hit = trace_bvh<COUNT>(sc, p.ro, p.rd, bx, by, bz, stk, c);
+#ifdef RT_PHASE_PROF
+            {
+                const unsigned long long t2 = __builtin_amdgcn_s_memtime();
+                const unsigned long long tm = g_phase_mid[wid];
+                const unsigned long long mid = tm > t1 && tm < t2 ? tm : t1;
+                ph[1] += mid - t1;
+                ph[2] += t2 - mid;
+                ph[6] += (unsigned long long)__popcll(__ballot(true));
+            }
+            const unsigned long long t2s = __builtin_amdgcn_s_memtime();
+#endif
             // run-time exactness guard: a deterministic sample of the rays, with the
             // bounded result, is queued for wf_check's plain KD re-trace
             if (!COUNT && st.chk) {
@@ -1132,7 +1159,7 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_FIN_BVH_WAVES) wf_finish_bvh(RtDe
                     const uint32_t i = wave_append(st.chk_ctr, rec);
                     if (rec && i < WF_CHECK_CAP) {
                         st.chk[3 * (size_t)i] =
-                            RtF4{p.ro.x, p.ro.y, p.ro.z, __int_as_float(st.chk_fault && hit >= 0 ? hit ^ 1 : hit)};
+                            RtF4{p.ro.x, p.ro.y, p.ro.z, __int_as_float(st.chk_fault ? (hit >= 0 ? hit ^ 1 : 0) : hit)};
                         st.chk[3 * (size_t)i + 1] = RtF4{p.rd.x, p.rd.y, p.rd.z, bx};
                         st.chk[3 * (size_t)i + 2] = RtF4{by, bz, 0.0f, 0.0f};
                     }
@@ -1147,9 +1174,16 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_FIN_BVH_WAVES) wf_finish_bvh(RtDe
             to_long = want && st.long_depth > 0 && p.depth > st.long_depth;
             if (!want || to_long) store_regs(st, fr, p);
             if (!want) active = false;
+#ifdef RT_PHASE_PROF
+            ph[3] += __builtin_amdgcn_s_memtime() - t2s;
+#endif
         }
         if (__any(to_long) && publish_long_capped(st, to_long, p.slot, p.ro, p.rd) && to_long) active = false;
     }
+#ifdef RT_PHASE_PROF
+    if (lane == 0)
+        for (int k = 0; k < 7; ++k) atomicAdd(g_phase_acc + k, ph[k]);
+#endif
     if (COUNT) flush_counters(c, fr.counters);
     if (st.fin_live) { // this wave's hand-offs are published: the persistent wf_long may stop once all are past here
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1526,6 +1560,25 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_LONG_WAVES) wf_long(RtDevScene sc
         t_idle = __builtin_amdgcn_s_memrealtime();
     }
     if (COUNT) flush_counters(c, fr.counters);
+}
+
+// debug (tools/phase_profile.py): the -DRT_PHASE_PROF build's per-phase wave
+// time of wf_finish_bvh since the last reset (zeros in other builds)
+extern "C" int rt_debug_phase_profile(unsigned long long *out8, int reset)
+{
+#ifdef RT_PHASE_PROF
+    if (hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_phase_acc), 8 * sizeof(unsigned long long)) != hipSuccess)
+        return RT_E_HIP;
+    if (reset) {
+        unsigned long long z[8] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_phase_acc), z, sizeof z) != hipSuccess) return RT_E_HIP;
+    }
+#else
+    (void)reset;
+    for (int k = 0; k < 8; ++k) out8[k] = 0;
+#endif
+    return RT_OK;
 }
 
 // ---------------------------------------------------------------- launcher

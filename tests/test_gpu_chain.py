@@ -106,14 +106,14 @@ def test_guard_counts_checks_and_no_mismatch():
 
 
 def test_guard_catches_a_corrupted_result():
-    """RT_DEBUG_CHECK_FAULT records every checked hit with a wrong triangle:
-    the KD re-trace must flag each of them (and only hits: misses stay)."""
+    """RT_DEBUG_CHECK_FAULT records every checked ray with a wrong result (a
+    hit's triangle index flipped, a miss as a hit of triangle 0): the KD
+    re-trace must flag every one of them."""
     run = helpers.GpuRun("cornell")
     rt.deviation_stats(reset=True)
     _render_calls(run, 128, 128, [4], check_interval=16, debug=4)
     dev = rt.deviation_stats(reset=True)
     assert dev["bounded_checked"] > 1000, dev
-    # the closed box: every ray hits something
     assert dev["bounded_mismatches"] == dev["bounded_checked"], dev
     assert any(v != 0.0 for v in dev["mismatch_ray"]), dev
 
