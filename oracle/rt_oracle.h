@@ -27,8 +27,14 @@ extern "C" {
 
 typedef struct OrScene OrScene;
 
-/* counters, same meaning as RT_CNT_* in include/isaklm_rt.h */
-#define OR_CNT_COUNT 40 /* [16] depth-limit cuts, [17..34] deep-path histogram, [35..39] hazard triggers */
+/* counters.  Only indices 0..9 (RT_CNT_NODE .. RT_CNT_MAXDEPTH) and 15
+ * (RT_CNT_DEEP_PUSH) have the meaning of the product's RT_CNT_* in
+ * include/isaklm_rt.h; the rest are the oracle's own and must not be
+ * compared element-wise with the product's array: [16] depth-limit cuts,
+ * [17..34] deep-path histogram (the product reports these through
+ * rt_deviation_stats), [35..39] hazard triggers (oracle.py HAZARDS; the
+ * product's 35..39 are timing / bounded-traversal counters). */
+#define OR_CNT_COUNT 40
 
 typedef struct OrOptions {
     int width, height;
