@@ -2014,9 +2014,16 @@ int debug_long_log(Workspace &w, unsigned long long *buf);
 int launch_whole(Workspace &w, int dev, const RtDevScene &sc, const RtDevFrame &fr, const RtDevCamera &cam,
                  hipStream_t stream, int long_depth, bool prof, bool overlap, uint32_t check_mask, int debug)
 {
-    (void)dev;
     const size_t slots = (size_t)fr.width * fr.height;
-    const int grid = 1536; // every wave slot at the finisher's 6 waves/SIMD (1,536 blocks of 4 waves)
+    // every wave slot at the finisher's occupancy (MI355X: 256 CUs x 4 SIMDs x 6 waves / 4 waves per
+    // block = 1,536 blocks), the last WF_LONG_BLOCKS of them left to wf_long
+    static int cus = 0;
+    if (!cus) {
+        hipDeviceProp_t prop;
+        cus = hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0 ? prop.multiProcessorCount
+                                                                                               : 256;
+    }
+    const int grid = cus * 4 * WF_FIN_BVH_WAVES / (WF_BLOCK / 64);
     if (ensure(w, slots, grid, 1) != 0) return -1;
     ChainKey key;
     memset(&key, 0, sizeof key);
