@@ -358,6 +358,7 @@ int rt_gbuffer_create(int w, int h, uint64_t skip, G_Buffer *g)
 int rt_gbuffer_destroy(G_Buffer *g)
 {
     if (!g) return RT_E_INVALID;
+    (void)rt_wavefront_join(nullptr); // (a chained render's tail may still write it)
     (void)hipFree(g->frame_buffer);
     (void)hipFree(g->squared_luminance);
     (void)hipFree(g->sample_count);
@@ -681,6 +682,7 @@ int rt_scene_prepare_counts(const Scene *ds, int node_count, int index_count, rt
 
 int rt_scene_release(rt_scene_t s)
 {
+    (void)rt_wavefront_join(nullptr); // (a chained render's tail may still read it)
     release(s);
     return RT_OK;
 }
