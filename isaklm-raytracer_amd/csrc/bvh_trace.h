@@ -237,173 +237,4 @@ __device__ __forceinline__ int trace_bvh(const RtDevScene &sc, const Vec3D o, co
     }
 }
 
-// ---- trace_bvh in resumable steps (wavefront.hip wf_finish_sm) ----------
-// The same operations in the same order as trace_bvh — the scene-box test,
-// the BVH query for s_min, the bounded KD descent with its leaf tests — cut
-// into steps of at most `cap` dependent node loads, so that a lane whose ray
-// is done can shade and start its next ray while the other lanes of its wave
-// still traverse (trace_bvh holds every lane until the wave's slowest ray is
-// done).  The state lives in registers; the stack is the lane's (LDS +
-// spill), used by the BVH query and then, from empty, by the KD descent.
-enum { TR_BVH = 1, TR_KD = 2, TR_HIT = 3, TR_MISS = 4 };
-struct RayTrav {
-    Vec3D r3;        // BVH: 1 / d (slab tests); KD: rt_recip_guard(d) (split distances)
-    float m;         // BVH: rt_ray_margin
-    float best;      // BVH: the smallest passing s so far; KD: s_min
-    float entry, exit_, root_exit;
-    uint32_t node;   // BVH: the current reference; KD: the node to load next
-    int sp;
-    int phase;       // TR_*
-};
-
-// the KD descent starts (from the root, with the scene box's interval)
-__device__ __forceinline__ void trav_kd_begin(RayTrav &t, Vec3D d, float s_min, float entry)
-{
-    t.best = s_min;
-    t.entry = entry;
-    t.exit_ = t.root_exit;
-    t.r3 = rt_v3(rt_recip_guard(d.x), rt_recip_guard(d.y), rt_recip_guard(d.z));
-    t.node = 0;
-    t.sp = 0;
-    t.phase = TR_KD;
-}
-
-// trace_bvh's first lines: the scene box, then the BVH query or (a ray
-// lying in a split plane, rt_bounded_ray) the plain KD traversal
-__device__ __forceinline__ void trav_begin(const RtDevScene &sc, RayTrav &t, Vec3D o, Vec3D d)
-{
-    float entry, exit_;
-    if (!bbox_hit(sc, o, d, entry, exit_)) {
-        t.phase = TR_MISS;
-        return;
-    }
-    t.root_exit = exit_;
-    if (rt_bounded_ray(o, d, sc.split_vals, sc.split_off)) {
-        t.m = rt_ray_margin(o.x, o.y, o.z, sc.bvh_scale);
-        t.r3 = rt_v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-        t.best = exit_;
-        t.entry = entry; // (kept for the KD descent)
-        t.node = 0;      // the BVH root (always an inner node)
-        t.sp = 0;
-        t.phase = TR_BVH;
-    } else {
-        trav_kd_begin(t, d, -INFINITY, entry);
-    }
-}
-
-// up to `cap` BVH node visits (bvh_bound's while-while descent), then the
-// leaf's tests and the pop; at the query's end s_min = best: no passing test
-// at all is a miss, else the KD descent begins
-template <typename STACK>
-__device__ __forceinline__ void trav_bvh_step(const RtDevScene &sc, RayTrav &t, Vec3D o, Vec3D d, STACK &stk, int cap)
-{
-    const Vec3D om = rt_v3(o.x + t.m, o.y + t.m, o.z + t.m), op = rt_v3(o.x - t.m, o.y - t.m, o.z - t.m);
-    auto pop = [&]() -> uint32_t {
-        while (t.sp > 0) {
-            --t.sp;
-            uint32_t n;
-            float tn;
-            stk.get(t.sp, n, tn);
-            if (tn <= t.best) return n;
-        }
-        return RT_BVH_EMPTY;
-    };
-    for (int k = 0; k < cap && !(t.node & RT_BVH_LEAF); ++k) {
-        const RtF4 *nd = sc.bvh_nodes + 4 * (size_t)t.node;
-        const RtF4 a = ldc4(nd), b = ldc4(nd + 1), c = ldc4(nd + 2);
-        const uint2 ch = ldc_u2(nd + 3);
-        float tn0, tn1;
-        const bool h0 = rt_bvh_box(a.x, a.y, a.z, a.w, b.x, b.y, om, op, t.r3, t.best, tn0) && ch.x != RT_BVH_EMPTY;
-        const bool h1 = rt_bvh_box(b.z, b.w, c.x, c.y, c.z, c.w, om, op, t.r3, t.best, tn1) && ch.y != RT_BVH_EMPTY;
-        if (h0 && h1) {
-            const bool second_first = tn1 < tn0;
-            stk.put(t.sp, second_first ? ch.x : ch.y, second_first ? tn0 : tn1);
-            ++t.sp;
-            t.node = second_first ? ch.y : ch.x;
-        } else if (h0 || h1) {
-            t.node = h0 ? ch.x : ch.y;
-        } else {
-            t.node = pop();
-        }
-    }
-    if (!(t.node & RT_BVH_LEAF)) return; // (descending: more next step)
-    if (t.node != RT_BVH_EMPTY) {
-        const uint32_t first = (t.node & ~RT_BVH_LEAF) >> 3, end = first + (t.node & 7u) + 1u;
-        float bx, by, bz;
-        Cnt cn;
-        (void)leaf_scan<false>(sc.bvh_a, sc.bvh_bary, first, end, o, d, t.best, bx, by, bz, cn);
-        t.node = pop();
-        if (t.node != RT_BVH_EMPTY) return;
-    }
-    // the query is over: s_min = best (the stack is empty)
-    if (!(t.best < t.root_exit)) {
-        t.phase = TR_MISS;
-        return;
-    }
-    trav_kd_begin(t, d, t.best, t.entry);
-}
-
-// up to `cap` KD node loads of trace_bvh's bounded descent, with the leaf
-// tests of the leaves reached; a hit ends the ray (TR_HIT, its triangle
-// index and barycentrics), an empty stack too (TR_MISS)
-template <typename STACK>
-__device__ __forceinline__ int trav_kd_step(const RtDevScene &sc, RayTrav &t, Vec3D o, Vec3D d, STACK &stk, int cap,
-                                            float &hbx, float &hby, float &hbz)
-{
-    for (int k = 0; k < cap; ++k) {
-        const uint2 nd = ldc_u2(sc.nodes + 2 * (size_t)t.node);
-        if ((nd.y & 3u) != RT_LEAF_TAG) {
-            const uint32_t axis = nd.y & 3u;
-            const float split = as_float(nd.x);
-            const float oax = axis == 0 ? o.x : (axis == 1 ? o.y : o.z);
-            const float dax = axis == 0 ? d.x : (axis == 1 ? d.y : d.z);
-            const float yax = axis == 0 ? t.r3.x : (axis == 1 ? t.r3.y : t.r3.z);
-            uint32_t near_c = t.node + 1, far_c = nd.y >> 2;
-            if (oax >= split) { // ray_behind_plane (:174-188)
-                near_c = nd.y >> 2;
-                far_c = t.node + 1;
-            }
-            const float tt = rt_div_by(split - oax, dax, yax); // intersect_plane (:190-210)
-            if (tt >= t.exit_ || tt < 0) {
-                t.node = near_c;
-            } else if (tt <= t.entry) {
-                t.node = far_c;
-            } else if (tt <= t.best) { // the near side holds no hit: its leaves' exits are <= tt
-                t.node = far_c;
-                t.entry = tt;
-            } else {
-                stk.put(t.sp, far_c, tt);
-                ++t.sp;
-                t.node = near_c;
-                t.exit_ = tt;
-            }
-            continue;
-        }
-        const uint32_t count = nd.y >> 2;
-        if (count > 0 && t.exit_ > t.best) {
-            // trace_leaf_node (:115-172): closest starts at the leaf's exit
-            float smallest = t.exit_;
-            float bx = 0.0f, by = 0.0f, bz = 0.0f;
-            Cnt cn;
-            const int be = leaf_scan<false>(sc.isect_a, sc.isect_bary, nd.x, nd.x + count, o, d, smallest, bx, by, bz, cn);
-            if (be >= 0) {
-                hbx = bx;
-                hby = by;
-                hbz = bz;
-                t.phase = TR_HIT;
-                return (int)ldc_u2(&sc.isect_bary[be].rd).y;
-            }
-        }
-        if (t.sp == 0) {
-            t.phase = TR_MISS;
-            return -1;
-        }
-        --t.sp;
-        t.node = stk.node_at(t.sp);
-        t.entry = stk.entry_at(t.sp);
-        t.exit_ = t.sp > 0 ? stk.entry_at(t.sp - 1) : t.root_exit;
-    }
-    return -1;
-}
-
 } // namespace rtk

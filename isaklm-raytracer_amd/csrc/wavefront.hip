@@ -95,10 +95,7 @@ static_assert(WF_BLOCK % WF_TBLOCK == 0 && WF_TBLOCK % 64 == 0, "WF_TBLOCK must 
 #define WF_BVH_WAVES 6  // wf_trace_bvh occupancy target
 #endif
 #ifndef WF_FIN_BVH_WAVES
-#define WF_FIN_BVH_WAVES 6 // wf_finish_bvh / wf_finish_sm occupancy target
-#endif
-#ifndef WF_FIN_SM
-#define WF_FIN_SM 0        // the whole-call finisher: 1 = wf_finish_sm (state machine), 0 = wf_finish_bvh
+#define WF_FIN_BVH_WAVES 6 // wf_finish_bvh occupancy target
 #endif
 // per-thread spill entries: the deeper of the KD stack (past WF_LDS_STACK) and the BVH stack (past WF_BVH_LDS)
 #define WF_SPILL_ENTRIES \
@@ -1195,206 +1192,6 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_FIN_BVH_WAVES) wf_finish_bvh(RtDe
     }
 }
 
-#ifndef WF_SM_CAP
-#define WF_SM_CAP 4        // wf_finish_sm: dependent node loads per traversal step
-#endif
-#ifndef WF_SM_SHADE
-#define WF_SM_SHADE 24     // wf_finish_sm: lanes with a finished ray before the wave shades them
-#endif
-
-// The whole-call finisher as a per-lane state machine (the default since
-// round 4; wf_finish_bvh is the counting build's and the queue tail's).
-// wf_finish_bvh runs one ray query per lane per loop trip, so a wave waits
-// for its slowest lane's ray every trip and then shades all lanes at once.
-// Here each lane is IDLE (no pixel), TRACING (trace_bvh cut into steps of
-// WF_SM_CAP dependent loads: bvh_trace.h trav_*) or SHADING (its ray is
-// done); every trip, tracing lanes advance one step, and once WF_SM_SHADE
-// lanes (or all that are not idle) have a finished ray, those lanes run
-// shade_step together and start their next rays.  Per pixel the events and
-// their arithmetic are exactly wf_finish_bvh's (trace_bvh, shade_step), so
-// every result is bit-identical; only the interleaving of lanes changes.
-__global__ void __launch_bounds__(WF_BLOCK, WF_FIN_BVH_WAVES) wf_finish_sm(RtDevScene sc, RtDevFrame fr, RtDevCamera cam,
-                                                                      WfState st, int q)
-{
-    __shared__ uint32_t s_node[WF_BVH_LDS * WF_BLOCK];
-    __shared__ float s_entry[WF_BVH_LDS * WF_BLOCK];
-    const int tid = threadIdx.x;
-    const int gtid = blockIdx.x * WF_BLOCK + tid;
-    Stack<WF_BVH_LDS> stk{s_node + tid, s_entry + tid, WF_BLOCK, st.spill + gtid, st.spill_threads};
-    Cnt c;
-    const uint32_t n1 = st.heavy_first ? st.counts[6 + 1] : 0u;
-    const uint32_t n = st.counts[6 + q] + n1;
-    uint32_t *fetch = st.counts + 4;
-    const int limit = fr.max_depth > 0 ? fr.max_depth : RT_WATCHDOG_BOUNCES;
-    const int lane = __lane_id();
-    unsigned long long *const ret_word = reinterpret_cast<unsigned long long *>(st.ret_ctr);
-    uint32_t *const ret_claimed = st.ret_ctr + 2;
-    if (st.long_return && lane == 0) // this wave is alive: wf_long may return pixels to it
-        __hip_atomic_fetch_add(ret_word, 1ull << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    enum { IDLE = 0, TRACING = 1, SHADING = 2, PENDING = 3 }; // PENDING: shaded, its next ray set up
-    PathRegs p;
-    p.slot = 0;
-    p.ro = p.rd = rt_v3(0, 0, 0);
-    RayTrav t;
-    t.phase = TR_MISS;
-    int state = IDLE, hit = -1;
-    float bx = 0.0f, by = 0.0f, bz = 0.0f;
-    bool exhausted = false;              // this lane found the path list empty
-    unsigned long long idle_since = 0;   // (lane 0) when the wave first had nothing to do
-    bool seated = false;                 // (lane 0) holds a linger seat
-    while (true) {
-        // ---- idle lanes take the next queued paths, or pixels wf_long returned
-        uint32_t load = 0xFFFFFFFFu; // the pixel this lane takes now
-        bool returned = false;
-        const bool need = state == IDLE && !exhausted;
-        const unsigned long long m = __ballot(need);
-        if (m) {
-            const int leader = __ffsll((long long)m) - 1;
-            uint32_t base = 0;
-            if (lane == leader) base = atomicAdd(fetch, (uint32_t)__popcll(m));
-            base = __shfl(base, leader);
-            if (need) {
-                const uint32_t e = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-                if (e >= n) exhausted = true;
-                else load = e < n1 ? st.q_slot[1][e] : st.q_slot[q][e - n1];
-            }
-        }
-        if (st.long_return) {
-            // (one compare-and-swap per wave)
-            const bool idle = state == IDLE && exhausted;
-            const unsigned long long im = __ballot(idle);
-            if (im) {
-                const int leader = __ffsll((long long)im) - 1;
-                uint32_t base = 0, got = 0;
-                if (lane == leader) {
-                    uint32_t c0 = __hip_atomic_load(ret_claimed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    const uint32_t r =
-                        (uint32_t)__hip_atomic_load(ret_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    const uint32_t want_n = (uint32_t)__popcll(im);
-                    const uint32_t take = r > c0 ? (r - c0 < want_n ? r - c0 : want_n) : 0u;
-                    if (take && __hip_atomic_compare_exchange_strong(ret_claimed, &c0, c0 + take, __ATOMIC_RELAXED,
-                                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                        base = c0;
-                        got = take;
-                    }
-                }
-                base = (uint32_t)__shfl((int)base, leader);
-                got = (uint32_t)__shfl((int)got, leader);
-                const uint32_t rank = (uint32_t)__popcll(im & ((1ull << lane) - 1ull));
-                if (idle && rank < got) {
-                    const uint32_t e = base + rank;
-                    unsigned long long v;
-                    do { // reserved by wf_long, its store may still be in flight
-                        v = __hip_atomic_load(st.ret_ring + e % st.long_cap, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    } while ((uint32_t)(v >> 32) != e + 1u);
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                    __hip_atomic_fetch_sub(st.ret_ctr + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    load = (uint32_t)v;
-                    returned = true;
-                }
-            }
-        }
-        bool start = state == PENDING; // the lane's next ray begins this trip (PENDING: set up by its shading)
-        if (load != 0xFFFFFFFFu) {
-            first_ray(st, fr, load, p);
-            if (returned) { // back from wf_long: no longer OUT; plus the passes chained calls queued meanwhile
-                const uint32_t owed = __hip_atomic_exchange(st.pxo + load, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                p.passes_left += (int)(owed & RT_PX_PASSES);
-            }
-            start = true;
-        }
-        // ---- the next ray of the lanes that start one (a scene-box miss is finished at once)
-        if (start) {
-            trav_begin(sc, t, p.ro, p.rd);
-            hit = -1;
-            state = t.phase == TR_MISS ? SHADING : TRACING;
-        }
-        if (!__any(state != IDLE)) {
-            if (!st.long_return) break; // every lane exhausted
-            // leave only while every reserved return is claimed (else: claim them next round), and
-            // while pixels are out in wf_long linger for them (bounded: st.linger)
-            int leave = 0;
-            if (lane == 0) {
-                if (idle_since == 0) idle_since = __builtin_amdgcn_s_memrealtime();
-                bool out = st.linger != 0 &&
-                           __hip_atomic_load(st.ret_ctr + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
-                if (out && !seated) {
-                    if (__hip_atomic_fetch_add(st.ret_ctr + 4, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
-                        WF_FIN_LINGER_WAVES)
-                        seated = true;
-                    else
-                        out = false;
-                }
-                unsigned long long w = __hip_atomic_load(ret_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const uint32_t cl = __hip_atomic_load(ret_claimed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if ((uint32_t)w == cl && (!out || __builtin_amdgcn_s_memrealtime() - idle_since > st.linger) &&
-                    __hip_atomic_compare_exchange_strong(ret_word, &w, w - (1ull << 32), __ATOMIC_RELAXED,
-                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-                    leave = 1;
-            }
-            if (__shfl(leave, 0)) break;
-            __builtin_amdgcn_s_sleep(8);
-            continue;
-        }
-        idle_since = 0;
-        // ---- traversal steps until WF_SM_SHADE lanes (or every lane that is not idle) have a finished ray
-        // (a tight loop over the traversal state alone: the path state waits outside it)
-        while (true) {
-            const unsigned long long tm = __ballot(state == TRACING);
-            if (!tm || __popcll(__ballot(state == SHADING)) >= WF_SM_SHADE) break;
-            if (state == TRACING) {
-                if (t.phase == TR_BVH) {
-                    trav_bvh_step(sc, t, p.ro, p.rd, stk, WF_SM_CAP);
-                } else {
-                    const int h = trav_kd_step(sc, t, p.ro, p.rd, stk, WF_SM_CAP, bx, by, bz);
-                    if (t.phase == TR_HIT) hit = h;
-                }
-                if (t.phase == TR_HIT || t.phase == TR_MISS) state = SHADING;
-            }
-        }
-        // ---- shading of the lanes with a finished ray
-        bool to_long = false;
-        if (state == SHADING) {
-            // run-time exactness guard: a deterministic sample of the rays, with the
-            // bounded result, is queued for wf_check's plain KD re-trace
-            if (st.chk) {
-                uint32_t h = p.slot * 0x9E3779B1u ^ (uint32_t)p.passes_left * 0x85EBCA77u ^
-                             (uint32_t)p.depth * 0xC2B2AE3Du ^ (p.shadow ? 0x27D4EB2Fu : 0u);
-                h ^= h >> 15;
-                h *= 0x2C1B3C6Du;
-                h ^= h >> 12;
-                if ((h & st.chk_mask) == 0u) {
-                    const uint32_t i = atomicAdd(st.chk_ctr, 1u);
-                    if (i < WF_CHECK_CAP) {
-                        st.chk[3 * (size_t)i] = RtF4{p.ro.x, p.ro.y, p.ro.z,
-                                                     __int_as_float(st.chk_fault ? (hit >= 0 ? hit ^ 1 : 0) : hit)};
-                        st.chk[3 * (size_t)i + 1] = RtF4{p.rd.x, p.rd.y, p.rd.z, bx};
-                        st.chk[3 * (size_t)i + 2] = RtF4{by, bz, 0.0f, 0.0f};
-                    }
-                }
-            }
-            const bool cam_ray = !p.shadow && p.depth == 1;
-            const bool want = shade_step<false>(sc, fr, cam, p, hit, bx, by, bz, limit, c);
-            // heavy-first ordering: a pixel whose camera ray enters glass (where the
-            // deep total-internal-reflection paths start) is marked for later calls
-            if (st.heavy_first && cam_ray && want && p.inside && !(st.heavy[p.slot] & 2u)) st.heavy[p.slot] |= 2u;
-            // a path deeper than long_depth goes on in wf_long (64 lanes per ray)
-            to_long = want && st.long_depth > 0 && p.depth > st.long_depth;
-            if (!want || to_long) store_regs(st, fr, p);
-            state = want && !to_long ? PENDING : IDLE;
-        }
-        if (__any(to_long)) {
-            const bool handed = publish_long_capped(st, to_long, p.slot, p.ro, p.rd);
-            if (to_long && !handed) state = PENDING; // the hand-off ring is full: the lane keeps its path
-        }
-    }
-    if (st.fin_live) { // this wave's hand-offs are published: the persistent wf_long may stop once all are past here
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        if (lane == 0) __hip_atomic_fetch_sub(st.fin_live, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
 // The run-time exactness guard's second half: every ray wf_finish_bvh
 // recorded is traced again with the plain KD traversal (trace(), i.e.
 // trace_ray, rt/trace_ray.cuh:244-318) and compared bit for bit with the
@@ -2095,11 +1892,7 @@ int launch_whole(Workspace &w, int dev, const RtDevScene &sc, const RtDevFrame &
     if (hipEventRecord(w.fin_ready, s) != hipSuccess) return -1;
     // (the finisher is launched before its wf_long: on a shared hardware queue
     // it then completes first, and wf_long finds its producers done)
-#if WF_FIN_SM
-    hipLaunchKernelGGL(wf_finish_sm, dim3(fgrid), dim3(WF_BLOCK), 0, s, sc, fr, cam, st, 0);
-#else
     hipLaunchKernelGGL(wf_finish_bvh<false>, dim3(fgrid), dim3(WF_BLOCK), 0, s, sc, fr, cam, st, 0);
-#endif
     if (hipGetLastError() != hipSuccess || !mark(3)) return -1;
     Pipe *lp = nullptr;
     if (long_return) {
