@@ -101,11 +101,11 @@ def traversal_of(args, rt):
 def bounded_kernel_bytes(c):
     """Bytes the bounded finisher's algorithm reads / writes (counters of a
     RT_TRAVERSAL_BOUNDED_COUNTED call; DESIGN.md "Roofline"): per ray query
-    64 B per BVH node (both child boxes), 16 B per plane test (BVH or KD),
-    56 B per barycentric record read, 8 B per KD node; per hit its 112-B
-    shading record and 64-B material; per sample the pixel's fb / sq / count
-    read and written (40 B)."""
-    return (64 * c["b_bvh_node"] + 16 * (c["b_bvh_tri"] + c["tri"]) + 56 * c["b_bary"] + 8 * c["node"] +
+    112 B per 4-wide BVH node (4 child boxes + references), 16 B per plane
+    test (BVH or KD), 56 B per barycentric record read, 8 B per KD node; per
+    hit its 112-B shading record and 64-B material; per sample the pixel's
+    fb / sq / count read and written (40 B)."""
+    return (112 * c["b_bvh_node"] + 16 * (c["b_bvh_tri"] + c["tri"]) + 56 * c["b_bary"] + 8 * c["node"] +
             176 * c["hit"] + 40 * c["sample"])
 
 
@@ -681,7 +681,7 @@ def main(argv=None, binding=None):
         roof["work_ratio"] = round(roof["algorithmic_bytes_per_sample"] / pb, 2)
         roof["product_GBps"] = round(pb * samples_per_s / 1e9, 1)
         roof["product_frac"] = round(pb * samples_per_s / 1e9 / HBM_PEAK_GBPS, 4)
-        roof["product_note"] = ("product_bytes_per_sample: per ray 64 B per BVH node, 16 B per plane test, 56 B per "
+        roof["product_note"] = ("product_bytes_per_sample: per ray 112 B per 4-wide BVH node, 16 B per plane test, 56 B per "
                                 "barycentric record, 8 B per KD node; per hit 176 B of shading records; per sample "
                                 "40 B of pixel state (bench.py bounded_kernel_bytes); frac = the counter-measured "
                                 "HBM traffic / peak, product_frac = these bytes at the timed rate / peak")

@@ -160,6 +160,98 @@ __device__ __forceinline__ float bvh_bound(const RtDevScene &sc, Vec3D o, Vec3D 
     }
 }
 
+// s_min of step 2 over the 4-wide collapse of the BVH (host/bvh_build.h
+// collapse_bvh4): the same conservative boxes and leaves as bvh_bound's
+// binary tree, so the same smallest passing s whatever the visiting order,
+// with half the dependent node loads (a node is one 128-B line: the 4 child
+// boxes SoA and their references).  The hit children go nearest-first: the
+// nearest is descended into, the others pushed farthest-first with their
+// entry distance, and popped only while that distance is <= the best s so far.
+#ifndef RT_BVH4
+#define RT_BVH4 1 // trace_bvh's s_min query on the 4-wide collapse (0: the binary tree)
+#endif
+template <bool COUNT, typename STACK>
+__device__ __forceinline__ float bvh4_bound(const RtDevScene &sc, Vec3D o, Vec3D d, float best, STACK &stk, Cnt &cn)
+{
+    const float m = rt_ray_margin(o.x, o.y, o.z, sc.bvh_scale);
+    const Vec3D om = rt_v3(o.x + m, o.y + m, o.z + m), op = rt_v3(o.x - m, o.y - m, o.z - m);
+    const Vec3D inv = rt_v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    int sp = 0;
+    uint32_t cur = 0; // the root (always an inner node)
+    auto pop = [&]() -> uint32_t {
+        while (sp > 0) {
+            --sp;
+            uint32_t n;
+            float tn;
+            stk.get(sp, n, tn);
+            if (tn <= best) return n;
+        }
+        return RT_BVH_EMPTY;
+    };
+    while (true) {
+        while (!(cur & RT_BVH_LEAF)) {
+            const RtF4 *nd = sc.bvh4 + 8 * (size_t)cur;
+            if (COUNT) cn.v[RT_CNT_B_BVH_NODE]++;
+            const RtF4 lx = ldc4(nd), ly = ldc4(nd + 1), lz = ldc4(nd + 2), hx = ldc4(nd + 3), hy = ldc4(nd + 4),
+                       hz = ldc4(nd + 5);
+            const uint4 rf = ldc_u4(reinterpret_cast<const uint32_t *>(nd + 6));
+            float t0, t1, t2, t3;
+            uint32_t r0 = rf.x, r1 = rf.y, r2 = rf.z, r3 = rf.w;
+            if (!(rt_bvh_box(lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, om, op, inv, best, t0) && r0 != RT_BVH_EMPTY)) {
+                t0 = INFINITY;
+                r0 = RT_BVH_EMPTY;
+            }
+            if (!(rt_bvh_box(lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, om, op, inv, best, t1) && r1 != RT_BVH_EMPTY)) {
+                t1 = INFINITY;
+                r1 = RT_BVH_EMPTY;
+            }
+            if (!(rt_bvh_box(lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, om, op, inv, best, t2) && r2 != RT_BVH_EMPTY)) {
+                t2 = INFINITY;
+                r2 = RT_BVH_EMPTY;
+            }
+            if (!(rt_bvh_box(lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, om, op, inv, best, t3) && r3 != RT_BVH_EMPTY)) {
+                t3 = INFINITY;
+                r3 = RT_BVH_EMPTY;
+            }
+            // sort the 4 (entry, ref) pairs by entry (misses last): a 5-comparator network
+            auto cswap = [](float &ta, uint32_t &ra, float &tb, uint32_t &rb) {
+                const bool sw = tb < ta || (ra == RT_BVH_EMPTY && rb != RT_BVH_EMPTY);
+                const float t = sw ? tb : ta, u = sw ? ta : tb;
+                const uint32_t r = sw ? rb : ra, q = sw ? ra : rb;
+                ta = t;
+                tb = u;
+                ra = r;
+                rb = q;
+            };
+            cswap(t0, r0, t1, r1);
+            cswap(t2, r2, t3, r3);
+            cswap(t0, r0, t2, r2);
+            cswap(t1, r1, t3, r3);
+            cswap(t1, r1, t2, r2);
+            if (r3 != RT_BVH_EMPTY) {
+                stk.put(sp, r3, t3);
+                ++sp;
+            }
+            if (r2 != RT_BVH_EMPTY) {
+                stk.put(sp, r2, t2);
+                ++sp;
+            }
+            if (r1 != RT_BVH_EMPTY) {
+                stk.put(sp, r1, t1);
+                ++sp;
+            }
+            cur = r0 != RT_BVH_EMPTY ? r0 : pop();
+        }
+        if (cur == RT_BVH_EMPTY) return best;
+        const uint32_t first = (cur & ~RT_BVH_LEAF) >> 3, end = first + (cur & 7u) + 1u;
+        if (COUNT) cn.v[RT_CNT_B_BVH_TRI] += end - first;
+        float bx, by, bz;
+        (void)leaf_scan<COUNT>(sc.bvh_a, sc.bvh_bary, first, end, o, d, best, bx, by, bz, cn);
+        cur = pop();
+        if (cur == RT_BVH_EMPTY) return best;
+    }
+}
+
 // trace_ray with the bound: returns the triangle index or -1 and the hit's
 // barycentric coordinates, bit-identical to trace().  COUNT (RT_TRAVERSAL_
 // BOUNDED_COUNTED): this traversal's own work — RT_CNT_RAY, RT_CNT_NODE / _TRI
@@ -175,7 +267,7 @@ __device__ __forceinline__ int trace_bvh(const RtDevScene &sc, const Vec3D o, co
     const float root_exit = exit_;
     float s_min = -INFINITY; // (the plain KD traversal)
     if (rt_bounded_ray(o, d, sc.split_vals, sc.split_off)) {
-        s_min = bvh_bound<COUNT>(sc, o, d, exit_, stk, c);
+        s_min = RT_BVH4 ? bvh4_bound<COUNT>(sc, o, d, exit_, stk, c) : bvh_bound<COUNT>(sc, o, d, exit_, stk, c);
         RT_PHASE_MID();
         if (!(s_min < root_exit)) return -1;
     }

@@ -337,4 +337,89 @@ int build_bvh(const Triangle *tris, int ntris, const RtF4 *plane, const RtIsectB
     return RT_OK;
 }
 
+// The 4-wide collapse (bvh_build.h): starting from a binary node's two
+// children, the inner child with the largest box surface is replaced by its
+// two children until there are 4 (or only leaves).  Child boxes and leaf
+// references are the binary tree's own; an inner child refers to its 4-wide
+// node.  Layout per node (8 RtF4, 128 B): lo.x, lo.y, lo.z, hi.x, hi.y, hi.z
+// of children 0..3 (one RtF4 each), then the 4 references, then padding;
+// unused slots hold RT_BVH_EMPTY.
+void collapse_bvh4(const std::vector<RtF4> &bin, std::vector<RtF4> &out4)
+{
+    out4.clear();
+    const size_t nb = bin.size() / 4;
+    if (nb == 0) return;
+    struct Child {
+        uint32_t ref;
+        float lo[3], hi[3];
+    };
+    auto child_of = [&](uint32_t node, int c) {
+        const RtF4 *nd = &bin[4 * (size_t)node];
+        Child ch;
+        memcpy(&ch.ref, c == 0 ? &nd[3].x : &nd[3].y, 4);
+        if (c == 0) {
+            ch.lo[0] = nd[0].x; ch.lo[1] = nd[0].y; ch.lo[2] = nd[0].z;
+            ch.hi[0] = nd[0].w; ch.hi[1] = nd[1].x; ch.hi[2] = nd[1].y;
+        } else {
+            ch.lo[0] = nd[1].z; ch.lo[1] = nd[1].w; ch.lo[2] = nd[2].x;
+            ch.hi[0] = nd[2].y; ch.hi[1] = nd[2].z; ch.hi[2] = nd[2].w;
+        }
+        return ch;
+    };
+    std::vector<int> idx(nb, -1);
+    std::vector<std::vector<Child>> wide; // per 4-wide node, its children (binary refs)
+    std::vector<uint32_t> order{0};
+    idx[0] = 0;
+    for (size_t q = 0; q < order.size(); ++q) {
+        const uint32_t b = order[q];
+        std::vector<Child> ch;
+        for (int c = 0; c < 2; ++c) {
+            const Child x = child_of(b, c);
+            if (x.ref != RT_BVH_EMPTY) ch.push_back(x);
+        }
+        while (ch.size() < 4) {
+            int pick = -1;
+            float area = -1.0f;
+            for (size_t k = 0; k < ch.size(); ++k) {
+                if (ch[k].ref & RT_BVH_LEAF) continue;
+                const float ex = ch[k].hi[0] - ch[k].lo[0], ey = ch[k].hi[1] - ch[k].lo[1], ez = ch[k].hi[2] - ch[k].lo[2];
+                const float a = ex * ey + ey * ez + ez * ex;
+                if (!(a <= area)) { // (NaN or larger: take it)
+                    area = a;
+                    pick = (int)k;
+                }
+            }
+            if (pick < 0) break;
+            const uint32_t inner = ch[(size_t)pick].ref;
+            ch.erase(ch.begin() + pick);
+            for (int c = 0; c < 2; ++c) {
+                const Child x = child_of(inner, c);
+                if (x.ref != RT_BVH_EMPTY) ch.push_back(x);
+            }
+        }
+        for (const Child &x : ch)
+            if (!(x.ref & RT_BVH_LEAF) && idx[x.ref] < 0) {
+                idx[x.ref] = (int)order.size();
+                order.push_back(x.ref);
+            }
+        wide.push_back(std::move(ch));
+    }
+    out4.assign(8 * wide.size(), RtF4{0, 0, 0, 0});
+    for (size_t i = 0; i < wide.size(); ++i) {
+        float *f = reinterpret_cast<float *>(&out4[8 * i]);
+        for (int k = 0; k < 4; ++k) {
+            uint32_t ref = RT_BVH_EMPTY;
+            if ((size_t)k < wide[i].size()) {
+                const Child &x = wide[i][(size_t)k];
+                ref = (x.ref & RT_BVH_LEAF) ? x.ref : (uint32_t)idx[x.ref];
+                for (int a = 0; a < 3; ++a) {
+                    f[4 * a + k] = x.lo[a];
+                    f[4 * (3 + a) + k] = x.hi[a];
+                }
+            }
+            memcpy(&f[4 * 6 + k], &ref, 4);
+        }
+    }
+}
+
 } // namespace rt_host

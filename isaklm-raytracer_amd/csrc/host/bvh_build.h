@@ -143,4 +143,10 @@ struct BvhHost {
 // are gathered into `order` by the caller
 int build_bvh(const Triangle *tris, int ntris, const RtF4 *plane, const RtIsectBary *bary, BvhHost &out);
 
+// the 4-wide collapse of a binary BVH (nodes as BvhHost::nodes): the same
+// boxes and leaves, half the levels — what the device's s_min query walks
+// (bvh_trace.h bvh_bound).  8 RtF4 per node (SoA of 4 children: lo.x, lo.y,
+// lo.z, hi.x, hi.y, hi.z, references, padding).
+void collapse_bvh4(const std::vector<RtF4> &bin, std::vector<RtF4> &out4);
+
 } // namespace rt_host

@@ -59,6 +59,8 @@ struct PreparedHost {
     // the conservative BVH that bounds each ray's first hit (bvh_build.h);
     // bvh_depth < 0: not built (the KD-only traversal runs)
     std::vector<RtF4> bvh_nodes;          // 4 per node
+    std::vector<RtF4> bvh4;               // the 4-wide collapse (bvh_build.h collapse_bvh4), 8 per node
+    int bvh4_stack = 0;                   // the deepest stack its query can build (must be < RT_BVH_STACK)
     std::vector<RtF4> bvh_a;              // BVH leaf-slot order
     std::vector<RtIsectBary> bvh_bary;    // BVH leaf-slot order
     float bvh_scale = 0.0f;

@@ -258,6 +258,25 @@ int prepare_host(const Triangle *tris, int ntris, const KD_Tree_Node *nodes, int
     const int brc = build_bvh(tris, ntris, ta.data(), tbary.data(), bvh);
     if (brc == RT_OK && bvh.depth < RT_BVH_STACK) {
         out.bvh_nodes = std::move(bvh.nodes);
+        collapse_bvh4(out.bvh_nodes, out.bvh4);
+        // the 4-wide query pushes up to 3 entries per level: the deepest stack any root-to-leaf
+        // path can build must fit the traversal stack (RT_BVH_STACK), else no bounded traversal
+        {
+            int worst = 0;
+            std::vector<std::pair<uint32_t, int>> st{{0u, 0}};
+            while (!st.empty()) {
+                const auto [node, depth] = st.back();
+                st.pop_back();
+                const uint32_t *ref = reinterpret_cast<const uint32_t *>(&out.bvh4[8 * (size_t)node + 6]);
+                int kids = 0;
+                for (int k = 0; k < 4; ++k) kids += ref[k] != RT_BVH_EMPTY;
+                const int below = depth + (kids > 0 ? kids - 1 : 0);
+                worst = below > worst ? below : worst;
+                for (int k = 0; k < 4; ++k)
+                    if (ref[k] != RT_BVH_EMPTY && !(ref[k] & RT_BVH_LEAF)) st.push_back({ref[k], below});
+            }
+            out.bvh4_stack = worst;
+        }
         out.bvh_a.resize(bvh.order.size());
         out.bvh_bary.resize(bvh.order.size());
 #pragma omp parallel for schedule(static)
@@ -266,7 +285,7 @@ int prepare_host(const Triangle *tris, int ntris, const KD_Tree_Node *nodes, int
             out.bvh_bary[k] = tbary[bvh.order[k]];
         }
         out.bvh_scale = bvh.scale;
-        out.bvh_depth = bvh.depth;
+        out.bvh_depth = out.bvh4_stack < RT_BVH_STACK ? bvh.depth : -1; // (too deep: the KD traversal alone)
         // the grid cells' start nodes: wf_long enters each deep bounce's KD traversal at the cell
         // of the ray's origin (coop_trace.h kd_origin_frontier)
         build_kd_starts(out, bounds);

@@ -17,6 +17,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <random>
 #include <vector>
 
@@ -195,6 +196,57 @@ float bvh_bound(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, float best, Wo
 }
 
 long long g_origin_mism = 0;
+long long g_bvh4_mism = 0;
+
+// the product's s_min query on the 4-wide collapse (bvh_trace.h bvh4_bound):
+// nearest-first, the other hit children pushed farthest-first
+float bvh4_bound(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, float best, Work &w)
+{
+    const float m = rt_ray_margin(o.x, o.y, o.z, h.bvh_scale);
+    const Vec3D om = rt_v3(o.x + m, o.y + m, o.z + m), op = rt_v3(o.x - m, o.y - m, o.z - m);
+    const Vec3D inv = rt_v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    struct E { uint32_t ref; float tn; };
+    std::vector<E> stk;
+    uint32_t cur = 0;
+    auto pop = [&]() -> uint32_t {
+        while (!stk.empty()) {
+            const E e = stk.back();
+            stk.pop_back();
+            if (e.tn <= best) return e.ref;
+        }
+        return RT_BVH_EMPTY;
+    };
+    while (true) {
+        while (!(cur & RT_BVH_LEAF)) {
+            ++w.bvh_nodes;
+            const float *f = reinterpret_cast<const float *>(&h.bvh4[8 * (size_t)cur]);
+            const uint32_t *rf = reinterpret_cast<const uint32_t *>(f + 24);
+            E c[4];
+            for (int k = 0; k < 4; ++k) {
+                float tn;
+                const bool hit = rt_bvh_box(f[k], f[4 + k], f[8 + k], f[12 + k], f[16 + k], f[20 + k], om, op, inv,
+                                            best, tn) && rf[k] != RT_BVH_EMPTY;
+                c[k] = hit ? E{rf[k], tn} : E{RT_BVH_EMPTY, INFINITY};
+            }
+            std::stable_sort(c, c + 4, [](const E &a, const E &b) {
+                const bool ea = a.ref == RT_BVH_EMPTY, eb = b.ref == RT_BVH_EMPTY;
+                return ea != eb ? eb : a.tn < b.tn;
+            });
+            for (int k = 3; k >= 1; --k)
+                if (c[k].ref != RT_BVH_EMPTY) stk.push_back(c[k]);
+            cur = c[0].ref != RT_BVH_EMPTY ? c[0].ref : pop();
+        }
+        if (cur == RT_BVH_EMPTY) return best;
+        const uint32_t first = (cur & ~RT_BVH_LEAF) >> 3, end = first + (cur & 7u) + 1u;
+        for (uint32_t e = first; e < end; ++e) {
+            float s, b[3];
+            ++w.bvh_tests;
+            if (test(h.bvh_a.data(), h.bvh_bary.data(), e, o, d, best, s, b)) best = s;
+        }
+        cur = pop();
+        if (cur == RT_BVH_EMPTY) return best;
+    }
+}
 
 // restatement of coop_trace.h kd_origin_frontier's replay: the descent along
 // the stored root path of a grid cell's start node, each decision checked
@@ -243,7 +295,13 @@ Hit bounded_trace(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, Work &w)
     float t1, t2;
     if (!scene_box(h, o, d, t1, t2)) return Hit{};
     if (!rt_bounded_ray(o, d, h.split_vals.data(), h.split_off)) return kd_trace(h, o, d, t1, t2, -INFINITY, w);
-    const float s_min = bvh_bound(h, o, d, t2, w);
+    Work w2;
+    const float s_bin = bvh_bound(h, o, d, t2, w2);
+    const float s_min = bvh4_bound(h, o, d, t2, w); // the product's query
+    if (memcmp(&s_bin, &s_min, 4) != 0) {
+#pragma omp atomic
+        ++g_bvh4_mism;
+    }
     if (!(s_min < t2)) return Hit{};
     return kd_trace(h, o, d, t1, t2, s_min, w);
 }
@@ -467,5 +525,7 @@ int main(int argc, char **argv)
     printf("bounded per ray: bvh nodes %.1f bvh tests %.1f kd nodes %.1f leaves %.2f tests %.1f\n", wb.bvh_nodes / R,
            wb.bvh_tests / R, wb.nodes / R, wb.leaves / R, wb.tests / R);
     printf("origin-cell entry: %lld resumed, mismatches vs the plain traversal %lld\n", g_origin_resumed, g_origin_mism);
-    return mism == 0 && g_origin_mism == 0 ? 0 : 1;
+    printf("4-wide s_min query: %zu nodes, deepest stack %d, s_min differing from the binary query %lld\n",
+           h.bvh4.size() / 8, h.bvh4_stack, g_bvh4_mism);
+    return mism == 0 && g_origin_mism == 0 && g_bvh4_mism == 0 ? 0 : 1;
 }
