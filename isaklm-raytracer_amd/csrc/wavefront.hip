@@ -1868,9 +1868,11 @@ int launch_whole(Workspace &w, int dev, const RtDevScene &sc, const RtDevFrame &
         // the hand-off state from zero (nothing of it is in flight now)
         if (join_all(w, stream) != 0) return -1;
         if (long_return) {
+            // (the rings' whole capacity: the workspace may be sized for an earlier, larger frame, and a
+            // stale tag beyond this frame's pixel count would look published to wf_long / the finishers)
             if (hipMemsetAsync(st.long_ctr, 0, 256, stream) != hipSuccess) return -1;
-            if (hipMemsetAsync(st.long_ent, 0, slots * 8, stream) != hipSuccess) return -1;
-            if (hipMemsetAsync(st.ret_ring, 0, slots * 8, stream) != hipSuccess) return -1;
+            if (hipMemsetAsync(st.long_ent, 0, (size_t)st.long_cap * 8, stream) != hipSuccess) return -1;
+            if (hipMemsetAsync(st.ret_ring, 0, (size_t)st.long_cap * 8, stream) != hipSuccess) return -1;
             if (hipMemsetAsync(st.ret_ctr, 0, 256, stream) != hipSuccess) return -1;
         }
         if (st.long_log && hipMemsetAsync(long_log_buf, 0, 8 * 4 * 65536, stream) != hipSuccess) return -1;
@@ -2150,8 +2152,9 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
     if (join_all(w, stream) != 0) return -1;
     w.chain_open = false;
     if (long_depth > 0) {
-        // (the ring from zero: a pixel is handed over at most once per call here)
-        if (hipMemsetAsync(lst.long_ent, 0, slots * 8, stream) != hipSuccess) return -1;
+        // (the ring from zero — its whole capacity, see launch_whole; a pixel is handed over at most once
+        // per call here)
+        if (hipMemsetAsync(lst.long_ent, 0, (size_t)lst.long_cap * 8, stream) != hipSuccess) return -1;
         if (hipMemsetAsync(lst.long_ctr, 0, 256, stream) != hipSuccess) return -1;
     }
     // fork: every pipeline stream starts after the caller's stream

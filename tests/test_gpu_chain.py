@@ -133,3 +133,20 @@ def test_megakernel_two_streams_equal_serial():
     rb, _, _ = run.render(W, H, 4, kernel=rt.KERNEL_MEGA, seed_skip=W * H)
     helpers.assert_bitwise(ga.download(), ra, what="megakernel stream 1")
     helpers.assert_bitwise(gb.download(), rb, what="megakernel stream 2")
+
+
+def test_small_frame_after_a_large_one(tmp_path):
+    """The per-device workspace is sized by the largest frame so far; a later,
+    smaller frame must not see that frame's hand-off ring entries (a stale
+    sequence tag beyond the small frame's pixel count looks published).  A
+    1080p room2m call, then the 600-unit light guide (every path past 64
+    bounces goes through the ring, many more entries than pixels) against the
+    oracle."""
+    big = helpers.GpuRun("room2m")
+    big.render(1920, 1080, [2], kernel=WF)
+    trap = helpers.make_trap_scene(str(tmp_path / "t"), 600.0)
+    run = helpers.GpuRun(trap)
+    W, H, P = 64, 48, 4
+    gpu, _, _ = run.render(W, H, P, calls=2, kernel=WF)
+    ref, _ = helpers.oracle_render(trap, W, H, P, calls=2)
+    helpers.assert_bitwise(gpu, ref, what="light guide after a 1080p frame")
