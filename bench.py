@@ -142,9 +142,11 @@ def parse_args(argv=None):
     ap.add_argument("--overlap", type=int, choices=[0, 1], default=1,
                     help="chained rt_render calls (RtOptions.overlap): a call's deep-path tail overlaps the next "
                          "call; the timed region ends with the tonemap, which joins them (identical images)")
+    ap.add_argument("--debug", type=int, default=0,
+                    help="RtOptions.debug (diagnostics: 1 = per-call hand-off log on stderr)")
     ap.add_argument("--check-interval", type=int, default=0,
                     help="the bounded traversal's run-time guard: 1 ray in N re-traced by the KD traversal "
-                         "(RtOptions.check_interval; 0 = the library default 1024, < 0 off)")
+                         "(RtOptions.check_interval; 0 = the library default 4096, < 0 off)")
     ap.add_argument("--min-samples", type=int, default=100)
     ap.add_argument("--max-depth", type=int, default=0, help="0 = unbounded (reference)")
     ap.add_argument("--scene-dir", default=os.environ.get("RT_SCENE_DIR", os.path.join(ROOT, "build", "scenes")))
@@ -506,7 +508,8 @@ def main(argv=None, binding=None):
     kernel = rt.KERNEL_WAVEFRONT if args.kernel == "wavefront" else rt.KERNEL_MEGA
     wavefront = kernel == rt.KERNEL_WAVEFRONT
     render_kw = dict(adaptive=args.adaptive, min_samples=args.min_samples, max_depth=args.max_depth, kernel=kernel,
-                     traversal=traversal_of(args, rt), check_interval=args.check_interval)
+                     traversal=traversal_of(args, rt), check_interval=args.check_interval,
+                     debug=args.debug)
     bounded = wavefront and args.traversal == "bounded"
     spc = max(1, args.steps_per_call)
     profiles = []
@@ -724,7 +727,7 @@ def main(argv=None, binding=None):
             "deep_pushes": c["deep_push"], "deep_pushes_scope": "one extra counted call of the same options",
             "bounded_checked": dev.get("bounded_checked"), "bounded_mismatches": dev.get("bounded_mismatches"),
             "bounded_check_note": "run-time guard of the BVH-bounded traversal: a deterministic 1-in-"
-                                  f"{args.check_interval or 1024} sample of the finisher's rays, re-traced by the "
+                                  f"{args.check_interval or 4096} sample of the finisher's rays, re-traced by the "
                                   "plain KD traversal (trace_ray) inside the timed region and compared bit for bit",
             "note": "paths cut by the 2^24-1-bounce watchdog (SURVEY H8; the reference loops unbounded), paths cut "
                     "by max_depth, the longest path in bounces and the histogram of paths that ended at depth >= 64; "

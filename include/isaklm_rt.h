@@ -465,7 +465,7 @@ typedef struct RtOptions {
      * complete when its launches are (rt/main.cu:114-155). */
     int overlap;
     /* run-time exactness guard of the bounded traversal (default render):
-     * 1 ray in check_interval (rounded up to a power of two; 0 = 1024) of
+     * 1 ray in check_interval (rounded up to a power of two; 0 = 4096) of
      * those the finisher traces is recorded with its result and traced again
      * by the plain KD traversal after the call; disagreements are counted in
      * RtDeviations.bounded_mismatches.  < 0: off. */

@@ -95,7 +95,7 @@ static_assert(WF_BLOCK % WF_TBLOCK == 0 && WF_TBLOCK % 64 == 0, "WF_TBLOCK must 
 #define WF_BVH_WAVES 6  // wf_trace_bvh occupancy target
 #endif
 #ifndef WF_FIN_BVH_WAVES
-#define WF_FIN_BVH_WAVES 6 // wf_finish_bvh occupancy target
+#define WF_FIN_BVH_WAVES 5 // wf_finish_bvh occupancy target (5: +3 % over 6 with the 4-wide s_min query, profiles/r04)
 #endif
 // per-thread spill entries: the deeper of the KD stack (past WF_LDS_STACK) and the BVH stack (past WF_BVH_LDS)
 #define WF_SPILL_ENTRIES \
@@ -119,7 +119,17 @@ static_assert(WF_BLOCK % WF_TBLOCK == 0 && WF_TBLOCK % 64 == 0, "WF_TBLOCK must 
 // Either strands pixels instead of hanging the GPU.
 #define WF_LONG_IDLE 2000000000ull
 #define WF_LONG_IDLE_PERSIST 60000000000ull
-#define WF_CHECK_INTERVAL_DEFAULT 1024u // RtOptions.check_interval: 1 ray in this many re-traced by the KD traversal
+// an idle persistent wf_long wave of an open chain stays until no entry has
+// been reserved (for any wave) for this long (50 ms) AND no wave runs a path:
+// the next calls' deep paths (WfState.chain_flag).  The grid leaves as a whole
+// — one whose idle waves left while a few ran 10^4-bounce samples on (a call's
+// tail can go 50 ms without a hand-off) served the next calls with those few
+// waves, its stream-queued successor blocked behind them.
+#define WF_LONG_CHAIN_IDLE 5000000ull
+// RtOptions.check_interval: 1 ray in this many re-traced by the KD traversal
+// (a KD re-trace costs ~50 bounded queries: 1024 took 4 % of a 256-pass
+// room2m call, 4096 ~1 %, and still checks ~2M rays in the 20-step bench)
+#define WF_CHECK_INTERVAL_DEFAULT 4096u
 #define WF_CHECK_CAP (1u << 20)         // cross-check records per call (more are dropped, not counted)
 // per-pixel hand-off word (WfState.pxo): a pixel handed to wf_long is OUT
 // until a finisher takes it back or wf_long finishes it (LONGDONE: its state
@@ -172,6 +182,13 @@ struct WfState {
     // the persistent wf_long's producers: finisher waves of its call not yet
     // past their last hand-off (nullptr: wf_long runs in host-kicked slices)
     uint32_t *fin_live;
+    // 1 while a chain of calls is open (set by chained calls, cleared by its
+    // drain): an idle persistent wf_long wave then stays up to WF_LONG_CHAIN_IDLE
+    // for the later calls' deep paths instead of leaving at its first idle
+    // moment (which left the next calls' entries to the few waves still busy,
+    // the stream-queued successor blocked behind them).  Bounded: the drain's
+    // clear may sit behind this very wf_long when streams share a hardware queue.
+    uint32_t *chain_flag;
     // pixels whose path went to wf_long in the previous call run first (their
     // passes are the call's longest chains): wf_start puts them on path list 1,
     // the whole-call finisher takes list 1 before list 0
@@ -1038,26 +1055,15 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_FIN_BVH_WAVES) wf_finish_bvh(RtDe
 #ifdef RT_PHASE_PROF
         const unsigned long long t0 = __builtin_amdgcn_s_memtime();
 #endif
-        const bool need = !active && !exhausted;
-        const unsigned long long m = __ballot(need);
-        if (m) {
-            const int leader = __ffsll((long long)m) - 1;
-            uint32_t base = 0;
-            if (lane == leader) base = atomicAdd(fetch, (uint32_t)__popcll(m));
-            base = __shfl(base, leader);
-            if (need) {
-                const uint32_t e = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-                if (e >= n) {
-                    exhausted = true;
-                } else {
-                    active = true;
-                    first_ray(st, fr, e < n1 ? st.q_slot[1][e] : st.q_slot[q][e - n1], p);
-                }
-            }
-        }
         if (st.long_return) {
-            // idle lanes take pixels wf_long returned (one compare-and-swap per wave)
-            const bool idle = !active && exhausted;
+            // free lanes take pixels wf_long returned BEFORE fresh ones (one
+            // compare-and-swap per wave): a returned pixel is mid-chain — it may
+            // carry the passes of chained calls that skipped it (pxo) — and
+            // started only at the end of the path list it would end the call late.
+            // Chained calls (no linger): only while the path list lasts — the call's
+            // tail leaves later returns to the next call's (or the drain's) finisher
+            const bool chained = st.linger == 0ull;
+            const bool idle = !active && !(chained && exhausted);
             const unsigned long long im = __ballot(idle);
             if (im) {
                 const int leader = __ffsll((long long)im) - 1;
@@ -1067,7 +1073,9 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_FIN_BVH_WAVES) wf_finish_bvh(RtDe
                     const uint32_t r =
                         (uint32_t)__hip_atomic_load(ret_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     const uint32_t want_n = (uint32_t)__popcll(im);
-                    const uint32_t take = r > c0 ? (r - c0 < want_n ? r - c0 : want_n) : 0u;
+                    uint32_t take = r > c0 ? (r - c0 < want_n ? r - c0 : want_n) : 0u;
+                    if (take && chained && __hip_atomic_load(fetch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= n)
+                        take = 0u;
                     if (take && __hip_atomic_compare_exchange_strong(ret_claimed, &c0, c0 + take, __ATOMIC_RELAXED,
                                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
                         base = c0;
@@ -1091,13 +1099,38 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_FIN_BVH_WAVES) wf_finish_bvh(RtDe
                     const uint32_t owed = __hip_atomic_exchange(st.pxo + (uint32_t)v, 0u, __ATOMIC_RELAXED,
                                                                 __HIP_MEMORY_SCOPE_AGENT);
                     p.passes_left += (int)(owed & RT_PX_PASSES);
+                    if (owed & RT_PX_PASSES) { // (statistics for RT_DEBUG_CALL_LOG: most passes owed, pixels owed)
+                        __hip_atomic_fetch_max(st.ret_ctr + 5, owed & RT_PX_PASSES, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_fetch_add(st.ret_ctr + 6, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                }
+            }
+        }
+        const bool need = !active && !exhausted;
+        const unsigned long long m = __ballot(need);
+        if (m) {
+            const int leader = __ffsll((long long)m) - 1;
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(fetch, (uint32_t)__popcll(m));
+            base = __shfl(base, leader);
+            if (need) {
+                const uint32_t e = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+                if (e >= n) {
+                    exhausted = true;
+                } else {
+                    active = true;
+                    first_ray(st, fr, e < n1 ? st.q_slot[1][e] : st.q_slot[q][e - n1], p);
                 }
             }
         }
         if (!__any(active)) {
             if (!st.long_return) break; // every lane exhausted
+            if (st.linger == 0ull) { // chained: returns left are the next call's (or the drain's)
+                if (lane == 0) __hip_atomic_fetch_sub(ret_word, 1ull << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
             // leave only while every reserved return is claimed (else: claim them next round), and
-            // while pixels are out in wf_long linger for them (bounded: WF_FIN_LINGER)
+            // while pixels are out in wf_long linger for them (bounded: st.linger)
             int leave = 0;
             if (lane == 0) {
                 if (idle_since == 0) idle_since = __builtin_amdgcn_s_memrealtime();
@@ -1396,6 +1429,7 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_LONG_WAVES) wf_long(RtDevScene sc
     uint32_t *const reserved = st.long_ctr, *const claimed = st.long_ctr + 1, *const running = st.long_ctr + 3;
     const bool persist = st.fin_live != nullptr;
     unsigned long long t_idle = __builtin_amdgcn_s_memrealtime();
+    uint32_t r_seen = 0;
     while (true) {
         // ---- claim the next published entry (lane 0): its tag and ray are read
         // before the claim (a claimed ring slot may be reused at once)
@@ -1406,11 +1440,18 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_LONG_WAVES) wf_long(RtDevScene sc
             while (true) {
                 // (producers first: once they are all past their last hand-off,
                 // `reserved` read after this acquire holds every entry)
-                const bool done = persist && __hip_atomic_load(st.fin_live, __ATOMIC_RELAXED,
-                                                               __HIP_MEMORY_SCOPE_AGENT) == 0u;
+                const bool done =
+                    persist && __hip_atomic_load(st.fin_live, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u &&
+                    (__hip_atomic_load(st.chain_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u ||
+                     (__builtin_amdgcn_s_memrealtime() - t_idle > WF_LONG_CHAIN_IDLE &&
+                      __hip_atomic_load(running, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u));
                 if (done) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                 e = __hip_atomic_load(claimed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 const uint32_t r = __hip_atomic_load(reserved, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (r != r_seen) { // entries still flowing (to any wave): not idle
+                    r_seen = r;
+                    t_idle = __builtin_amdgcn_s_memrealtime();
+                }
                 if (e < r) {
                     const uint32_t k = e % st.long_cap;
                     const unsigned long long v =
@@ -1516,11 +1557,21 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_LONG_WAVES) wf_long(RtDevScene sc
                     }
                 }
                 // return mode: the deep sample is over once the pixel's next one starts (depth 1);
-                // the pixel goes back to the finishers if one is still alive to take it
+                // the pixel goes back to the finishers if one is still alive to take it.  While a
+                // chain is open: always — this call's, the next call's or the chain's drain
+                // finisher takes it (a finisher in its tail takes none: a returned pixel's whole
+                // remaining chain would hold up the call's end and the next call's start).  The
+                // drain finisher lingers (WF_FIN_LINGER) while a pixel is out, so a return
+                // reserved just as its clear of the flag lands is still taken.
                 if (want && st.long_return && p.depth == 1 && !p.shadow) {
                     unsigned long long *const ret_word = reinterpret_cast<unsigned long long *>(st.ret_ctr);
+                    if (st.linger == 0ull &&
+                        __hip_atomic_load(st.chain_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+                        want = 2;
+                        ret_e = (uint32_t)__hip_atomic_fetch_add(ret_word, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
                     unsigned long long w = __hip_atomic_load(ret_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    while ((w >> 32) != 0ull) {
+                    while (want != 2 && (w >> 32) != 0ull) {
                         if (__hip_atomic_compare_exchange_strong(ret_word, &w, w + 1ull, __ATOMIC_RELAXED,
                                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
                             want = 2;
@@ -1633,6 +1684,12 @@ struct Workspace {
     unsigned long long call_seq = 0;
     bool chain_open = false; // the last call was a whole-call call with RtOptions.overlap
     ChainKey key{};
+    // the open chain's last call (its drain runs with them)
+    RtDevScene last_sc{};
+    RtDevFrame last_fr{};
+    RtDevCamera last_cam{};
+    int last_long_depth = 0;
+    int last_debug = 0;
     RtProfile prof{};        // last profiled call
 };
 
@@ -1678,6 +1735,8 @@ int ensure_streams(Workspace &w, int npipes)
     return 0;
 }
 
+int launch_drain(Workspace &w);
+
 int ensure(Workspace &w, size_t slots, int grid, int npipes)
 {
     if (ensure_streams(w, npipes > WF_PIPES_DEFAULT ? npipes : WF_PIPES_DEFAULT) != 0) return -1;
@@ -1685,7 +1744,9 @@ int ensure(Workspace &w, size_t slots, int grid, int npipes)
     // traversal stack spill for the pipelines in use (at least the default 3)
     const int spill_pipes = npipes > WF_PIPES_DEFAULT ? npipes : WF_PIPES_DEFAULT;
     if (w.blob) {
-        (void)hipDeviceSynchronize(); // (a chained call's wf_long may still use the old blob)
+        // (an open chain drained first: its wf_longs use the old blob until then)
+        if (launch_drain(w) != 0) return -1;
+        (void)hipDeviceSynchronize();
         (void)hipFree(w.blob);
     }
     w.blob = nullptr;
@@ -1761,6 +1822,7 @@ int ensure(Workspace &w, size_t slots, int grid, int npipes)
         st.linger = WF_FIN_LINGER;
         st.pxo = (uint32_t *)(b + o_px);
         st.fin_live = nullptr;
+        st.chain_flag = (uint32_t *)(b + o_ctl + 128);
         st.heavy = (uint8_t *)(b + o_hv);
         st.heavy_first = 0;
         st.chk = nullptr; // (whole-call mode only: launch_whole)
@@ -1781,9 +1843,10 @@ float elapsed_ms(hipEvent_t a, hipEvent_t b)
 }
 
 // `stream` waits for every call's device work on this workspace (the
-// pipelines' last launches and every wf_long) — stream NULL: the host does
+// pipelines' last launches and every wf_long), an open chain drained first
 int join_all(Workspace &w, hipStream_t stream)
 {
+    if (launch_drain(w) != 0) return -1;
     for (int pi = 0; pi < WF_MAX_PIPES; ++pi) {
         Pipe &p = w.pipe[pi];
         if (p.joined && hipStreamWaitEvent(stream, p.join, 0) != hipSuccess) return -1;
@@ -1812,8 +1875,8 @@ int launch_whole(Workspace &w, int dev, const RtDevScene &sc, const RtDevFrame &
                  hipStream_t stream, int long_depth, bool prof, bool overlap, uint32_t check_mask, int debug)
 {
     const size_t slots = (size_t)fr.width * fr.height;
-    // every wave slot at the finisher's occupancy (MI355X: 256 CUs x 4 SIMDs x 6 waves / 4 waves per
-    // block = 1,536 blocks), the last WF_LONG_BLOCKS of them left to wf_long
+    // every wave slot at the finisher's occupancy (MI355X: 256 CUs x 4 SIMDs x 5 waves / 4 waves per
+    // block = 1,280 blocks), the last WF_LONG_BLOCKS of them left to wf_long
     static int cus = 0;
     if (!cus) {
         hipDeviceProp_t prop;
@@ -1821,7 +1884,6 @@ int launch_whole(Workspace &w, int dev, const RtDevScene &sc, const RtDevFrame &
                                                                                                : 256;
     }
     const int grid = cus * 4 * WF_FIN_BVH_WAVES / (WF_BLOCK / 64);
-    if (ensure(w, slots, grid, 1) != 0) return -1;
     ChainKey key;
     memset(&key, 0, sizeof key);
     key.nodes = sc.nodes;
@@ -1841,6 +1903,10 @@ int launch_whole(Workspace &w, int dev, const RtDevScene &sc, const RtDevFrame &
     key.tolerance = fr.tolerance;
     key.cam = cam;
     const bool chained = overlap && w.chain_open && !fr.reset && memcmp(&key, &w.key, sizeof key) == 0;
+    // a fresh call: an open chain drained and every earlier call's work on the
+    // workspace first (before a larger frame's workspace replaces the old one)
+    if (!chained && join_all(w, stream) != 0) return -1;
+    if (ensure(w, slots, grid, 1) != 0) return -1;
     Pipe &pp = w.pipe[0];
     WfState st = pp.st;
     const int long_return = long_depth > 0 ? 1 : 0;
@@ -1864,9 +1930,7 @@ int launch_whole(Workspace &w, int dev, const RtDevScene &sc, const RtDevFrame &
     const uint32_t k = (uint32_t)(w.call_seq % 8);
     st.fin_live = long_return ? w.fin_live + k : nullptr;
     if (!chained) {
-        // a fresh call: every earlier call's work on the workspace first, then
         // the hand-off state from zero (nothing of it is in flight now)
-        if (join_all(w, stream) != 0) return -1;
         if (long_return) {
             // (the rings' whole capacity: the workspace may be sized for an earlier, larger frame, and a
             // stale tag beyond this frame's pixel count would look published to wf_long / the finishers)
@@ -1888,6 +1952,7 @@ int launch_whole(Workspace &w, int dev, const RtDevScene &sc, const RtDevFrame &
     if (st.fin_live && hipMemsetD32Async((hipDeviceptr_t)st.fin_live, (int)(fgrid * (WF_BLOCK / 64)), 1, s) != hipSuccess)
         return -1;
     if (st.chk && hipMemsetAsync(st.chk_ctr, 0, 4, s) != hipSuccess) return -1;
+    if (long_return && hipMemsetD32Async((hipDeviceptr_t)st.chain_flag, overlap ? 1 : 0, 1, s) != hipSuccess) return -1;
     const int tiles = ((fr.width + 15) / 16) * ((fr.height + 15) / 16);
     hipLaunchKernelGGL(wf_start<false>, dim3(tiles), dim3(WF_BLOCK), 0, s, fr, cam, st, 0, 1);
     if (!mark(1) || !mark(2)) return -1;
@@ -1916,8 +1981,14 @@ int launch_whole(Workspace &w, int dev, const RtDevScene &sc, const RtDevFrame &
     // call overlaps the next one, after its wf_long
     if (hipStreamWaitEvent(stream, pp.join, 0) != hipSuccess) return -1;
     if (!overlap && lp && hipStreamWaitEvent(stream, lp->long_done, 0) != hipSuccess) return -1;
-    w.chain_open = overlap;
+    w.chain_open = overlap && long_return;
     w.key = key;
+    w.last_sc = sc;
+    w.last_fr = fr;
+    w.last_fr.reset = 0;
+    w.last_cam = cam;
+    w.last_long_depth = long_depth;
+    w.last_debug = debug;
     if (prof) {
         if (hipEventRecord(w.ev1, stream) != hipSuccess || hipEventSynchronize(pp.ev[4]) != hipSuccess ||
             hipEventSynchronize(w.ev1) != hipSuccess)
@@ -1935,16 +2006,73 @@ int launch_whole(Workspace &w, int dev, const RtDevScene &sc, const RtDevFrame &
         (void)hipStreamSynchronize(s);
         timespec ts;
         clock_gettime(CLOCK_MONOTONIC, &ts);
-        uint32_t lc[4] = {}, rc4[5] = {};
+        uint32_t lc[4] = {}, rc4[7] = {};
         (void)hipMemcpy(lc, st.long_ctr, sizeof lc, hipMemcpyDeviceToHost);
         (void)hipMemcpy(rc4, st.ret_ctr, sizeof rc4, hipMemcpyDeviceToHost);
         fprintf(stderr,
                 "[wf] call %llu%s finisher done t %.4f; long entries %u claimed %u running %u; returns reserved %u "
-                "claimed %u, finisher waves alive %u, pixels out %u\n",
+                "claimed %u, finisher waves alive %u, pixels out %u; owed passes: most %u, pixels %u\n",
                 w.call_seq, chained ? " (chained)" : "", ts.tv_sec + ts.tv_nsec * 1e-9, lc[0], lc[1], lc[3], rc4[0],
-                rc4[2], rc4[1], rc4[3]);
+                rc4[2], rc4[1], rc4[3], rc4[5], rc4[6]);
     }
     if (st.long_log && !overlap) return debug_long_log(w, long_log_buf);
+    return 0;
+}
+
+// The drain of an open chain (join_all, i.e. rt_join and every reader of the
+// frame, or the next call that does not continue it): a chained call's
+// finisher leaves pixels wf_long hands back after its path list ran out to the
+// next call; here one more finisher with an empty path list takes them, runs
+// their remaining passes (handing deep samples to its own wf_long again) and
+// lingers while any pixel is still out.  Enqueued on pipeline 0 after the
+// chain's last finisher; join_all then waits for it and every wf_long.
+int launch_drain(Workspace &w)
+{
+    if (!w.chain_open) return 0;
+    w.chain_open = false;
+    const RtDevFrame &fr = w.last_fr;
+    const size_t slots = (size_t)fr.width * fr.height;
+    Pipe &pp = w.pipe[0];
+    WfState st = pp.st;
+    st.long_depth = w.last_long_depth;
+    st.long_return = 1;
+    st.heavy_first = 1;
+    st.linger = WF_FIN_LINGER; // (a pixel still out after it: wf_long runs it to the end)
+    st.chk = nullptr;
+    st.chk_mask = 0;
+    st.chk_ctr = w.chk_ctr;
+    st.chk_fault = 0;
+    st.long_log = nullptr;
+    int fgrid = (int)((slots + WF_BLOCK - 1) / WF_BLOCK);
+    fgrid = fgrid > w.grid - WF_LONG_BLOCKS ? w.grid - WF_LONG_BLOCKS : fgrid;
+    st.fin_live = w.fin_live + (uint32_t)(w.call_seq % 8);
+    ++w.call_seq;
+    const hipStream_t s = pp.stream;
+    // an empty path list (counts[6], counts[7] = 0), no linger seat taken yet
+    if (hipMemsetAsync(st.counts, 0, 256, s) != hipSuccess) return -1;
+    if (hipMemsetAsync(st.ret_ctr + 4, 0, 4, s) != hipSuccess) return -1;
+    if (hipMemsetAsync(st.chain_flag, 0, 4, s) != hipSuccess) return -1; // the chain's wf_longs may leave once idle
+    if (hipMemsetD32Async((hipDeviceptr_t)st.fin_live, (int)(fgrid * (WF_BLOCK / 64)), 1, s) != hipSuccess) return -1;
+    if (hipEventRecord(w.fin_ready, s) != hipSuccess) return -1;
+    hipLaunchKernelGGL(wf_finish_bvh<false>, dim3(fgrid), dim3(WF_BLOCK), 0, s, w.last_sc, fr, w.last_cam, st, 0);
+    if (hipGetLastError() != hipSuccess) return -1;
+    Pipe &lp = w.pipe[1 + (int)(w.call_seq & 1)];
+    if (hipStreamWaitEvent(lp.stream, w.fin_ready, 0) != hipSuccess) return -1;
+    hipLaunchKernelGGL(wf_long<false>, dim3(WF_LONG_BLOCKS), dim3(WF_BLOCK), 0, lp.stream, w.last_sc, fr, w.last_cam, st, 1);
+    if (hipGetLastError() != hipSuccess) return -1;
+    if (hipEventRecord(lp.long_done, lp.stream) != hipSuccess) return -1;
+    lp.long_rec = true;
+    if (hipEventRecord(pp.join, s) != hipSuccess) return -1;
+    pp.joined = true;
+    if (w.last_debug & RT_DEBUG_CALL_LOG) {
+        (void)hipStreamSynchronize(s);
+        timespec ts;
+        clock_gettime(CLOCK_MONOTONIC, &ts);
+        uint32_t rc[7] = {};
+        (void)hipMemcpy(rc, st.ret_ctr, sizeof rc, hipMemcpyDeviceToHost);
+        fprintf(stderr, "[wf] drain done t %.4f; returns reserved %u claimed %u, pixels out %u; owed passes: most %u, pixels %u\n",
+                ts.tv_sec + ts.tv_nsec * 1e-9, rc[0], rc[2], rc[3], rc[5], rc[6]);
+    }
     return 0;
 }
 
@@ -1973,6 +2101,28 @@ int debug_long_log(Workspace &w, unsigned long long *buf)
     for (size_t i = 0; i < v.size() && i < 8; ++i)
         fprintf(stderr, "  %.1f %.1f %llu %.2f %llu\n", v[i].start, v[i].end, v[i].bounces,
                 (v[i].end - v[i].start) * 1e3 / (double)(v[i].bounces ? v[i].bounces : 1), v[i].slot);
+    // per pixel: deep samples, their summed time in wf_long, first claim and last end
+    std::map<unsigned long long, Rec> px;
+    std::map<unsigned long long, int> nd;
+    for (const Rec &r : v) {
+        auto it = px.find(r.slot);
+        if (it == px.end()) {
+            px[r.slot] = Rec{r.start, r.end, 0, (unsigned long long)0};
+            it = px.find(r.slot);
+        }
+        it->second.start = std::min(it->second.start, r.start);
+        it->second.end = std::max(it->second.end, r.end);
+        it->second.slot += (unsigned long long)((r.end - r.start) * 1e3); // (us in wf_long)
+        it->second.bounces += r.bounces;
+        ++nd[r.slot];
+    }
+    std::vector<std::pair<unsigned long long, Rec>> pv(px.begin(), px.end());
+    std::sort(pv.begin(), pv.end(), [](const auto &a, const auto &b) { return a.second.end > b.second.end; });
+    fprintf(stderr, "[wf long log] %zu pixels; latest-ending 10 (slot, deep samples, bounces, ms in wf_long, first claim, last end):\n",
+            pv.size());
+    for (size_t i = 0; i < pv.size() && i < 10; ++i)
+        fprintf(stderr, "  %llu %d %llu %.1f %.1f %.1f\n", pv[i].first, nd[pv[i].first], pv[i].second.bounces,
+                pv[i].second.slot * 1e-3, pv[i].second.start, pv[i].second.end);
     return 0;
 }
 
@@ -2002,6 +2152,7 @@ int rt_wavefront_join(void *stream)
         w = it->second;
     }
     if (!stream) {
+        if (launch_drain(*w) != 0) return -1;
         for (int pi = 0; pi < WF_MAX_PIPES; ++pi) {
             Pipe &p = w->pipe[pi];
             if (p.joined && hipEventSynchronize(p.join) != hipSuccess) return -1;
@@ -2024,6 +2175,7 @@ void rt_wavefront_shutdown()
         Workspace *w = kv.second;
         if (!w) continue;
         if (hipSetDevice(kv.first) != hipSuccess) continue;
+        if (w->blob) (void)launch_drain(*w); // (an open chain's wf_longs leave only after its drain)
         (void)hipDeviceSynchronize();
         if (w->blob) (void)hipFree(w->blob);
         for (int i = WF_MAX_PIPES - 1; i >= 0; --i) {
