@@ -2,7 +2,7 @@
 per rt_render call, chained (RtOptions.overlap = 1) and unchained: the
 reference calls render() once per pass (rt/main.cu:114-155).  Each row renders
 `total` passes after a warm-up, in calls of `per_call` passes, and ends with
-rt_join.  usage: python tools/call_granularity.py [total passes] [per-call list]"""
+rt_join.  usage: python tools/call_granularity.py [total passes] [per-call passes ...]"""
 import json
 import os
 import sys
@@ -14,7 +14,7 @@ import helpers  # noqa: E402
 import rt  # noqa: E402
 
 total = int(sys.argv[1]) if len(sys.argv) > 1 else 256
-per_calls = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [1, 16, 64, 256]
+per_calls = [int(x) for a in sys.argv[2:] for x in a.split(",")] or [1, 16, 64, 256]
 scene = os.environ.get("RT_SCENE", "room2m")
 W, H = 1920, 1080
 rt.check(rt.lib().rt_set_device(0))
