@@ -275,9 +275,13 @@ __device__ __forceinline__ float bvh4_bound(const RtDevScene &sc, Vec3D o, Vec3D
 // BOUNDED_COUNTED): this traversal's own work — RT_CNT_RAY, RT_CNT_NODE / _TRI
 // (KD nodes / plane tests), RT_CNT_B_* (BVH nodes / plane tests, barycentric
 // records of both phases)
+// `hint`: any starting value for the s_min query's running best (a shadow
+// ray: just past its light point).  Exact whatever its value: the query
+// returns min(hint, what it finds below it), and a leaf with exit <= that
+// still accepts no test (a test passing below it would have been found).
 template <bool COUNT, typename STACK>
 __device__ __forceinline__ int trace_bvh(const RtDevScene &sc, const Vec3D o, const Vec3D d, float &hbx, float &hby,
-                                         float &hbz, STACK &stk, Cnt &c)
+                                         float &hbz, STACK &stk, Cnt &c, float hint = INFINITY)
 {
     if (COUNT) c.v[RT_CNT_RAY]++;
     float entry, exit_;
@@ -285,7 +289,8 @@ __device__ __forceinline__ int trace_bvh(const RtDevScene &sc, const Vec3D o, co
     const float root_exit = exit_;
     float s_min = -INFINITY; // (the plain KD traversal)
     if (rt_bounded_ray(o, d, sc.split_vals, sc.split_off)) {
-        s_min = RT_BVH4 ? bvh4_bound<COUNT>(sc, o, d, exit_, stk, c) : bvh_bound<COUNT>(sc, o, d, exit_, stk, c);
+        const float b0 = hint < exit_ ? hint : exit_;
+        s_min = RT_BVH4 ? bvh4_bound<COUNT>(sc, o, d, b0, stk, c) : bvh_bound<COUNT>(sc, o, d, b0, stk, c);
         RT_PHASE_MID();
         if (!(s_min < root_exit)) return -1;
     }
