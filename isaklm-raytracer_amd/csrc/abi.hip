@@ -102,7 +102,6 @@ int upload_prepared(const rt_host::PreparedHost &h, int ntris, int nindices, rt_
     RtDevScene &dv = s->dev;
     dv.bvh_nodes = nullptr;
     dv.bvh4 = nullptr;
-    dv.bvh4q = nullptr;
     dv.bvh_a = nullptr;
     dv.bvh_bary = nullptr;
     dv.bvh_scale = h.bvh_scale;
@@ -114,7 +113,6 @@ int upload_prepared(const rt_host::PreparedHost &h, int ntris, int nindices, rt_
     for (int a = 0; a < 4; ++a) dv.split_off[a] = h.split_off[a];
     if (h.bvh_depth >= 0 && ((rc = upload_vec(*s, h.bvh_nodes, &dv.bvh_nodes)) ||
                              (rc = upload_vec(*s, h.bvh4, &dv.bvh4)) ||
-                             (rc = upload_vec(*s, h.bvh4q, &dv.bvh4q)) ||
                              (rc = upload_vec(*s, h.bvh_a, &dv.bvh_a)) ||
                              (rc = upload_vec(*s, h.bvh_bary, &dv.bvh_bary)) ||
                              (rc = upload_vec(*s, h.split_vals, &dv.split_vals)))) {

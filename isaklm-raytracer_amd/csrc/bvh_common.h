@@ -65,19 +65,6 @@ RT_HD bool rt_bvh_box(float lx, float ly, float lz, float hx, float hy, float hz
     return tn <= tf && tf >= 0.0f && tn <= best;
 }
 
-// The quantized 4-wide node (host/bvh_build.h quantize_bvh4), 4 RtF4 = 64 B:
-//   {origin.x, origin.y, origin.z, scale.x}, {qlo.x, qlo.y, qlo.z, qhi.x},
-//   {qhi.y, qhi.z, scale.y, scale.z}, {ref0, ref1, ref2, ref3}
-// (q words: one byte per child, child k in bits 8k..8k+7; scales powers of
-// two).  A child's bound on an axis is origin + q * scale, evaluated as here
-// on the host and the device alike; the builder picks every byte so that
-// this float value contains the child's conservative box (lo rounded down,
-// hi up), so the query on it finds the same smallest passing s.
-RT_HD float rt_bvh4q_decode(uint32_t word, int k, float origin, float scale)
-{
-    return origin + (float)((word >> (8 * k)) & 255u) * scale;
-}
-
 // intersect_triangle's plane part (rt/trace_ray.cuh:73-96) on the
 // precomputed plane A = {n, dot(n, p1)}: s, and whether the test goes on
 // (dn != 0, s >= 1e-5, s < closest)

@@ -170,9 +170,6 @@ __device__ __forceinline__ float bvh_bound(const RtDevScene &sc, Vec3D o, Vec3D 
 #ifndef RT_BVH4
 #define RT_BVH4 1 // trace_bvh's s_min query on the 4-wide collapse (0: the binary tree)
 #endif
-#ifndef RT_BVH4Q
-#define RT_BVH4Q 0 // ... on its quantized 64-B nodes (host/bvh_build.h quantize_bvh4)
-#endif
 template <bool COUNT, typename STACK>
 __device__ __forceinline__ float bvh4_bound(const RtDevScene &sc, Vec3D o, Vec3D d, float best, STACK &stk, Cnt &cn)
 {
@@ -194,25 +191,10 @@ __device__ __forceinline__ float bvh4_bound(const RtDevScene &sc, Vec3D o, Vec3D
     while (true) {
         while (!(cur & RT_BVH_LEAF)) {
             if (COUNT) cn.v[RT_CNT_B_BVH_NODE]++;
-#if RT_BVH4Q
-            // the quantized node: 4 loads of 16 B (one 64-B half line) instead of 7
-            const RtF4 *nd = sc.bvh4q + 4 * (size_t)cur;
-            const RtF4 q0 = ldc4(nd), q2 = ldc4(nd + 2);
-            const uint4 q1 = ldc_u4(reinterpret_cast<const uint32_t *>(nd + 1));
-            const uint4 rf = ldc_u4(reinterpret_cast<const uint32_t *>(nd + 3));
-            const uint32_t qhy = __float_as_uint(q2.x), qhz = __float_as_uint(q2.y);
-            auto dec4 = [](uint32_t w, float o, float s) {
-                return RtF4{rt_bvh4q_decode(w, 0, o, s), rt_bvh4q_decode(w, 1, o, s), rt_bvh4q_decode(w, 2, o, s),
-                            rt_bvh4q_decode(w, 3, o, s)};
-            };
-            const RtF4 lx = dec4(q1.x, q0.x, q0.w), ly = dec4(q1.y, q0.y, q2.z), lz = dec4(q1.z, q0.z, q2.w),
-                       hx = dec4(q1.w, q0.x, q0.w), hy = dec4(qhy, q0.y, q2.z), hz = dec4(qhz, q0.z, q2.w);
-#else
             const RtF4 *nd = sc.bvh4 + 8 * (size_t)cur;
             const RtF4 lx = ldc4(nd), ly = ldc4(nd + 1), lz = ldc4(nd + 2), hx = ldc4(nd + 3), hy = ldc4(nd + 4),
                        hz = ldc4(nd + 5);
             const uint4 rf = ldc_u4(reinterpret_cast<const uint32_t *>(nd + 6));
-#endif
             float t0, t1, t2, t3;
             uint32_t r0 = rf.x, r1 = rf.y, r2 = rf.z, r3 = rf.w;
             if (!(rt_bvh_box(lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, om, op, inv, best, t0) && r0 != RT_BVH_EMPTY)) {
@@ -275,13 +257,9 @@ __device__ __forceinline__ float bvh4_bound(const RtDevScene &sc, Vec3D o, Vec3D
 // BOUNDED_COUNTED): this traversal's own work — RT_CNT_RAY, RT_CNT_NODE / _TRI
 // (KD nodes / plane tests), RT_CNT_B_* (BVH nodes / plane tests, barycentric
 // records of both phases)
-// `hint`: any starting value for the s_min query's running best (a shadow
-// ray: just past its light point).  Exact whatever its value: the query
-// returns min(hint, what it finds below it), and a leaf with exit <= that
-// still accepts no test (a test passing below it would have been found).
 template <bool COUNT, typename STACK>
 __device__ __forceinline__ int trace_bvh(const RtDevScene &sc, const Vec3D o, const Vec3D d, float &hbx, float &hby,
-                                         float &hbz, STACK &stk, Cnt &c, float hint = INFINITY)
+                                         float &hbz, STACK &stk, Cnt &c)
 {
     if (COUNT) c.v[RT_CNT_RAY]++;
     float entry, exit_;
@@ -289,8 +267,7 @@ __device__ __forceinline__ int trace_bvh(const RtDevScene &sc, const Vec3D o, co
     const float root_exit = exit_;
     float s_min = -INFINITY; // (the plain KD traversal)
     if (rt_bounded_ray(o, d, sc.split_vals, sc.split_off)) {
-        const float b0 = hint < exit_ ? hint : exit_;
-        s_min = RT_BVH4 ? bvh4_bound<COUNT>(sc, o, d, b0, stk, c) : bvh_bound<COUNT>(sc, o, d, b0, stk, c);
+        s_min = RT_BVH4 ? bvh4_bound<COUNT>(sc, o, d, exit_, stk, c) : bvh_bound<COUNT>(sc, o, d, exit_, stk, c);
         RT_PHASE_MID();
         if (!(s_min < root_exit)) return -1;
     }

@@ -423,80 +423,4 @@ void collapse_bvh4(const std::vector<RtF4> &bin, std::vector<RtF4> &out4)
     }
 }
 
-bool quantize_bvh4(const std::vector<RtF4> &n4, std::vector<RtF4> &q4)
-{
-    const size_t nn = n4.size() / 8;
-    q4.assign(4 * nn, RtF4{0, 0, 0, 0});
-    bool ok = true;
-#pragma omp parallel for schedule(static) reduction(&& : ok)
-    for (long long i = 0; i < (long long)nn; ++i) {
-        const float *f = reinterpret_cast<const float *>(&n4[8 * (size_t)i]);
-        const uint32_t *ref = reinterpret_cast<const uint32_t *>(f + 24);
-        float origin[3] = {0, 0, 0}, scale[3] = {1, 1, 1};
-        uint32_t qlo[3] = {0, 0, 0}, qhi[3] = {0, 0, 0};
-        for (int a = 0; a < 3 && ok; ++a) {
-            float lo = INFINITY, hi = -INFINITY;
-            for (int k = 0; k < 4; ++k)
-                if (ref[k] != RT_BVH_EMPTY) {
-                    const float l = f[4 * a + k], h = f[4 * (3 + a) + k];
-                    if (!std::isfinite(l) || !std::isfinite(h)) ok = false;
-                    lo = std::min(lo, l);
-                    hi = std::max(hi, h);
-                }
-            if (!ok) break;
-            if (!(lo <= hi)) { // no child: any origin, every byte "empty"
-                lo = hi = 0.0f;
-            }
-            origin[a] = lo;
-            // the smallest power-of-two scale whose 255 steps span the node (then up while a bound does not fit)
-            int e = -126;
-            {
-                const double ext = (double)hi - (double)lo;
-                if (ext > 0) e = std::max(-126, (int)std::ceil(std::log2(ext / 255.0)));
-            }
-            for (;; ++e) {
-                const float sc = std::ldexp(1.0f, e);
-                bool fit = true;
-                uint32_t wl = 0, wh = 0;
-                for (int k = 0; k < 4 && fit; ++k) {
-                    uint32_t bl = 255u, bh = 0u; // (an empty child: lo above hi)
-                    if (ref[k] != RT_BVH_EMPTY) {
-                        const float l = f[4 * a + k], h = f[4 * (3 + a) + k];
-                        double ql = std::floor(((double)l - (double)lo) / (double)sc);
-                        int il = (int)std::max(0.0, std::min(255.0, ql));
-                        while (il > 0 && rt_bvh4q_decode((uint32_t)il, 0, lo, sc) > l) --il;
-                        double qh = std::ceil(((double)h - (double)lo) / (double)sc);
-                        int ih = (int)std::max(0.0, std::min(255.0, qh));
-                        while (ih < 255 && rt_bvh4q_decode((uint32_t)ih, 0, lo, sc) < h) ++ih;
-                        if (rt_bvh4q_decode((uint32_t)il, 0, lo, sc) > l || rt_bvh4q_decode((uint32_t)ih, 0, lo, sc) < h)
-                            fit = false;
-                        bl = (uint32_t)il;
-                        bh = (uint32_t)ih;
-                    }
-                    wl |= bl << (8 * k);
-                    wh |= bh << (8 * k);
-                }
-                if (fit) {
-                    scale[a] = sc;
-                    qlo[a] = wl;
-                    qhi[a] = wh;
-                    break;
-                }
-                if (e > 120) {
-                    ok = false;
-                    break;
-                }
-            }
-        }
-        if (!ok) continue;
-        RtF4 *q = &q4[4 * (size_t)i];
-        auto bits = [](uint32_t u) { float x; memcpy(&x, &u, 4); return x; };
-        q[0] = RtF4{origin[0], origin[1], origin[2], scale[0]};
-        q[1] = RtF4{bits(qlo[0]), bits(qlo[1]), bits(qlo[2]), bits(qhi[0])};
-        q[2] = RtF4{bits(qhi[1]), bits(qhi[2]), scale[1], scale[2]};
-        q[3] = RtF4{bits(ref[0]), bits(ref[1]), bits(ref[2]), bits(ref[3])};
-    }
-    return ok;
-}
-
 } // namespace rt_host

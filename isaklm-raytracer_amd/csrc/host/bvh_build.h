@@ -149,10 +149,4 @@ int build_bvh(const Triangle *tris, int ntris, const RtF4 *plane, const RtIsectB
 // lo.z, hi.x, hi.y, hi.z, references, padding).
 void collapse_bvh4(const std::vector<RtF4> &bin, std::vector<RtF4> &out4);
 
-// the 4-wide collapse quantized to 64 B per node (bvh_common.h
-// rt_bvh4q_decode): per axis the node's origin and a power-of-two scale,
-// per child one byte per bound, rounded outward and checked with the
-// device's own decode expression.  Returns false on a non-finite box.
-bool quantize_bvh4(const std::vector<RtF4> &n4, std::vector<RtF4> &q4);
-
 } // namespace rt_host

@@ -60,7 +60,6 @@ struct PreparedHost {
     // bvh_depth < 0: not built (the KD-only traversal runs)
     std::vector<RtF4> bvh_nodes;          // 4 per node
     std::vector<RtF4> bvh4;               // the 4-wide collapse (bvh_build.h collapse_bvh4), 8 per node
-    std::vector<RtF4> bvh4q;              // its quantized form (bvh_build.h quantize_bvh4), 4 per node
     int bvh4_stack = 0;                   // the deepest stack its query can build (must be < RT_BVH_STACK)
     std::vector<RtF4> bvh_a;              // BVH leaf-slot order
     std::vector<RtIsectBary> bvh_bary;    // BVH leaf-slot order

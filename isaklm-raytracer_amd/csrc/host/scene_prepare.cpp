@@ -277,9 +277,6 @@ int prepare_host(const Triangle *tris, int ntris, const KD_Tree_Node *nodes, int
             }
             out.bvh4_stack = worst;
         }
-        // 64-B nodes for the device query (a non-finite box: no bounded traversal)
-        const bool quantized = quantize_bvh4(out.bvh4, out.bvh4q);
-        if (!quantized) out.bvh4_stack = RT_BVH_STACK;
         out.bvh_a.resize(bvh.order.size());
         out.bvh_bary.resize(bvh.order.size());
 #pragma omp parallel for schedule(static)

@@ -96,7 +96,6 @@ struct RtDevScene {
     // bvh_trace.h); bvh_nodes == nullptr: none (KD-only traversal)
     const RtF4 *bvh_nodes;      // 4 per node: child boxes {lo0, hi0.x}, {hi0.yz, lo1.xy}, {lo1.z, hi1}, {ref0, ref1, -, -}
     const RtF4 *bvh4;           // its 4-wide collapse, 8 per node: lo.x, lo.y, lo.z, hi.x, hi.y, hi.z of 4 children, refs, -
-    const RtF4 *bvh4q;          // the same quantized, 4 per node (bvh_common.h rt_bvh4q_decode)
     const RtF4 *bvh_a;          // per BVH leaf slot: plane (as isect_a)
     const RtIsectBary *bvh_bary; // per BVH leaf slot: barycentric-test record (as isect_bary)
     float bvh_scale;            // largest |vertex|_1 (rt_ray_margin)

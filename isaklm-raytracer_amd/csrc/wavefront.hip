@@ -94,9 +94,6 @@ static_assert(WF_BLOCK % WF_TBLOCK == 0 && WF_TBLOCK % 64 == 0, "WF_TBLOCK must 
 #ifndef WF_BVH_WAVES
 #define WF_BVH_WAVES 6  // wf_trace_bvh occupancy target
 #endif
-#ifndef RT_SHADOW_HINT
-#define RT_SHADOW_HINT 0 // the finisher's shadow-ray queries start with best = the light point's distance
-#endif
 #ifndef WF_FIN_BVH_WAVES
 #define WF_FIN_BVH_WAVES 5 // wf_finish_bvh occupancy target (5: +3 % over 6 with the 4-wide s_min query, profiles/r04)
 #endif
@@ -1170,13 +1167,7 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_FIN_BVH_WAVES) wf_finish_bvh(RtDe
 #endif
         if (active) {
             float bx = 0.0f, by = 0.0f, bz = 0.0f;
-#if RT_SHADOW_HINT
-            // a shadow ray's query needs nothing beyond its light point (any bound is exact, trace_bvh)
-            const float hint = p.shadow ? rt_magnitude(p.rp - p.ro) * 1.0009765625f + 1e-5f : INFINITY;
-            const int hit = trace_bvh<COUNT>(sc, p.ro, p.rd, bx, by, bz, stk, c, hint);
-#else
             const int hit = trace_bvh<COUNT>(sc, p.ro, p.rd, bx, by, bz, stk, c);
-#endif
 #ifdef RT_PHASE_PROF
             {
                 const unsigned long long t2 = __builtin_amdgcn_s_memtime();

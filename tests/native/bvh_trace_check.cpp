@@ -248,68 +248,6 @@ float bvh4_bound(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, float best, W
     }
 }
 
-long long g_bvh4q_mism = 0, g_bvh4q_diff = 0;
-
-// the same query on the quantized nodes (bvh_trace.h with RT_BVH4Q): each
-// child's box decoded with the device's expression (bvh_common.h
-// rt_bvh4q_decode); the boxes contain the 4-wide collapse's, so the smallest
-// passing s must come out the same
-float bvh4q_bound(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, float best, Work &w)
-{
-    const float m = rt_ray_margin(o.x, o.y, o.z, h.bvh_scale);
-    const Vec3D om = rt_v3(o.x + m, o.y + m, o.z + m), op = rt_v3(o.x - m, o.y - m, o.z - m);
-    const Vec3D inv = rt_v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-    struct E { uint32_t ref; float tn; };
-    std::vector<E> stk;
-    uint32_t cur = 0;
-    auto pop = [&]() -> uint32_t {
-        while (!stk.empty()) {
-            const E e = stk.back();
-            stk.pop_back();
-            if (e.tn <= best) return e.ref;
-        }
-        return RT_BVH_EMPTY;
-    };
-    while (true) {
-        while (!(cur & RT_BVH_LEAF)) {
-            ++w.bvh_nodes;
-            const float *f = reinterpret_cast<const float *>(&h.bvh4q[4 * (size_t)cur]);
-            const uint32_t *u = reinterpret_cast<const uint32_t *>(f);
-            const float org[3] = {f[0], f[1], f[2]}, sc[3] = {f[3], f[10], f[11]};
-            const uint32_t ql[3] = {u[4], u[5], u[6]}, qh[3] = {u[7], u[8], u[9]};
-            const uint32_t *rf = u + 12;
-            E c[4];
-            for (int k = 0; k < 4; ++k) {
-                float lo[3], hi[3];
-                for (int a = 0; a < 3; ++a) {
-                    lo[a] = rt_bvh4q_decode(ql[a], k, org[a], sc[a]);
-                    hi[a] = rt_bvh4q_decode(qh[a], k, org[a], sc[a]);
-                }
-                float tn;
-                const bool hit = rt_bvh_box(lo[0], lo[1], lo[2], hi[0], hi[1], hi[2], om, op, inv, best, tn) &&
-                                 rf[k] != RT_BVH_EMPTY;
-                c[k] = hit ? E{rf[k], tn} : E{RT_BVH_EMPTY, INFINITY};
-            }
-            std::stable_sort(c, c + 4, [](const E &a, const E &b) {
-                const bool ea = a.ref == RT_BVH_EMPTY, eb = b.ref == RT_BVH_EMPTY;
-                return ea != eb ? eb : a.tn < b.tn;
-            });
-            for (int k = 3; k >= 1; --k)
-                if (c[k].ref != RT_BVH_EMPTY) stk.push_back(c[k]);
-            cur = c[0].ref != RT_BVH_EMPTY ? c[0].ref : pop();
-        }
-        if (cur == RT_BVH_EMPTY) return best;
-        const uint32_t first = (cur & ~RT_BVH_LEAF) >> 3, end = first + (cur & 7u) + 1u;
-        for (uint32_t e = first; e < end; ++e) {
-            float s, b[3];
-            ++w.bvh_tests;
-            if (test(h.bvh_a.data(), h.bvh_bary.data(), e, o, d, best, s, b)) best = s;
-        }
-        cur = pop();
-        if (cur == RT_BVH_EMPTY) return best;
-    }
-}
-
 // restatement of coop_trace.h kd_origin_frontier's replay: the descent along
 // the stored root path of a grid cell's start node, each decision checked
 bool kd_resume(const rt_host::PreparedHost &h, uint32_t start, uint32_t packed, Vec3D o, Vec3D d, float entry,
@@ -363,25 +301,6 @@ Hit bounded_trace(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, Work &w)
     if (memcmp(&s_bin, &s_min, 4) != 0) {
 #pragma omp atomic
         ++g_bvh4_mism;
-    }
-    Work w3;
-    const float s_q = bvh4q_bound(h, o, d, t2, w3);
-    if (memcmp(&s_q, &s_min, 4) != 0) {
-#pragma omp atomic
-        ++g_bvh4q_diff;
-    }
-    // the s_min values may differ (a sliver's whole-scene box: its test can pass at any s, even
-    // before the scene box, so the queries' visiting orders can end on different values); what
-    // exactness needs is that no skipped leaf would accept a test — so the KD phase on the
-    // quantized query's s_min must give the same hit
-    {
-        Work w4;
-        const Hit hq = !(s_q < t2) ? Hit{} : kd_trace(h, o, d, t1, t2, s_q, w4);
-        const Hit h4 = !(s_min < t2) ? Hit{} : kd_trace(h, o, d, t1, t2, s_min, w4);
-        if (hq.tri != h4.tri || memcmp(hq.b, h4.b, sizeof hq.b) != 0) {
-#pragma omp atomic
-            ++g_bvh4q_mism;
-        }
     }
     if (!(s_min < t2)) return Hit{};
     return kd_trace(h, o, d, t1, t2, s_min, w);
@@ -608,8 +527,5 @@ int main(int argc, char **argv)
     printf("origin-cell entry: %lld resumed, mismatches vs the plain traversal %lld\n", g_origin_resumed, g_origin_mism);
     printf("4-wide s_min query: %zu nodes, deepest stack %d, s_min differing from the binary query %lld\n",
            h.bvh4.size() / 8, h.bvh4_stack, g_bvh4_mism);
-    printf("quantized 4-wide s_min query: %zu nodes of 64 B, s_min differing from the 4-wide query's %lld, "
-           "hits differing %lld\n",
-           h.bvh4q.size() / 4, g_bvh4q_diff, g_bvh4q_mism);
-    return mism == 0 && g_origin_mism == 0 && g_bvh4_mism == 0 && g_bvh4q_mism == 0 ? 0 : 1;
+    return mism == 0 && g_origin_mism == 0 && g_bvh4_mism == 0 ? 0 : 1;
 }
