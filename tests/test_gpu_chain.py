@@ -150,3 +150,50 @@ def test_small_frame_after_a_large_one(tmp_path):
     gpu, _, _ = run.render(W, H, P, calls=2, kernel=WF)
     ref, _ = helpers.oracle_render(trap, W, H, P, calls=2)
     helpers.assert_bitwise(gpu, ref, what="light guide after a 1080p frame")
+
+
+def test_chain_interrupted_by_another_frame(tmp_path):
+    """A chain left open on one G_Buffer is drained when a call for another
+    frame comes (join_all in the fresh call): both frames equal their
+    unchained renders.  The light guide keeps pixels out in wf_long across
+    call boundaries, so the first chain really has owed passes to drain."""
+    trap = helpers.make_trap_scene(str(tmp_path / "t"))
+    run = helpers.GpuRun(trap)
+    W, H = 96, 64
+    ga, gb = rt.GBuffer(W, H), rt.GBuffer(W, H, W * H)
+    for c in range(3):
+        rt.render(run.dev, ga, run.camera, 0 if c == 0 else 1,
+                  rt.options(W, H, 1, adaptive=False, kernel=WF, overlap=True, wf_long_depth=8))
+    for c in range(3):  # another frame: not a continuation, the open chain drains first
+        rt.render(run.dev, gb, run.camera, 0 if c == 0 else 1,
+                  rt.options(W, H, 2, adaptive=False, kernel=WF, overlap=True, wf_long_depth=8))
+    rt.join()
+    ra, _ = helpers.oracle_render(trap, W, H, [1, 1, 1])
+    rb, _ = helpers.oracle_render(trap, W, H, [2, 2, 2], seed_skip=W * H)
+    helpers.assert_bitwise(ga.download(), ra, what="chain A drained by frame B's call")
+    helpers.assert_bitwise(gb.download(), rb, what="chain B")
+
+
+def test_chain_left_open_at_exit(tmp_path):
+    """A process that ends with a chain still open (no rt_join): rt_shutdown
+    (atexit) drains it before it frees the workspace — the process exits
+    cleanly and promptly."""
+    import subprocess
+    import sys
+    import textwrap
+    trap = helpers.make_trap_scene(str(tmp_path / "t"))
+    code = textwrap.dedent(f"""
+        import sys
+        sys.path[:0] = {[p for p in sys.path if p.endswith(('isaklm-raytracer_amd', 'tests', 'oracle'))]!r}
+        import helpers, rt
+        rt.check(rt.lib().rt_set_device(0))
+        run = helpers.GpuRun({trap!r})
+        g = rt.GBuffer(96, 64)
+        for c in range(4):
+            rt.render(run.dev, g, run.camera, 0 if c == 0 else 1,
+                      rt.options(96, 64, 1, adaptive=False, kernel=rt.KERNEL_WAVEFRONT, overlap=True,
+                                 wf_long_depth=8))
+        print("enqueued", flush=True)
+    """)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "enqueued" in r.stdout, r.stdout + r.stderr
