@@ -93,11 +93,7 @@ int upload_prepared(const rt_host::PreparedHost &h, int ntris, int nindices, rt_
     const RtF4 *a = nullptr, *sh = nullptr;
     const RtIsectBary *bary = nullptr;
     const RtDevMaterial *mats = nullptr;
-    // (one zero node past the end: the wide traversal loads node + 1 beside every node)
-    std::vector<uint32_t> padded(h.nodes);
-    padded.push_back(0u);
-    padded.push_back(0u);
-    if ((rc = upload_vec(*s, padded, &nodes)) || (rc = upload_vec(*s, h.isect_a, &a)) ||
+    if ((rc = upload_vec(*s, h.nodes, &nodes)) || (rc = upload_vec(*s, h.isect_a, &a)) ||
         (rc = upload_vec(*s, h.isect_bary, &bary)) || (rc = upload_vec(*s, h.shade, &sh)) ||
         (rc = upload_vec(*s, h.materials, &mats)) || (rc = upload_vec(*s, h.lights, &lights))) {
         release(s);

@@ -453,9 +453,6 @@ __device__ __forceinline__ bool coop_round(const RtDevScene &sc, CoopRay &r, STK
 // charged to its first child (acc) and committed only when a leaf at or
 // before the winning leaf is consumed — the nodes the sequential traversal
 // visits are exactly those at or before the winning leaf in order.
-#ifndef WIDE_2LV
-#define WIDE_2LV 0 // non-counting wide traversal: two levels per round where the near child is node + 1
-#endif
 #define WIDE_CAP 256        // frontier items per wave
 #define WIDE_RESERVE 24     // head-only growth room (tree depth <= 20)
 #define WIDE_LEAF_BUDGET 256 // entries tested per batch (at least one whole leaf)
@@ -510,18 +507,15 @@ __device__ __forceinline__ void wide_trace_from(const RtDevScene &sc, Vec3D o, V
     while (n > 0) {
         if (COUNT && counter_lane) c.v[RT_CNT_WIDE_ROUNDS]++;
         const unsigned long long tr0 = COUNT ? __builtin_amdgcn_s_memtime() : 0ull;
-        // expansions add at most one item each (two-level ones two)
-        constexpr bool two = !COUNT && WIDE_2LV;
-        int k = two ? (W.cap - WIDE_RESERVE - n) / 2 : W.cap - WIDE_RESERVE - n;
+        int k = W.cap - WIDE_RESERVE - n; // expansions add at most one item each
         k = k < 1 ? 1 : (k > 64 ? 64 : k);
         k = k < n ? k : n;
         WideItem it = WideItem{0u, 0.0f, 0.0f, 0u};
-        uint2 nd = make_uint2(0u, 0u), nd1 = nd; // nd1 (two-level): node + 1, the pre-order next
+        uint2 nd = make_uint2(0u, 0u);
         const bool have = lane < k;
         if (have) {
             it = F[n - 1 - lane];
             nd = *reinterpret_cast<const uint2 *>(sc.nodes + 2 * (size_t)it.node);
-            if (two) nd1 = *reinterpret_cast<const uint2 *>(sc.nodes + 2 * (size_t)it.node + 2); // (array padded)
         }
         const bool leaf = have && (nd.y & 3u) == RT_LEAF_TAG;
         const unsigned long long lmask = __ballot(leaf);
@@ -621,66 +615,6 @@ __device__ __forceinline__ void wide_trace_from(const RtDevScene &sc, Vec3D o, V
             if (counter_lane) c.v[RT_CNT_T_WIDE_LEAF] += tex - tph;
         }
         // expand the rest of the k items (leaves behind an inner item stay as they are)
-        if (two) {
-            // two levels where the near child is node + 1 (its words came with the
-            // node's): the sequential rule at the node, then at that child — the
-            // pushes below, the final near item on top, as two rounds would leave them
-            int c_out = 0;
-            WideItem fin = it, p0 = it, p1 = it;
-            int np = 0;
-            if (have && lane >= Le) {
-                c_out = 1;
-                if (!leaf) {
-                    float en = it.entry, ex = it.exit_;
-                    uint32_t cur = it.node;
-                    uint2 w = nd;
-                    for (int lev = 0; lev < 2; ++lev) {
-                        const uint32_t axis = w.y & 3u;
-                        const float split = as_float(w.x);
-                        const float oax = axis == 0 ? ox : (axis == 1 ? oy : oz);
-                        const float dax = axis == 0 ? dx : (axis == 1 ? dy : dz);
-                        const float yax = axis == 0 ? yx : (axis == 1 ? yy : yz);
-                        uint32_t near_c = cur + 1, far_c = w.y >> 2;
-                        if (oax >= split) { // ray_behind_plane (:174-188)
-                            near_c = w.y >> 2;
-                            far_c = cur + 1;
-                        }
-                        const float t = rt_div_by(split - oax, dax, yax); // intersect_plane (:190-210)
-                        uint32_t next;
-                        if (t >= ex || t < 0) {
-                            next = near_c;
-                        } else if (t <= en) {
-                            next = far_c;
-                        } else {
-                            const WideItem pu = WideItem{far_c, t, ex, 0u};
-                            if (np == 0) p0 = pu;
-                            else p1 = pu;
-                            ++np;
-                            next = near_c;
-                            ex = t;
-                        }
-                        const bool again = lev == 0 && next == cur + 1 && (nd1.y & 3u) != RT_LEAF_TAG;
-                        cur = next;
-                        if (!again) break;
-                        w = nd1;
-                    }
-                    fin = WideItem{cur, en, ex, 0u};
-                    c_out = 1 + np;
-                }
-            }
-            int pos = wave_incl_add(c_out);
-            const int M = lane63(pos);
-            pos -= c_out;
-            const int top = n - k + M - 1 - pos;
-            if (c_out >= 1) F[top] = fin;
-            if (np == 1) F[top - 1] = p0;
-            if (np == 2) {
-                F[top - 1] = p1;
-                F[top - 2] = p0;
-            }
-            n = n - k + M;
-            continue;
-        }
         int c_out = 0;
         WideItem a = it, b = it;
         if (have && lane >= Le) {
