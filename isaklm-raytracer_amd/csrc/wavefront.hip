@@ -94,6 +94,9 @@ static_assert(WF_BLOCK % WF_TBLOCK == 0 && WF_TBLOCK % 64 == 0, "WF_TBLOCK must 
 #ifndef WF_BVH_WAVES
 #define WF_BVH_WAVES 6  // wf_trace_bvh occupancy target
 #endif
+#ifndef WF_LONG_PINGPONG
+#define WF_LONG_PINGPONG 1 // whole-call mode: wf_long on pipelines 1 and 2 alternately (0: always pipeline 1)
+#endif
 #ifndef WF_FIN_BVH_WAVES
 #define WF_FIN_BVH_WAVES 5 // wf_finish_bvh occupancy target (5: +3 % over 6 with the 4-wide s_min query, profiles/r04)
 #endif
@@ -112,7 +115,9 @@ static_assert(WF_BLOCK % WF_TBLOCK == 0 && WF_TBLOCK % 64 == 0, "WF_TBLOCK must 
 #define WF_MAX_PIPES 6                // concurrent pipelines (RtOptions.wf_pipelines); more than 3 need GPU_MAX_HW_QUEUES > 4
 #define WF_PIPES_DEFAULT 3
 #define WF_LONG_DEPTH_DEFAULT 64      // RtOptions.wf_long_depth: paths deeper than this go to wf_long
-#define WF_LONG_BLOCKS 64             // wf_long grid (4 waves each, one path per wave at a time)
+#ifndef WF_LONG_BLOCKS
+#define WF_LONG_BLOCKS 64 // wf_long grid (4 waves each, one path per wave at a time)
+#endif
 // safety nets (s_memrealtime ticks, 100 MHz), never reached by a working
 // protocol: a wf_long slice wave leaves after 20 s without a claim; a
 // persistent wf_long wave (whole-call mode) after 600 s without a claim.
@@ -1963,7 +1968,7 @@ int launch_whole(Workspace &w, int dev, const RtDevScene &sc, const RtDevFrame &
     if (hipGetLastError() != hipSuccess || !mark(3)) return -1;
     Pipe *lp = nullptr;
     if (long_return) {
-        lp = &w.pipe[1 + (int)(w.call_seq & 1)];
+        lp = &w.pipe[1 + (WF_LONG_PINGPONG ? (int)(w.call_seq & 1) : 0)];
         if (hipStreamWaitEvent(lp->stream, w.fin_ready, 0) != hipSuccess) return -1;
         hipLaunchKernelGGL(wf_long<false>, dim3(WF_LONG_BLOCKS), dim3(WF_BLOCK), 0, lp->stream, sc, fr, cam, st, 1);
         if (hipGetLastError() != hipSuccess) return -1;
@@ -2056,7 +2061,7 @@ int launch_drain(Workspace &w)
     if (hipEventRecord(w.fin_ready, s) != hipSuccess) return -1;
     hipLaunchKernelGGL(wf_finish_bvh<false>, dim3(fgrid), dim3(WF_BLOCK), 0, s, w.last_sc, fr, w.last_cam, st, 0);
     if (hipGetLastError() != hipSuccess) return -1;
-    Pipe &lp = w.pipe[1 + (int)(w.call_seq & 1)];
+    Pipe &lp = w.pipe[1 + (WF_LONG_PINGPONG ? (int)(w.call_seq & 1) : 0)];
     if (hipStreamWaitEvent(lp.stream, w.fin_ready, 0) != hipSuccess) return -1;
     hipLaunchKernelGGL(wf_long<false>, dim3(WF_LONG_BLOCKS), dim3(WF_BLOCK), 0, lp.stream, w.last_sc, fr, w.last_cam, st, 1);
     if (hipGetLastError() != hipSuccess) return -1;
