@@ -95,7 +95,7 @@ static_assert(WF_BLOCK % WF_TBLOCK == 0 && WF_TBLOCK % 64 == 0, "WF_TBLOCK must 
 #define WF_BVH_WAVES 6  // wf_trace_bvh occupancy target
 #endif
 #ifndef WF_LONG_PINGPONG
-#define WF_LONG_PINGPONG 1 // whole-call mode: wf_long on pipelines 1 and 2 alternately (0: always pipeline 1)
+#define WF_LONG_PINGPONG 0 // whole-call mode: wf_long always on pipeline 1 (1: pipelines 1 and 2 alternately; +1.6 % with one grid, profiles/r04/ab)
 #endif
 #ifndef WF_FIN_BVH_WAVES
 #define WF_FIN_BVH_WAVES 5 // wf_finish_bvh occupancy target (5: +3 % over 6 with the 4-wide s_min query, profiles/r04)
