@@ -94,6 +94,9 @@ static_assert(WF_BLOCK % WF_TBLOCK == 0 && WF_TBLOCK % 64 == 0, "WF_TBLOCK must 
 #ifndef WF_BVH_WAVES
 #define WF_BVH_WAVES 6  // wf_trace_bvh occupancy target
 #endif
+#ifndef WF_CHECK_BLOCKS
+#define WF_CHECK_BLOCKS 256 // wf_check's grid (it runs beside the next call's finisher)
+#endif
 #ifndef WF_LONG_PINGPONG
 #define WF_LONG_PINGPONG 0 // whole-call mode: wf_long always on pipeline 1 (1: pipelines 1 and 2 alternately; +1.6 % with one grid, profiles/r04/ab)
 #endif
@@ -1686,6 +1689,10 @@ struct Workspace {
     uint32_t *fin_live = nullptr; // 8 producer words (whole-call mode, one per call in flight: call % 8)
     RtF4 *chk = nullptr;          // the exactness guard's records (WF_CHECK_CAP x 3 RtF4) and their counter
     uint32_t *chk_ctr = nullptr;
+    // the guard runs on pipeline 2's stream beside the next call's finisher: records and counter
+    // per call parity, and the event after each parity's wf_check (the call two later waits for it)
+    hipEvent_t chk_done[2] = {};
+    bool chk_rec[2] = {false, false};
     unsigned long long call_seq = 0;
     bool chain_open = false; // the last call was a whole-call call with RtOptions.overlap
     ChainKey key{};
@@ -1721,6 +1728,8 @@ int ensure_streams(Workspace &w, int npipes)
         if (hipEventCreateWithFlags(&w.fork, hipEventDisableTiming) != hipSuccess) return -1;
         if (hipEventCreateWithFlags(&w.fin_ready, hipEventDisableTiming) != hipSuccess) return -1;
         if (hipEventCreateWithFlags(&w.long_ev, hipEventDisableTiming) != hipSuccess) return -1;
+        for (auto &e : w.chk_done)
+            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return -1;
         if (hipEventCreate(&w.ev0) != hipSuccess || hipEventCreate(&w.ev1) != hipSuccess) return -1;
         w.streams_ok = true;
     }
@@ -1769,7 +1778,7 @@ int ensure(Workspace &w, size_t slots, int grid, int npipes)
     // long-path hand-off (shared by the pipelines), wf_long's stack-free wide traversal needs no spill;
     // the cross-check records
     const size_t o_le = take(slots * 8), o_lr = take(slots * 32), o_lc = take(256), o_rr = take(slots * 8),
-                 o_rc = take(256), o_hv = take(slots), o_ctl = take(256), o_chk = take((size_t)WF_CHECK_CAP * 48);
+                 o_rc = take(256), o_hv = take(slots), o_ctl = take(256), o_chk = take(2 * (size_t)WF_CHECK_CAP * 48);
     // per pipeline (path lists sized for every pixel: a pipeline never holds
     // more; ray queues for two rays per path: a shadow and an extension ray)
     size_t o_qs0[WF_MAX_PIPES], o_qs1[WF_MAX_PIPES], o_qr0[WF_MAX_PIPES], o_qr1[WF_MAX_PIPES], o_h[WF_MAX_PIPES],
@@ -1920,8 +1929,9 @@ int launch_whole(Workspace &w, int dev, const RtDevScene &sc, const RtDevFrame &
     st.heavy_first = long_return;
     st.linger = overlap ? 0ull : WF_FIN_LINGER;
     st.chk_mask = check_mask;
-    st.chk = check_mask == 0xFFFFFFFFu ? nullptr : w.chk;
-    st.chk_ctr = w.chk_ctr;
+    const int par = (int)(w.call_seq & 1);
+    st.chk = check_mask == 0xFFFFFFFFu ? nullptr : w.chk + 3 * (size_t)WF_CHECK_CAP * (size_t)par;
+    st.chk_ctr = w.chk_ctr + par;
     st.chk_fault = (debug & RT_DEBUG_CHECK_FAULT) ? 1 : 0;
     // debug (RT_DEBUG_LONG_LOG): every deep sample's claim / end time and bounces
     static unsigned long long *long_log_buf = nullptr;
@@ -1956,7 +1966,10 @@ int launch_whole(Workspace &w, int dev, const RtDevScene &sc, const RtDevFrame &
     if (hipMemsetAsync(st.counts, 0, 256, s) != hipSuccess) return -1;
     if (st.fin_live && hipMemsetD32Async((hipDeviceptr_t)st.fin_live, (int)(fgrid * (WF_BLOCK / 64)), 1, s) != hipSuccess)
         return -1;
-    if (st.chk && hipMemsetAsync(st.chk_ctr, 0, 4, s) != hipSuccess) return -1;
+    if (st.chk) { // (this parity's records: after the wf_check of two calls ago)
+        if (w.chk_rec[par] && hipStreamWaitEvent(s, w.chk_done[par], 0) != hipSuccess) return -1;
+        if (hipMemsetAsync(st.chk_ctr, 0, 4, s) != hipSuccess) return -1;
+    }
     if (long_return && hipMemsetD32Async((hipDeviceptr_t)st.chain_flag, overlap ? 1 : 0, 1, s) != hipSuccess) return -1;
     const int tiles = ((fr.width + 15) / 16) * ((fr.height + 15) / 16);
     hipLaunchKernelGGL(wf_start<false>, dim3(tiles), dim3(WF_BLOCK), 0, s, fr, cam, st, 0, 1);
@@ -1975,11 +1988,24 @@ int launch_whole(Workspace &w, int dev, const RtDevScene &sc, const RtDevFrame &
         if (hipEventRecord(lp->long_done, lp->stream) != hipSuccess) return -1;
         lp->long_rec = true;
     }
-    if (st.chk) {
-        hipLaunchKernelGGL(wf_check, dim3(grid), dim3(WF_BLOCK), 0, s, sc, st, fr.dev_stats);
-        if (hipGetLastError() != hipSuccess) return -1;
-    }
     if (!mark(4)) return -1;
+    if (st.chk) {
+        // the guard's re-traces beside the next call (pipeline 2): latency-bound single-lane KD
+        // traversals, 256 blocks
+        // (its KD stacks spill into pipeline 2's area: pipeline 0's belongs to the next finisher)
+        Pipe &cp = w.pipe[2];
+        WfState cs = st;
+        cs.spill = cp.st.spill;
+        if (!cs.spill) return -1;
+        if (hipEventRecord(pp.fin_done, s) != hipSuccess || hipStreamWaitEvent(cp.stream, pp.fin_done, 0) != hipSuccess)
+            return -1;
+        hipLaunchKernelGGL(wf_check, dim3(WF_CHECK_BLOCKS), dim3(WF_BLOCK), 0, cp.stream, sc, cs, fr.dev_stats);
+        if (hipGetLastError() != hipSuccess) return -1;
+        if (hipEventRecord(w.chk_done[par], cp.stream) != hipSuccess || hipEventRecord(cp.join, cp.stream) != hipSuccess)
+            return -1;
+        w.chk_rec[par] = true;
+        cp.joined = true;
+    }
     if (hipEventRecord(pp.join, s) != hipSuccess) return -1;
     pp.joined = true;
     // join: the caller's stream continues after the finisher — and, unless the
@@ -2193,7 +2219,7 @@ void rt_wavefront_shutdown()
             if (p.host_count) (void)hipHostFree(p.host_count);
             if (p.stream) (void)hipStreamDestroy(p.stream);
         }
-        for (hipEvent_t e : {w->ev1, w->ev0, w->long_ev, w->fin_ready, w->fork})
+        for (hipEvent_t e : {w->chk_done[1], w->chk_done[0], w->ev1, w->ev0, w->long_ev, w->fin_ready, w->fork})
             if (e) (void)hipEventDestroy(e);
         delete w;
         kv.second = nullptr;

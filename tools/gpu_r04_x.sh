@@ -1,9 +1,7 @@
-# round 4: cheapest pixels last (WF_LPT) — parity of the variant, its tail stamps, headline bench A/B
+# round 4: the guard (wf_check) beside the next call's finisher — GPU suite on it, headline bench A/B
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-O=gpurun_out/r04l2; mkdir -p $O
-ISAKLM_RT_LIB_OVERRIDE=$PWD/ab_libs/lpt.so timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_gpu_chain.py tests/ -k "chain or every_pixel or deep_paths or adversarial" > $O/pytest_lpt.log 2>&1; tail -2 $O/pytest_lpt.log
-grep -q " passed" $O/pytest_lpt.log && ! grep -q "failed\|error" $O/pytest_lpt.log || exit 1
-ISAKLM_RT_LIB_OVERRIDE=$PWD/ab_libs/lpt_stamp.so timeout -k 10 300 python bench.py --no-pmc --no-cpu-baseline --steps 20 --warmup 5 --debug 1 > $O/stamp.json 2> $O/stamp.err || exit 1
-grep "exhausted" $O/stamp.err
-timeout -k 10 1200 bash tools/gpu_ab_bench.sh r04l2 2 ab_libs/base_r04.so ab_libs/lpt.so
+O=gpurun_out/r04c3; mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1; tail -2 $O/pytest.log
+grep -q " passed" $O/pytest.log && ! grep -q "failed\|error" $O/pytest.log || exit 1
+timeout -k 10 1200 bash tools/gpu_ab_bench.sh r04c3 2 ab_libs/base_r04.so ab_libs/chk2.so
