@@ -236,7 +236,8 @@ int rt_set_device(int device);
 int rt_synchronize(void);
 /* `stream` (NULL: the calling thread) waits for every rt_render's device work
  * on the current device, including the deep-path tails that chained calls
- * (RtOptions.overlap) leave running past their stream point */
+ * (RtOptions.overlap) leave running past their stream point (an open chain is
+ * drained first: one more finisher launch for the pixels still owed passes) */
 int rt_join(void *stream);
 /* releases the library's per-device workspaces (streams, events, device
  * buffers) after their device work is done; registered with atexit by
@@ -460,7 +461,10 @@ typedef struct RtOptions {
      * is bit-identical to unchained calls.  Whatever reads the frame in
      * between must join first: rt_join(stream), rt_synchronize, or the
      * library's own readers (rt_tonemap, rt_save_render, rt_gbuffer_save,
-     * rt_reduce_shards, rt_deviation_stats), which join by themselves.  The
+     * rt_reduce_shards, rt_deviation_stats), which join by themselves.  A
+     * join of an open chain first enqueues its drain (the pixels still owed
+     * passes run to the end); so do a call that does not continue the chain
+     * and rt_shutdown.  The
      * reference's render() (rt/render.cuh:62-76) has no such tail: a call is
      * complete when its launches are (rt/main.cu:114-155). */
     int overlap;
