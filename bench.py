@@ -513,12 +513,15 @@ def main(argv=None, binding=None):
     bounded = wavefront and args.traversal == "bounded"
     spc = max(1, args.steps_per_call)
     profiles = []
+    # chained calls only where the timed region has several calls to chain (a lone call is
+    # faster unchained: its finisher takes returned pixels back at once instead of a drain)
+    chain = bool(args.overlap) and len(call_plan(args.warmup, args.steps, spc)) > 1
 
     def steps(first, count):
         """render steps [first, first + count) in calls of up to spc steps"""
         for start, k in call_plan(first, count, spc):
             rt.render(dscene, gb, host.camera, 0 if start == 0 else 1,
-                      rt.options(W, H, P * k, profile=wavefront, overlap=bool(args.overlap), **render_kw))
+                      rt.options(W, H, P * k, profile=wavefront, overlap=chain, **render_kw))
             if wavefront:
                 profiles.append(dict(rt.last_profile(), passes=P * k))
 
@@ -710,7 +713,7 @@ def main(argv=None, binding=None):
                          f"{'on (min ' + str(args.min_samples) + ')' if args.adaptive else 'off'}, "
                          f"max depth {args.max_depth or 'unbounded'}"),
             "adaptive": args.adaptive, "max_depth": args.max_depth,
-            "scene": args.scene, "width": W, "height": H, "spp_per_step": P, "steps_per_call": spc,
+            "scene": args.scene, "width": W, "height": H, "spp_per_step": P, "steps_per_call": spc, "chained_calls": chain,
             "triangles": info["triangles"], "kd_nodes": info["nodes"], "kd_indices": info["indices"],
             "parallelism": parallelism,
         },
