@@ -561,15 +561,17 @@ def main(argv=None, binding=None):
     if dist:  # every rank's statistics (sums; max of the longest path)
         import torch
 
+        hk = list(getattr(rt, "HANDOFF_FIELDS", ()))
         dv = torch.tensor([dev["watchdog_paths"], dev["cut_paths"], dev["deep_paths"], dev["bounded_checked"],
-                           dev["bounded_mismatches"]] + dev["deep_hist"], dtype=torch.int64)
+                           dev["bounded_mismatches"]] + [dev.get(k, 0) for k in hk] + dev["deep_hist"],
+                          dtype=torch.int64)
         dist.all_reduce(dv)
         mx = torch.tensor([dev["max_deep_depth"]], dtype=torch.int64)
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         v = [int(x) for x in dv.tolist()]
         dev = {"watchdog_paths": v[0], "cut_paths": v[1], "deep_paths": v[2], "bounded_checked": v[3],
-               "bounded_mismatches": v[4], "deep_hist": v[5:], "max_deep_depth": int(mx.item()),
-               "mismatch_ray": dev.get("mismatch_ray")}
+               "bounded_mismatches": v[4], **dict(zip(hk, v[5:5 + len(hk)])), "deep_hist": v[5 + len(hk):],
+               "max_deep_depth": int(mx.item()), "mismatch_ray": dev.get("mismatch_ray")}
     total_samples = world * n * P * args.steps
     value = total_samples / elapsed / 1e6
     acc = gb.download()[2]
@@ -590,30 +592,36 @@ def main(argv=None, binding=None):
         launches = sum(p["trace_launches"] for p in profiles)
         avg_launch_ms = sum(p["trace_ms"] for p in profiles) / max(launches, 1)
         if bounded:
-            # the dominant kernel (the bounded finisher runs the whole call, one
-            # launch per pipeline) and its own work: one more call with the
-            # kernels counting (RT_TRAVERSAL_BOUNDED_COUNTED)
-            # (the timed calls' shape: passes x steps-per-call, so its bytes per
-            # launch and the timed launches' duration describe the same launch)
+            # the dominant kernel (the bounded finisher runs the whole call: one
+            # launch per call) and its own work: one more call of the timed
+            # calls' shape (passes x steps-per-call, the whole-call finisher) with
+            # that finisher counting its own work (RT_TRAVERSAL_BOUNDED_COUNTED:
+            # its COUNT instantiation, one launch)
             bcnt = rt.DeviceCounters()
             cp = P * call_steps(args)
             rt.render(dscene, gb, host.camera, 1, rt.options(W, H, cp, counters=bcnt.p, profile=True,
                                                              **dict(render_kw, traversal=rt.TRAVERSAL_BOUNDED_COUNTED)))
             bc = bcnt.read(finisher=True)
             cprof = rt.last_profile()
-            trace_bytes = bounded_kernel_bytes(bc)
             kname = "wf_finish_bvh<false>"
             launches = sum(p["finish_launches"] for p in profiles)
             avg_launch_ms = sum(p["finish_ms"] for p in profiles) / max(launches, 1)
             counted_launches = cprof["finish_launches"]
+            # per launch: the counted bytes per sample x the samples one timed launch runs
+            # (every pixel's passes of its call: W x H x passes-per-call, adaptive off)
+            samples_per_launch = n * sum(p["passes"] for p in profiles) / max(launches, 1)
+            trace_bytes = bounded_kernel_bytes(bc) / max(bc["sample"], 1) * samples_per_launch
+            counted_launches = 1
             work = {"rays": bc["ray"], "bvh_nodes_per_ray": round(bc["b_bvh_node"] / max(bc["ray"], 1), 2),
                     "bvh_tests_per_ray": round(bc["b_bvh_tri"] / max(bc["ray"], 1), 2),
                     "kd_nodes_per_ray": round(bc["node"] / max(bc["ray"], 1), 2),
                     "kd_tests_per_ray": round(bc["tri"] / max(bc["ray"], 1), 2),
                     "bary_per_ray": round(bc["b_bary"] / max(bc["ray"], 1), 2),
                     "rays_per_sample": round(bc["ray"] / max(bc["sample"], 1), 3),
-                    "bytes_per_sample": round(trace_bytes / max(bc["sample"], 1), 1),
+                    "bytes_per_sample": round(bounded_kernel_bytes(bc) / max(bc["sample"], 1), 1),
                     "counted_call_passes": cp,
+                    "counted_call_launches": cprof["finish_launches"],
+                    "samples_per_timed_launch": round(samples_per_launch),
                     "scope": "the finisher's paths; the deep paths handed to wf_long (depth > 64) are not counted"}
         else:
             cprof = rt.last_profile()
@@ -658,6 +666,10 @@ def main(argv=None, binding=None):
                     traffic=round(detail["hbm_bytes_per_sample"] * n * P), **detail)
         roof["traffic_unit"] = (f"HBM bytes per step of {P} passes (whole frame, every kernel), from one profiled "
                                 f"call of {P * call_steps(args)} passes = the timed calls' shape")
+        roof["pmc_call_shape"] = ("one UNCHAINED call of the timed calls' passes: counter collection serialises "
+                                  "dispatches, so the chained calls' overlap (a call's deep-path tail beside the "
+                                  "next call's finisher) cannot run under it; the finisher kernel and its per-sample "
+                                  "work are the same, the bytes per sample are applied to the chained timed rate")
         dk = detail["per_kernel"].get(detail["dominant_kernel"] or "", {})
         if wavefront and dk.get("dispatches") and kernel_detail["kernel"].split("<")[0] in (detail["dominant_kernel"] or ""):
             # the dominant kernel alone: its counter bytes per launch / its live
@@ -729,6 +741,12 @@ def main(argv=None, binding=None):
             "watchdog_limit": 16777215,
             "deep_pushes": c["deep_push"], "deep_pushes_scope": "one extra counted call of the same options",
             "bounded_checked": dev.get("bounded_checked"), "bounded_mismatches": dev.get("bounded_mismatches"),
+            "handoff": {k: dev.get(k) for k in getattr(rt, "HANDOFF_FIELDS", ())},
+            "handoff_note": "the deep-path hand-off over the timed region: owed_pixels / owed_passes = pixels that "
+                            "chained calls skipped while out in wf_long and the passes run for them later (the "
+                            "chained-call protocol firing); long_safety_quits, stranded_pixels, check_dropped = "
+                            "failure signals (0 in a working render); linger_expiries = finisher waves that stopped "
+                            "waiting for pixels out in wf_long",
             "bounded_check_note": "run-time guard of the BVH-bounded traversal: a deterministic 1-in-"
                                   f"{args.check_interval or 4096} sample of the finisher's rays, re-traced by the "
                                   "plain KD traversal (trace_ray) inside the timed region and compared bit for bit",

@@ -55,10 +55,12 @@ extern "C" {
  * rt_deviation_stats, rt_abi_version; 4 = RT_CNT_COUNT 40 (the optional
  * counters buffer grew); 5 = RtOptions.traversal; 6 = RtOptions.overlap /
  * check_interval / debug, RtDeviations' bounded-traversal guard fields,
- * rt_join, rt_shutdown.  An integrator checks rt_abi_version() ==
- * RT_ABI_VERSION at start-up: a binary built against an older header would
- * otherwise link (C linkage) and mis-pass arguments. */
-#define RT_ABI_VERSION 6
+ * rt_join, rt_shutdown; 7 = RtDeviations' hand-off fields (owed passes,
+ * safety-net exits, stranded pixels, dropped guard records, linger
+ * expiries), RT_E_INCOMPLETE from the joins.  An integrator checks
+ * rt_abi_version() == RT_ABI_VERSION at start-up: a binary built against an
+ * older header would otherwise link (C linkage) and mis-pass arguments. */
+#define RT_ABI_VERSION 7
 
 /* CUDA uchar4, used for texels (rt/scene.cuh:18) */
 typedef struct RtUChar4 { uint8_t x, y, z, w; } RtUChar4;
@@ -203,6 +205,8 @@ ISAKLM_RT_CHECK_LAYOUT()
 #define RT_E_PARSE (-4)     /* malformed OBJ / .mat / scene file */
 #define RT_E_UNSUPPORTED (-5) /* e.g. KD tree deeper than the traversal stack */
 #define RT_E_NOMEM (-6)
+#define RT_E_INCOMPLETE (-7) /* a join found pixels whose deep-path samples never came back
+                              * (RtDeviations.stranded_pixels): the frame misses passes */
 
 const char *rt_last_error(void);
 const char *rt_version(void);
@@ -233,11 +237,17 @@ int rt_device_count(int *count);
  * pipelines' streams there (call it before other GPU users of the process,
  * e.g. RCCL, take the hardware queues) */
 int rt_set_device(int device);
+/* hipDeviceSynchronize after rt_join(NULL): chained renders are complete */
 int rt_synchronize(void);
 /* `stream` (NULL: the calling thread) waits for every rt_render's device work
  * on the current device, including the deep-path tails that chained calls
  * (RtOptions.overlap) leave running past their stream point (an open chain is
- * drained first: one more finisher launch for the pixels still owed passes) */
+ * drained first: one more finisher launch for the pixels still owed passes).
+ * After the drain every pixel handed to the long-path kernel must be back; a
+ * check kernel verifies it (and releases any that are not).  Host joins
+ * (NULL, and rt_synchronize, rt_download, rt_tonemap / rt_save_render without
+ * a stream, rt_gbuffer_save) return RT_E_INCOMPLETE if that check — theirs or
+ * an earlier stream join's — found stranded pixels; RtDeviations counts them. */
 int rt_join(void *stream);
 /* releases the library's per-device workspaces (streams, events, device
  * buffers) after their device work is done; registered with atexit by
@@ -483,6 +493,8 @@ typedef struct RtOptions {
 #define RT_DEBUG_CALL_LOG 1  /* per call / queue iteration: counters and host times */
 #define RT_DEBUG_LONG_LOG 2  /* every deep sample's claim / end time and bounces (unchained calls) */
 #define RT_DEBUG_CHECK_FAULT 4 /* tests of the guard: every checked ray is recorded with a wrong result */
+#define RT_DEBUG_LONG_QUIT 8   /* tests of the failure path: the long-path kernel leaves at once, as if its
+                                * safety net fired, stranding every pixel handed to it */
 
 /* Per-call kernel timing of the last rt_render on this device with
  * RtOptions.profile = 1 (wavefront kernels; HIP events on the call's stream,
@@ -523,6 +535,25 @@ typedef struct RtDeviations {
     unsigned long long bounded_checked;
     unsigned long long bounded_mismatches;
     float mismatch_ray[6];
+    /* the deep-path hand-off of the default render (ABI 7):
+     * owed_pixels / owed_passes: pixels taken back from the long-path kernel
+     * that chained calls (RtOptions.overlap) had skipped, and the passes they
+     * owed (run by the taker, in the pixel's order; > 0 shows the chained-call
+     * protocol fired).  Failure signals, 0 in a working render:
+     * long_safety_quits: long-path waves that left by a safety net while
+     * handed-over paths were still unclaimed; stranded_pixels: pixels still
+     * handed over after a join's drain (the frame is incomplete: the join
+     * returns RT_E_INCOMPLETE, and the pixels are released so later renders
+     * run); check_dropped: rays the guard sampled past its per-call record
+     * capacity (not re-traced).  linger_expiries: finisher waves that stopped
+     * waiting (1 s) for pixels out in the long-path kernel, which then
+     * finishes those pixels itself (a slow tail, not an error). */
+    unsigned long long owed_pixels;
+    unsigned long long owed_passes;
+    unsigned long long long_safety_quits;
+    unsigned long long stranded_pixels;
+    unsigned long long check_dropped;
+    unsigned long long linger_expiries;
 } RtDeviations;
 int rt_deviation_stats(RtDeviations *out, int reset);
 

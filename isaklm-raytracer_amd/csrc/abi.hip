@@ -51,6 +51,23 @@ void rt_set_error(const char *fmt, ...)
         }                                                                                            \
     } while (0)
 
+const char *rt_wavefront_incomplete_msg();
+
+// rt_wavefront_join with the ABI's status: RT_E_INCOMPLETE when the join's
+// hand-off check found stranded pixels (a chained render's frame misses
+// passes), RT_E_HIP on a HIP failure; `who` names the entry point
+static int join_status(void *stream, const char *who)
+{
+    const int rc = rt_wavefront_join(stream);
+    if (rc == 0) return RT_OK;
+    if (rc == RT_WAVEFRONT_INCOMPLETE) {
+        rt_set_error("%s: %s", who, rt_wavefront_incomplete_msg());
+        return RT_E_INCOMPLETE;
+    }
+    rt_set_error("%s: join: %s", who, hipGetErrorString(hipGetLastError()));
+    return RT_E_HIP;
+}
+
 struct RtPreparedScene {
     RtDevScene dev;
     std::vector<void *> allocs;
@@ -195,14 +212,7 @@ void rt_shutdown(void)
     g_dev_stats.clear();
 }
 
-int rt_join(void *stream)
-{
-    if (rt_wavefront_join(stream) != 0) {
-        rt_set_error("rt_join: %s", hipGetErrorString(hipGetLastError()));
-        return RT_E_HIP;
-    }
-    return RT_OK;
-}
+int rt_join(void *stream) { return join_status(stream, "rt_join"); }
 
 int rt_deviation_stats(RtDeviations *out, int reset)
 {
@@ -210,6 +220,10 @@ int rt_deviation_stats(RtDeviations *out, int reset)
     unsigned long long *d = dev_stats_block();
     if (!d) { rt_set_error("rt_deviation_stats: no device block"); return RT_E_HIP; }
     unsigned long long w[RT_DEV_WORDS];
+    // (chained renders joined first, so their statistics are complete; stranded
+    // pixels are not an error here: stranded_pixels reports them)
+    const int jr = join_status(nullptr, "rt_deviation_stats");
+    if (jr != RT_OK && jr != RT_E_INCOMPLETE) return jr;
     HIPCHK(hipDeviceSynchronize());
     HIPCHK(hipMemcpy(w, d, sizeof w, hipMemcpyDeviceToHost));
     memset(out, 0, sizeof *out);
@@ -227,6 +241,12 @@ int rt_deviation_stats(RtDeviations *out, int reset)
         memcpy(&out->mismatch_ray[2 * k], &hi, 4);
         memcpy(&out->mismatch_ray[2 * k + 1], &lo, 4);
     }
+    out->owed_pixels = w[RT_DEV_OWED_PIXELS];
+    out->owed_passes = w[RT_DEV_OWED_PASSES];
+    out->long_safety_quits = w[RT_DEV_LONG_QUIT];
+    out->stranded_pixels = w[RT_DEV_STRANDED];
+    out->check_dropped = w[RT_DEV_CHK_DROP];
+    out->linger_expiries = w[RT_DEV_LINGER_EXP];
     if (reset) HIPCHK(hipMemset(d, 0, RT_DEV_WORDS * 8));
     return RT_OK;
 }
@@ -255,10 +275,8 @@ int rt_download(void *dst, const void *src, size_t bytes)
     if (bytes == 0) return RT_OK;
     if (!dst || !src) { rt_set_error("rt_download: null pointer"); return RT_E_INVALID; }
     // (cudaMemcpy after a render waits for it; so does this, chained renders' tails included)
-    if (rt_wavefront_join(nullptr) != 0) {
-        rt_set_error("rt_download: join: %s", hipGetErrorString(hipGetLastError()));
-        return RT_E_HIP;
-    }
+    const int jr = join_status(nullptr, "rt_download");
+    if (jr != RT_OK) return jr;
     HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
     return RT_OK;
 }
@@ -286,6 +304,10 @@ int rt_set_device(int device)
 }
 int rt_synchronize(void)
 {
+    // (chained renders' open chain drained first: hipDeviceSynchronize alone never
+    // enqueues the drain, and their owed passes would never run)
+    const int jr = join_status(nullptr, "rt_synchronize");
+    if (jr != RT_OK) return jr;
     HIPCHK(hipDeviceSynchronize());
     return RT_OK;
 }
@@ -383,7 +405,11 @@ int rt_gbuffer_save(G_Buffer g, int width, int height, int sample_count, const c
     }
     const size_t n = (size_t)width * height;
     std::vector<uint8_t> buf(n * 24);
-    HIPCHK(hipDeviceSynchronize()); // rt_render's pipelines run on their own non-blocking streams
+    // rt_render's pipelines run on their own non-blocking streams, and a chained render's
+    // owed passes run only in the open chain's drain: join (drain) first, then synchronise
+    const int jr = join_status(nullptr, "rt_gbuffer_save");
+    if (jr != RT_OK) return jr;
+    HIPCHK(hipDeviceSynchronize());
     HIPCHK(hipMemcpy(buf.data(), g.frame_buffer, n * 12, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(buf.data() + n * 12, g.squared_luminance, n * 4, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(buf.data() + n * 16, g.sample_count, n * 4, hipMemcpyDeviceToHost));
@@ -439,7 +465,11 @@ int rt_gbuffer_load(const char *path, G_Buffer g, int width, int height, int *sa
         rt_set_error("rt_gbuffer_load: %s is truncated", path);
         return RT_E_PARSE;
     }
-    HIPCHK(hipDeviceSynchronize()); // no render may still be writing this G_Buffer
+    // no render may still be writing this G_Buffer (a chained render's tail drained and
+    // joined first; the chain is closed, so the next call does not continue it)
+    const int jr = join_status(nullptr, "rt_gbuffer_load");
+    if (jr != RT_OK && jr != RT_E_INCOMPLETE) return jr; // (the frame is overwritten anyway)
+    HIPCHK(hipDeviceSynchronize());
     HIPCHK(hipMemcpy(g.frame_buffer, buf.data(), n * 12, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(g.squared_luminance, buf.data() + n * 12, n * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(g.sample_count, buf.data() + n * 16, n * 4, hipMemcpyHostToDevice));
@@ -777,10 +807,13 @@ int rt_render(rt_scene_t scene, G_Buffer g, Camera cam, int sample_count, const 
             rt_set_error("rt_render: wavefront launch failed: %s", hipGetErrorString(hipGetLastError()));
             return RT_E_HIP;
         }
-    } else if (rt_wavefront_join(stream) != 0 || // (chained wavefront calls' tails first: same frame state)
-               rt_launch_path(scene->dev, fr, dc, scene->max_depth, stream, o.traversal) != 0) {
-        rt_set_error("rt_render: kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
-        return RT_E_HIP;
+    } else {
+        const int jr = join_status(stream, "rt_render"); // (chained wavefront calls' tails first: same frame state)
+        if (jr != RT_OK) return jr;
+        if (rt_launch_path(scene->dev, fr, dc, scene->max_depth, stream, o.traversal) != 0) {
+            rt_set_error("rt_render: kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
+            return RT_E_HIP;
+        }
     }
     if (!o.stream) HIPCHK(hipStreamSynchronize(nullptr));
     return RT_OK;
@@ -792,8 +825,9 @@ int rt_tonemap(G_Buffer g, uint8_t *rgba, int w, int h, void *stream)
         rt_set_error("rt_tonemap: bad arguments");
         return RT_E_INVALID;
     }
-    if (rt_wavefront_join(stream) != 0 || // chained renders' deep-path tails first
-        rt_launch_tonemap(g.frame_buffer, g.sample_count, (RtUChar4 *)rgba, w * h, (hipStream_t)stream) != 0) {
+    const int jr = join_status(stream, "rt_tonemap"); // chained renders' deep-path tails first
+    if (jr != RT_OK) return jr;
+    if (rt_launch_tonemap(g.frame_buffer, g.sample_count, (RtUChar4 *)rgba, w * h, (hipStream_t)stream) != 0) {
         rt_set_error("rt_tonemap: launch failed");
         return RT_E_HIP;
     }

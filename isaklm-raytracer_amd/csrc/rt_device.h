@@ -52,8 +52,18 @@
 #define RT_DEV_CHECKED 21   // rays of the bounded traversal re-traced by the KD traversal (wf_check)
 #define RT_DEV_MISMATCH 22  // ... whose results differed
 #define RT_DEV_MISRAY 23    // 4 words: set flag, then the first mismatching ray's o, d as packed float bits
-#define RT_DEV_WORDS 32
-static_assert(RT_DEV_HIST + RT_DEV_HIST_BINS <= RT_DEV_CHECKED && RT_DEV_MISRAY + 4 <= RT_DEV_WORDS,
+// the chained-call hand-off protocol (wavefront.hip), one atomic per rare event:
+#define RT_DEV_OWED_PIXELS 27 // pixels taken back from wf_long owing passes of later chained calls
+#define RT_DEV_OWED_PASSES 28 // ... the passes they owed (run by the taker, in order)
+#define RT_DEV_LONG_QUIT 29   // wf_long waves that left by a safety net with hand-off entries unclaimed
+#define RT_DEV_LINGER_EXP 30  // finisher waves whose linger expired with pixels still out in wf_long
+#define RT_DEV_CHK_DROP 31    // guard records dropped past WF_CHECK_CAP (rays not re-traced)
+#define RT_DEV_STRANDED 32    // pixels found still OUT after a join's drain (wf_verify): an incomplete frame
+#define RT_DEV_WORDS 48
+// rt_wavefront_join's return when its hand-off check found stranded pixels (-1: a HIP failure)
+#define RT_WAVEFRONT_INCOMPLETE (-2)
+static_assert(RT_DEV_HIST + RT_DEV_HIST_BINS <= RT_DEV_CHECKED && RT_DEV_MISRAY + 4 <= RT_DEV_OWED_PIXELS &&
+                  RT_DEV_STRANDED < RT_DEV_WORDS,
               "deviation block");
 
 struct RtDevMaterial {          // 64 B

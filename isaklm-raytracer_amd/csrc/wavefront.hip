@@ -121,12 +121,18 @@ static_assert(WF_BLOCK % WF_TBLOCK == 0 && WF_TBLOCK % 64 == 0, "WF_TBLOCK must 
 #ifndef WF_LONG_BLOCKS
 #define WF_LONG_BLOCKS 64 // wf_long grid (4 waves each, one path per wave at a time)
 #endif
-// safety nets (s_memrealtime ticks, 100 MHz), never reached by a working
-// protocol: a wf_long slice wave leaves after 20 s without a claim; a
-// persistent wf_long wave (whole-call mode) after 600 s without a claim.
-// Either strands pixels instead of hanging the GPU.
-#define WF_LONG_IDLE 2000000000ull
-#define WF_LONG_IDLE_PERSIST 60000000000ull
+// safety nets of wf_long's claim loop (s_memrealtime ticks, 100 MHz), never
+// reached by a working protocol.  Every other wait there is bounded by the
+// protocol itself: while its producers (the finisher waves of its call) live,
+// while another wave runs a path (bounded by that path's watchdog), or while
+// hand-off entries keep coming, the idle clock does not run; once none of
+// these holds, a persistent wave leaves within the chain window (50 ms) and a
+// slice wave at once.  What is left for the nets: an entry reserved but never
+// published (WF_LONG_PUBLISH_WAIT) and a broken chain flag (WF_LONG_IDLE).
+// A net exit with entries unclaimed strands pixels instead of hanging the GPU
+// — counted (RT_DEV_LONG_QUIT), found by the join's wf_verify and reported.
+#define WF_LONG_IDLE 200000000ull         // 2 s idle with nothing that could still bring work
+#define WF_LONG_PUBLISH_WAIT 100000000ull // 1 s on one reserved, unpublished entry (publication is ~1 us)
 // an idle persistent wf_long wave of an open chain stays until no entry has
 // been reserved (for any wave) for this long (50 ms) AND no wave runs a path:
 // the next calls' deep paths (WfState.chain_flag).  The grid leaves as a whole
@@ -138,7 +144,7 @@ static_assert(WF_BLOCK % WF_TBLOCK == 0 && WF_TBLOCK % 64 == 0, "WF_TBLOCK must 
 // (a KD re-trace costs ~50 bounded queries: 1024 took 4 % of a 256-pass
 // room2m call, 4096 ~1 %, and still checks ~2M rays in the 20-step bench)
 #define WF_CHECK_INTERVAL_DEFAULT 4096u
-#define WF_CHECK_CAP (1u << 20)         // cross-check records per call (more are dropped, not counted)
+#define WF_CHECK_CAP (1u << 20)         // cross-check records per call (more are dropped: RT_DEV_CHK_DROP)
 // per-pixel hand-off word (WfState.pxo): a pixel handed to wf_long is OUT
 // until a finisher takes it back or wf_long finishes it (LONGDONE: its state
 // was written by the concurrently running wf_long, so the next reader
@@ -210,6 +216,7 @@ struct WfState {
     uint32_t *chk_ctr;
     uint32_t chk_mask;
     int chk_fault; // (RT_DEBUG_CHECK_FAULT, tests: record a wrong result for every checked ray)
+    int debug_quit; // (RT_DEBUG_LONG_QUIT, tests: wf_long leaves at once, as by its safety net)
 };
 
 namespace {
@@ -1107,9 +1114,11 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_FIN_BVH_WAVES) wf_finish_bvh(RtDe
                     const uint32_t owed = __hip_atomic_exchange(st.pxo + (uint32_t)v, 0u, __ATOMIC_RELAXED,
                                                                 __HIP_MEMORY_SCOPE_AGENT);
                     p.passes_left += (int)(owed & RT_PX_PASSES);
-                    if (owed & RT_PX_PASSES) { // (statistics for RT_DEBUG_CALL_LOG: most passes owed, pixels owed)
+                    if (owed & RT_PX_PASSES) { // (RT_DEBUG_CALL_LOG: most passes owed, pixels owed; RtDeviations)
                         __hip_atomic_fetch_max(st.ret_ctr + 5, owed & RT_PX_PASSES, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         __hip_atomic_fetch_add(st.ret_ctr + 6, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        atomicAdd(fr.dev_stats + RT_DEV_OWED_PIXELS, 1ull);
+                        atomicAdd(fr.dev_stats + RT_DEV_OWED_PASSES, (unsigned long long)(owed & RT_PX_PASSES));
                     }
                 }
             }
@@ -1157,8 +1166,11 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_FIN_BVH_WAVES) wf_finish_bvh(RtDe
                 const uint32_t cl = __hip_atomic_load(ret_claimed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if ((uint32_t)w == cl && (!out || __builtin_amdgcn_s_memrealtime() - idle_since > st.linger) &&
                     __hip_atomic_compare_exchange_strong(ret_word, &w, w - (1ull << 32), __ATOMIC_RELAXED,
-                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
                     leave = 1;
+                    // (pixels still out: wf_long, finding no finisher alive, finishes them itself)
+                    if (out) atomicAdd(fr.dev_stats + RT_DEV_LINGER_EXP, 1ull);
+                }
             }
             if (__shfl(leave, 0)) break;
             __builtin_amdgcn_s_sleep(8);
@@ -1248,6 +1260,7 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_check(RtDevScene sc, WfState st, 
     Stack<WF_LDS_STACK> stk{s_node + tid, s_entry + tid, WF_BLOCK, st.spill + gtid, st.spill_threads};
     Cnt c;
     uint32_t n = *st.chk_ctr;
+    if (n > WF_CHECK_CAP && gtid == 0) atomicAdd(dev + RT_DEV_CHK_DROP, (unsigned long long)(n - WF_CHECK_CAP));
     n = n < WF_CHECK_CAP ? n : WF_CHECK_CAP;
     unsigned long long checked = 0, bad = 0;
     for (uint32_t e = gtid; e < n; e += gridDim.x * WF_BLOCK) {
@@ -1276,6 +1289,37 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_check(RtDevScene sc, WfState st, 
     if ((tid & 63) == 0) {
         if (checked) atomicAdd(dev + RT_DEV_CHECKED, checked);
         if (bad) atomicAdd(dev + RT_DEV_MISMATCH, bad);
+    }
+}
+
+// The join's check of the hand-off protocol (after every finisher, wf_long and
+// drain of the workspace is done): a pixel still OUT was handed to wf_long and
+// never came back — its frame misses passes.  Counts such pixels (and releases
+// them, so later calls run them again) and the protocol's counters that must
+// be balanced by now: pixels out, returns reserved but unclaimed, hand-off
+// entries reserved but unclaimed, finisher waves still registered alive.
+// res: [0] stranded pixels, [1..4] those counters (accumulated until the host reads them).
+__global__ void __launch_bounds__(WF_BLOCK) wf_verify(WfState st, uint32_t n, uint32_t *res, unsigned long long *dev)
+{
+    uint32_t out = 0;
+    for (uint32_t i = blockIdx.x * WF_BLOCK + threadIdx.x; i < n; i += gridDim.x * WF_BLOCK) {
+        const uint32_t x = st.pxo[i];
+        if (x & RT_PX_OUT) {
+            ++out;
+            st.pxo[i] = 0u;
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) out += __shfl_xor(out, off);
+    if ((threadIdx.x & 63) == 0 && out) {
+        atomicAdd(res, out);
+        atomicAdd(dev + RT_DEV_STRANDED, (unsigned long long)out);
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        const unsigned long long rw = *reinterpret_cast<const unsigned long long *>(st.ret_ctr);
+        res[1] += st.ret_ctr[3];
+        res[2] += (uint32_t)rw - st.ret_ctr[2];
+        res[3] += st.long_ctr[0] - st.long_ctr[1];
+        res[4] += (uint32_t)(rw >> 32);
     }
 }
 
@@ -1436,8 +1480,10 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_LONG_WAVES) wf_long(RtDevScene sc
     const int limit = fr.max_depth > 0 ? fr.max_depth : RT_WATCHDOG_BOUNCES;
     uint32_t *const reserved = st.long_ctr, *const claimed = st.long_ctr + 1, *const running = st.long_ctr + 3;
     const bool persist = st.fin_live != nullptr;
-    unsigned long long t_idle = __builtin_amdgcn_s_memrealtime();
-    uint32_t r_seen = 0;
+    unsigned long long t_idle = __builtin_amdgcn_s_memrealtime(); // (chain window: since entries last flowed)
+    unsigned long long t_net = t_idle; // safety net: since anything that could still bring work last held
+    unsigned long long t_pub = 0;      // since entry e_pub was first seen reserved but unpublished
+    uint32_t r_seen = 0, e_pub = 0xffffffffu;
     while (true) {
         // ---- claim the next published entry (lane 0): its tag and ray are read
         // before the claim (a claimed ring slot may be reused at once)
@@ -1446,19 +1492,28 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_LONG_WAVES) wf_long(RtDevScene sc
         int quit = 0;
         if (lane == 0) {
             while (true) {
+                const unsigned long long now = __builtin_amdgcn_s_memrealtime();
                 // (producers first: once they are all past their last hand-off,
                 // `reserved` read after this acquire holds every entry)
+                const bool producing =
+                    persist && __hip_atomic_load(st.fin_live, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+                const bool others = __hip_atomic_load(running, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
                 const bool done =
-                    persist && __hip_atomic_load(st.fin_live, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u &&
+                    persist && !producing &&
                     (__hip_atomic_load(st.chain_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u ||
-                     (__builtin_amdgcn_s_memrealtime() - t_idle > WF_LONG_CHAIN_IDLE &&
-                      __hip_atomic_load(running, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u));
+                     (now - t_idle > WF_LONG_CHAIN_IDLE && !others));
                 if (done) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                 e = __hip_atomic_load(claimed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 const uint32_t r = __hip_atomic_load(reserved, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (r != r_seen) { // entries still flowing (to any wave): not idle
+                const bool flowing = r != r_seen;
+                if (flowing) { // entries still flowing (to any wave): not idle
                     r_seen = r;
-                    t_idle = __builtin_amdgcn_s_memrealtime();
+                    t_idle = now;
+                }
+                if (flowing || producing || others) t_net = now; // work may still come: a bounded wait
+                if (st.debug_quit) { // (tests: as if the net fired at once)
+                    quit = 2;
+                    break;
                 }
                 if (e < r) {
                     const uint32_t k = e % st.long_cap;
@@ -1478,23 +1533,30 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_LONG_WAVES) wf_long(RtDevScene sc
                         }
                         continue; // another wave took it: try the next one
                     }
-                    // reserved, its publication still in flight: wait for it
+                    // reserved, its publication still in flight: wait for it (safety net: 1 s)
+                    if (e != e_pub) {
+                        e_pub = e;
+                        t_pub = now;
+                    } else if (now - t_pub > WF_LONG_PUBLISH_WAIT) {
+                        quit = 2;
+                        break;
+                    }
                 } else {
                     // nothing claimable.  Persistent: done once the producers are; slices: the
                     // final one once every entry is claimed, the others unless a path still runs.
-                    const bool others = __hip_atomic_load(running, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
                     if (persist ? done : (final_slice || !others)) {
                         quit = 1;
                         break;
                     }
                 }
-                if (__builtin_amdgcn_s_memrealtime() - t_idle > (persist ? WF_LONG_IDLE_PERSIST : WF_LONG_IDLE)) {
-                    quit = 1; // safety net (see WF_LONG_IDLE)
+                if (now - t_net > WF_LONG_IDLE) { // safety net (see WF_LONG_IDLE)
+                    quit = e < r ? 2 : 1;
                     break;
                 }
                 __builtin_amdgcn_s_sleep(16);
             }
             if (!quit) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (quit == 2) atomicAdd(fr.dev_stats + RT_DEV_LONG_QUIT, 1ull); // entries left unclaimed: stranded
         }
         // (lane 0's values, wave-uniform: readfirstlane — every lane is active here)
         if (__builtin_amdgcn_readfirstlane(quit)) break;
@@ -1548,6 +1610,10 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_LONG_WAVES) wf_long(RtDevScene sc
                         x = __hip_atomic_exchange(st.pxo + p.slot, RT_PX_OUT, __ATOMIC_RELAXED,
                                                   __HIP_MEMORY_SCOPE_AGENT);
                         p.passes_left = (int)(x & RT_PX_PASSES);
+                        if (x & RT_PX_PASSES) { // (RtDeviations: owed passes, run here in the pixel's order)
+                            atomicAdd(fr.dev_stats + RT_DEV_OWED_PIXELS, 1ull);
+                            atomicAdd(fr.dev_stats + RT_DEV_OWED_PASSES, (unsigned long long)(x & RT_PX_PASSES));
+                        }
                         const Vec3D fb = fr.fb[p.slot];
                         const float sq = fr.sq[p.slot];
                         const int count = fr.count[p.slot];
@@ -1687,8 +1753,17 @@ struct Workspace {
     hipEvent_t long_ev = nullptr; // after the last wf_long slice on the caller's stream (queue mode)
     bool recorded = false;   // long_ev recorded by a previous call
     uint32_t *fin_live = nullptr; // 8 producer words (whole-call mode, one per call in flight: call % 8)
-    RtF4 *chk = nullptr;          // the exactness guard's records (WF_CHECK_CAP x 3 RtF4) and their counter
+    RtF4 *chk = nullptr;          // the exactness guard's records (2 x WF_CHECK_CAP x 3 RtF4; allocated on
+                                  // the first call with the guard on) and their counter
     uint32_t *chk_ctr = nullptr;
+    // the join's hand-off check (wf_verify): its result words (own allocation: they outlive a
+    // blob reallocation), a whole call with the hand-off ran since the last check, a check's
+    // result not yet read by a host join
+    uint32_t *verify_res = nullptr;
+    bool verify_pending = false;
+    bool verify_unread = false;
+    int cus = 0;                                // compute units of the device (the finisher's grid)
+    unsigned long long *long_log_buf = nullptr; // RT_DEBUG_LONG_LOG records
     // the guard runs on pipeline 2's stream beside the next call's finisher: records and counter
     // per call parity, and the event after each parity's wf_check (the call two later waits for it)
     hipEvent_t chk_done[2] = {};
@@ -1731,6 +1806,8 @@ int ensure_streams(Workspace &w, int npipes)
         for (auto &e : w.chk_done)
             if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return -1;
         if (hipEventCreate(&w.ev0) != hipSuccess || hipEventCreate(&w.ev1) != hipSuccess) return -1;
+        if (hipMalloc((void **)&w.verify_res, 64) != hipSuccess || hipMemset(w.verify_res, 0, 64) != hipSuccess)
+            return -1;
         w.streams_ok = true;
     }
     for (int i = 0; i < npipes && i < WF_MAX_PIPES; ++i) {
@@ -1775,10 +1852,9 @@ int ensure(Workspace &w, size_t slots, int grid, int npipes)
     const size_t o_pl = take(slots * 4), o_fl = take(slots * 4), o_T = take(slots * 12), o_L = take(slots * 12),
                  o_c = take(slots * 12), o_n = take(slots * 12), o_rp = take(slots * 12), o_li = take(slots * 4),
                  o_ro = take(slots * 12), o_es = take(slots * 4), o_ee = take(slots * 4), o_px = take(slots * 4);
-    // long-path hand-off (shared by the pipelines), wf_long's stack-free wide traversal needs no spill;
-    // the cross-check records
+    // long-path hand-off (shared by the pipelines), wf_long's stack-free wide traversal needs no spill
     const size_t o_le = take(slots * 8), o_lr = take(slots * 32), o_lc = take(256), o_rr = take(slots * 8),
-                 o_rc = take(256), o_hv = take(slots), o_ctl = take(256), o_chk = take(2 * (size_t)WF_CHECK_CAP * 48);
+                 o_rc = take(256), o_hv = take(slots), o_ctl = take(256);
     // per pipeline (path lists sized for every pixel: a pipeline never holds
     // more; ray queues for two rays per path: a shadow and an extension ray)
     size_t o_qs0[WF_MAX_PIPES], o_qs1[WF_MAX_PIPES], o_qr0[WF_MAX_PIPES], o_qr1[WF_MAX_PIPES], o_h[WF_MAX_PIPES],
@@ -1801,7 +1877,6 @@ int ensure(Workspace &w, size_t slots, int grid, int npipes)
     if (hipMemset(b + o_px, 0, slots * 4) != hipSuccess) return -1; // no pixel out
     if (hipMemset(b + o_ctl, 0, 256) != hipSuccess) return -1;
     w.fin_live = (uint32_t *)(b + o_ctl);
-    w.chk = (RtF4 *)(b + o_chk);
     w.chk_ctr = (uint32_t *)(b + o_ctl + 64);
     w.chain_open = false;
     for (int i = 0; i < WF_MAX_PIPES; ++i) {
@@ -1843,6 +1918,7 @@ int ensure(Workspace &w, size_t slots, int grid, int npipes)
         st.chk_ctr = nullptr;
         st.chk_mask = 0;
         st.chk_fault = 0;
+        st.debug_quit = 0;
     }
     w.slots = slots;
     w.grid = grid;
@@ -1856,8 +1932,22 @@ float elapsed_ms(hipEvent_t a, hipEvent_t b)
     return hipEventElapsedTime(&ms, a, b) == hipSuccess ? ms : 0.0f;
 }
 
+// the hand-off check (wf_verify) on `stream`, which has waited for all the workspace's work
+int launch_verify(Workspace &w, hipStream_t stream)
+{
+    if (!w.verify_pending || !w.blob) return 0;
+    w.verify_pending = false;
+    const int blocks = (int)std::min<size_t>((w.slots + WF_BLOCK - 1) / WF_BLOCK, 1024);
+    hipLaunchKernelGGL(wf_verify, dim3(blocks), dim3(WF_BLOCK), 0, stream, w.pipe[0].st, (uint32_t)w.slots,
+                       w.verify_res, w.last_fr.dev_stats);
+    if (hipGetLastError() != hipSuccess) return -1;
+    w.verify_unread = true;
+    return 0;
+}
+
 // `stream` waits for every call's device work on this workspace (the
-// pipelines' last launches and every wf_long), an open chain drained first
+// pipelines' last launches and every wf_long), an open chain drained first;
+// then the hand-off check runs on it
 int join_all(Workspace &w, hipStream_t stream)
 {
     if (launch_drain(w) != 0) return -1;
@@ -1867,7 +1957,7 @@ int join_all(Workspace &w, hipStream_t stream)
         if (p.long_rec && hipStreamWaitEvent(stream, p.long_done, 0) != hipSuccess) return -1;
     }
     if (w.recorded && hipStreamWaitEvent(stream, w.long_ev, 0) != hipSuccess) return -1;
-    return 0;
+    return launch_verify(w, stream);
 }
 
 int debug_long_log(Workspace &w, unsigned long long *buf);
@@ -1886,18 +1976,19 @@ int debug_long_log(Workspace &w, unsigned long long *buf);
 // library's readers of the frame wait for it.  Results are bit-identical to
 // unchained calls: a pixel's passes run in order whoever runs them.
 int launch_whole(Workspace &w, int dev, const RtDevScene &sc, const RtDevFrame &fr, const RtDevCamera &cam,
-                 hipStream_t stream, int long_depth, bool prof, bool overlap, uint32_t check_mask, int debug)
+                 hipStream_t stream, int long_depth, bool prof, bool overlap, uint32_t check_mask, int debug,
+                 bool count)
 {
     const size_t slots = (size_t)fr.width * fr.height;
     // every wave slot at the finisher's occupancy (MI355X: 256 CUs x 4 SIMDs x 5 waves / 4 waves per
     // block = 1,280 blocks), the last WF_LONG_BLOCKS of them left to wf_long
-    static int cus = 0;
-    if (!cus) {
+    if (!w.cus) {
         hipDeviceProp_t prop;
-        cus = hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0 ? prop.multiProcessorCount
-                                                                                               : 256;
+        w.cus = hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0
+                    ? prop.multiProcessorCount
+                    : 256;
     }
-    const int grid = cus * 4 * WF_FIN_BVH_WAVES / (WF_BLOCK / 64);
+    const int grid = w.cus * 4 * WF_FIN_BVH_WAVES / (WF_BLOCK / 64);
     ChainKey key;
     memset(&key, 0, sizeof key);
     key.nodes = sc.nodes;
@@ -1930,13 +2021,23 @@ int launch_whole(Workspace &w, int dev, const RtDevScene &sc, const RtDevFrame &
     st.linger = overlap ? 0ull : WF_FIN_LINGER;
     st.chk_mask = check_mask;
     const int par = (int)(w.call_seq & 1);
+    // (the guard's records: allocated by the first call that samples rays)
+    if (check_mask != 0xFFFFFFFFu && !w.chk &&
+        hipMalloc((void **)&w.chk, 2 * (size_t)WF_CHECK_CAP * 3 * sizeof(RtF4)) != hipSuccess) {
+        w.chk = nullptr;
+        return -1;
+    }
     st.chk = check_mask == 0xFFFFFFFFu ? nullptr : w.chk + 3 * (size_t)WF_CHECK_CAP * (size_t)par;
     st.chk_ctr = w.chk_ctr + par;
     st.chk_fault = (debug & RT_DEBUG_CHECK_FAULT) ? 1 : 0;
+    st.debug_quit = (debug & RT_DEBUG_LONG_QUIT) ? 1 : 0;
     // debug (RT_DEBUG_LONG_LOG): every deep sample's claim / end time and bounces
-    static unsigned long long *long_log_buf = nullptr;
-    if ((debug & RT_DEBUG_LONG_LOG) && !long_log_buf && hipMalloc((void **)&long_log_buf, 8 * 4 * 65536) != hipSuccess)
+    if ((debug & RT_DEBUG_LONG_LOG) && !w.long_log_buf &&
+        hipMalloc((void **)&w.long_log_buf, 8 * 4 * 65536) != hipSuccess) {
+        w.long_log_buf = nullptr;
         return -1;
+    }
+    unsigned long long *const long_log_buf = w.long_log_buf;
     st.long_log = (debug & RT_DEBUG_LONG_LOG) ? long_log_buf : nullptr;
     // the finisher: every wave slot but wf_long's blocks, at most one lane per pixel
     int fgrid = (int)((slots + WF_BLOCK - 1) / WF_BLOCK);
@@ -1972,12 +2073,15 @@ int launch_whole(Workspace &w, int dev, const RtDevScene &sc, const RtDevFrame &
     }
     if (long_return && hipMemsetD32Async((hipDeviceptr_t)st.chain_flag, overlap ? 1 : 0, 1, s) != hipSuccess) return -1;
     const int tiles = ((fr.width + 15) / 16) * ((fr.height + 15) / 16);
-    hipLaunchKernelGGL(wf_start<false>, dim3(tiles), dim3(WF_BLOCK), 0, s, fr, cam, st, 0, 1);
+    if (count) hipLaunchKernelGGL(wf_start<true>, dim3(tiles), dim3(WF_BLOCK), 0, s, fr, cam, st, 0, 1);
+    else hipLaunchKernelGGL(wf_start<false>, dim3(tiles), dim3(WF_BLOCK), 0, s, fr, cam, st, 0, 1);
     if (!mark(1) || !mark(2)) return -1;
     if (hipEventRecord(w.fin_ready, s) != hipSuccess) return -1;
     // (the finisher is launched before its wf_long: on a shared hardware queue
-    // it then completes first, and wf_long finds its producers done)
-    hipLaunchKernelGGL(wf_finish_bvh<false>, dim3(fgrid), dim3(WF_BLOCK), 0, s, sc, fr, cam, st, 0);
+    // it then completes first, and wf_long finds its producers done.  Counting:
+    // the finisher's own work; wf_long's deep paths are not counted)
+    if (count) hipLaunchKernelGGL(wf_finish_bvh<true>, dim3(fgrid), dim3(WF_BLOCK), 0, s, sc, fr, cam, st, 0);
+    else hipLaunchKernelGGL(wf_finish_bvh<false>, dim3(fgrid), dim3(WF_BLOCK), 0, s, sc, fr, cam, st, 0);
     if (hipGetLastError() != hipSuccess || !mark(3)) return -1;
     Pipe *lp = nullptr;
     if (long_return) {
@@ -2013,6 +2117,7 @@ int launch_whole(Workspace &w, int dev, const RtDevScene &sc, const RtDevFrame &
     if (hipStreamWaitEvent(stream, pp.join, 0) != hipSuccess) return -1;
     if (!overlap && lp && hipStreamWaitEvent(stream, lp->long_done, 0) != hipSuccess) return -1;
     w.chain_open = overlap && long_return;
+    w.verify_pending = w.verify_pending || long_return;
     w.key = key;
     w.last_sc = sc;
     w.last_fr = fr;
@@ -2073,6 +2178,7 @@ int launch_drain(Workspace &w)
     st.chk_mask = 0;
     st.chk_ctr = w.chk_ctr;
     st.chk_fault = 0;
+    st.debug_quit = (w.last_debug & RT_DEBUG_LONG_QUIT) ? 1 : 0;
     st.long_log = nullptr;
     int fgrid = (int)((slots + WF_BLOCK - 1) / WF_BLOCK);
     fgrid = fgrid > w.grid - WF_LONG_BLOCKS ? w.grid - WF_LONG_BLOCKS : fgrid;
@@ -2095,6 +2201,7 @@ int launch_drain(Workspace &w)
     lp.long_rec = true;
     if (hipEventRecord(pp.join, s) != hipSuccess) return -1;
     pp.joined = true;
+    w.verify_pending = true;
     if (w.last_debug & RT_DEBUG_CALL_LOG) {
         (void)hipStreamSynchronize(s);
         timespec ts;
@@ -2169,8 +2276,16 @@ int rt_wavefront_device_init()
     return ensure_streams(workspace(dev), WF_PIPES_DEFAULT);
 }
 
+static thread_local char g_incomplete[256];
+
+// the last RT_WAVEFRONT_INCOMPLETE's description (abi.hip: rt_last_error)
+const char *rt_wavefront_incomplete_msg() { return g_incomplete; }
+
 // rt_join: `stream` (NULL: the host) waits for every rt_render's device work
-// on the current device, chained calls' deep-path tails included
+// on the current device, chained calls' deep-path tails included, and for the
+// hand-off check after them.  A host join returns RT_WAVEFRONT_INCOMPLETE if
+// that check, or one enqueued by an earlier stream join, found pixels that
+// never came back from wf_long.
 int rt_wavefront_join(void *stream)
 {
     int dev = 0;
@@ -2182,17 +2297,32 @@ int rt_wavefront_join(void *stream)
         if (it == g_ws.end() || !it->second) return 0;
         w = it->second;
     }
-    if (!stream) {
-        if (launch_drain(*w) != 0) return -1;
-        for (int pi = 0; pi < WF_MAX_PIPES; ++pi) {
-            Pipe &p = w->pipe[pi];
-            if (p.joined && hipEventSynchronize(p.join) != hipSuccess) return -1;
-            if (p.long_rec && hipEventSynchronize(p.long_done) != hipSuccess) return -1;
-        }
-        if (w->recorded && hipEventSynchronize(w->long_ev) != hipSuccess) return -1;
-        return 0;
+    if (stream) return join_all(*w, (hipStream_t)stream);
+    if (launch_drain(*w) != 0) return -1;
+    for (int pi = 0; pi < WF_MAX_PIPES; ++pi) {
+        Pipe &p = w->pipe[pi];
+        if (p.joined && hipEventSynchronize(p.join) != hipSuccess) return -1;
+        if (p.long_rec && hipEventSynchronize(p.long_done) != hipSuccess) return -1;
     }
-    return join_all(*w, (hipStream_t)stream);
+    if (w->recorded && hipEventSynchronize(w->long_ev) != hipSuccess) return -1;
+    if (w->verify_pending) {
+        const hipStream_t s = w->pipe[0].stream; // (idle: everything above is done)
+        if (launch_verify(*w, s) != 0 || hipStreamSynchronize(s) != hipSuccess) return -1;
+    }
+    if (!w->verify_unread) return 0;
+    w->verify_unread = false;
+    uint32_t r[5] = {};
+    if (hipMemcpy(r, w->verify_res, sizeof r, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemset(w->verify_res, 0, sizeof r) != hipSuccess)
+        return -1;
+    if (r[0] | r[1] | r[2] | r[3] | r[4]) {
+        snprintf(g_incomplete, sizeof g_incomplete,
+                 "%u pixels stranded in the deep-path hand-off (pixels out %u, returns unclaimed %u, hand-offs "
+                 "unclaimed %u, finisher waves registered %u): the frame misses passes; RtDeviations counts it",
+                 r[0], r[1], r[2], r[3], r[4]);
+        return RT_WAVEFRONT_INCOMPLETE;
+    }
+    return 0;
 }
 
 // rt_shutdown: every stream, event and device blob of every device's
@@ -2209,6 +2339,8 @@ void rt_wavefront_shutdown()
         if (w->blob) (void)launch_drain(*w); // (an open chain's wf_longs leave only after its drain)
         (void)hipDeviceSynchronize();
         if (w->blob) (void)hipFree(w->blob);
+        for (void *p : {(void *)w->chk, (void *)w->verify_res, (void *)w->long_log_buf})
+            if (p) (void)hipFree(p);
         for (int i = WF_MAX_PIPES - 1; i >= 0; --i) {
             Pipe &p = w->pipe[i];
             for (auto &e : p.ev)
@@ -2264,17 +2396,21 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
     // call with deep paths cut (profiles/r03).  It runs as ONE pipeline whose
     // finisher spans the chip: three pipelines' fixed pixel sets finished up
     // to 0.7 s apart, each leaving its third of the chip idle.
-    const bool whole = bounded && !count && trace_kind == 1 && (tail_opt <= 0 || (size_t)tail_opt > slots);
+    // (RT_TRAVERSAL_BOUNDED_COUNTED: the same whole call, its finisher counting its own work — the
+    // bench's per-launch algorithmic bytes then describe the timed launch's own shape)
+    const bool whole = bounded && (!count || traversal == RT_TRAVERSAL_BOUNDED_COUNTED) && trace_kind == 1 &&
+                       (tail_opt <= 0 || (size_t)tail_opt > slots);
     if (whole) {
         // the run-time exactness guard: 1 ray in check_interval (a power of two) re-traced by the KD traversal
         uint32_t mask = 0xFFFFFFFFu;
-        if (check_interval >= 0) {
+        if (check_interval >= 0 && !count) {
             uint32_t iv = check_interval > 0 ? (uint32_t)check_interval : WF_CHECK_INTERVAL_DEFAULT;
             uint32_t p2 = 1;
             while (p2 < iv && p2 < (1u << 30)) p2 <<= 1;
             mask = p2 - 1;
         }
-        return launch_whole(w, dev, sc, fr, cam, stream, long_depth, profile != 0, overlap != 0, mask, debug);
+        return launch_whole(w, dev, sc, fr, cam, stream, long_depth, profile != 0, overlap != 0 && !count, mask,
+                            debug, count);
     }
     // persistent-ish grid for trace/shade (grid-stride over the queue).  512
     // blocks = 2,048 waves = a third of the chip's 6,144 wave slots at the

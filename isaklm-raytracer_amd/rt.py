@@ -82,19 +82,31 @@ class RtDeviations(ctypes.Structure):
                 ("max_deep_depth", ctypes.c_ulonglong), ("deep_paths", ctypes.c_ulonglong),
                 ("deep_hist", ctypes.c_ulonglong * DEV_HIST_BINS),
                 ("bounded_checked", ctypes.c_ulonglong), ("bounded_mismatches", ctypes.c_ulonglong),
-                ("mismatch_ray", ctypes.c_float * 6)]
+                ("mismatch_ray", ctypes.c_float * 6),
+                ("owed_pixels", ctypes.c_ulonglong), ("owed_passes", ctypes.c_ulonglong),
+                ("long_safety_quits", ctypes.c_ulonglong), ("stranded_pixels", ctypes.c_ulonglong),
+                ("check_dropped", ctypes.c_ulonglong), ("linger_expiries", ctypes.c_ulonglong)]
+
+
+HANDOFF_FIELDS = ("owed_pixels", "owed_passes", "long_safety_quits", "stranded_pixels", "check_dropped",
+                  "linger_expiries")
 
 
 def deviation_stats(reset=False):
     """Always-on deviation statistics of every rt_render on this device since
-    the last reset (rt_deviation_stats): watchdog / depth-limit cuts and the
-    histogram of paths that ended at depth >= 64 (bin k: [64*2^k, 64*2^(k+1)))."""
+    the last reset (rt_deviation_stats): watchdog / depth-limit cuts, the
+    histogram of paths that ended at depth >= 64 (bin k: [64*2^k, 64*2^(k+1))),
+    the guard's checks, and the deep-path hand-off's events (owed passes of
+    chained calls; safety-net exits, stranded pixels, dropped guard records
+    and linger expiries, which a working render keeps at 0)."""
     d = RtDeviations()
     check(lib().rt_deviation_stats(ctypes.byref(d), int(reset)))
-    return {"watchdog_paths": d.watchdog_paths, "cut_paths": d.cut_paths, "max_deep_depth": d.max_deep_depth,
-            "deep_paths": d.deep_paths, "deep_hist": [int(v) for v in d.deep_hist],
-            "bounded_checked": int(d.bounded_checked), "bounded_mismatches": int(d.bounded_mismatches),
-            "mismatch_ray": [float(v) for v in d.mismatch_ray]}
+    out = {"watchdog_paths": d.watchdog_paths, "cut_paths": d.cut_paths, "max_deep_depth": d.max_deep_depth,
+           "deep_paths": d.deep_paths, "deep_hist": [int(v) for v in d.deep_hist],
+           "bounded_checked": int(d.bounded_checked), "bounded_mismatches": int(d.bounded_mismatches),
+           "mismatch_ray": [float(v) for v in d.mismatch_ray]}
+    out.update({k: int(getattr(d, k)) for k in HANDOFF_FIELDS})
+    return out
 
 
 def join(stream=None):
@@ -103,7 +115,9 @@ def join(stream=None):
     check(lib().rt_join(stream))
 
 
-ABI_VERSION = 6  # RT_ABI_VERSION of include/isaklm_rt.h
+ABI_VERSION = 7  # RT_ABI_VERSION of include/isaklm_rt.h
+E_INCOMPLETE = -7  # RT_E_INCOMPLETE: a join found stranded pixels
+DEBUG_CALL_LOG, DEBUG_LONG_LOG, DEBUG_CHECK_FAULT, DEBUG_LONG_QUIT = 1, 2, 4, 8  # RtOptions.debug bits
 TRIANGLE_BYTES = 152
 NODE_BYTES = 20
 COUNTER_NAMES = ["node", "tri", "hit", "texel", "nee", "sample", "skip", "ray", "watchdog", "maxdepth"]
@@ -372,7 +386,8 @@ def options(width, height, passes=1, adaptive=True, min_samples=100, tolerance=0
     """RtOptions; traversal: TRAVERSAL_BOUNDED / TRAVERSAL_KD (None: the
     library default, or RT_TRAVERSAL from the environment); overlap: chained
     calls (RtOptions.overlap: join before reading the frame); check_interval:
-    the bounded traversal's run-time guard (0: 1 ray in 1024, < 0: off)."""
+    the bounded traversal's run-time guard (0: the library default, 1 ray in
+    4096; < 0: off)."""
     o = RtOptions()
     lib().rt_default_options(ctypes.byref(o))
     o.width, o.height, o.passes = width, height, passes

@@ -82,9 +82,10 @@ def test_version_string():
 
 
 def test_ctypes_binding_matches_header_layout(tmp_path):
-    """rt.py's RtOptions / RtProfile must mirror include/isaklm_rt.h field by
-    field: compile a probe with gcc and compare every offset and the size."""
-    structs = {"RtOptions": rt.RtOptions, "RtProfile": rt.RtProfile}
+    """rt.py's RtOptions / RtProfile / RtDeviations must mirror
+    include/isaklm_rt.h field by field: compile a probe with gcc and compare
+    every offset and the size."""
+    structs = {"RtOptions": rt.RtOptions, "RtProfile": rt.RtProfile, "RtDeviations": rt.RtDeviations}
     lines = ['#include <stddef.h>', '#include <stdio.h>', '#include "isaklm_rt.h"', "int main(void){"]
     for cname, cls in structs.items():
         lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')

@@ -69,6 +69,68 @@ def test_chained_deep_paths_vs_oracle(tmp_path):
     ref, _ = helpers.oracle_render(trap, W, H, split)
     helpers.assert_bitwise(gpu, ref, what="light guide, chained 1-pass calls")
     assert dev["deep_paths"] > 0, dev  # the hand-off really ran
+    # ... and the owed-passes protocol fired: pixels out in wf_long were skipped by later calls
+    assert dev["owed_pixels"] > 0 and dev["owed_passes"] >= dev["owed_pixels"], dev
+    assert dev["stranded_pixels"] == 0 and dev["long_safety_quits"] == 0, dev
+
+
+def test_checkpoint_mid_chain(tmp_path):
+    """rt_gbuffer_save between chained calls must join the open
+    chain first (its owed passes run in the drain), so the checkpoint holds
+    exactly the passes of the calls so far; resuming from it in a fresh
+    G_Buffer and finishing the passes is bit-identical to the oracle's
+    uninterrupted render.  The light guide keeps pixels out in wf_long across
+    call boundaries, so the chain really is open with passes owed."""
+    trap = helpers.make_trap_scene(str(tmp_path / "t"))
+    run = helpers.GpuRun(trap)
+    W, H = 96, 64
+    rt.deviation_stats(reset=True)
+    g = rt.GBuffer(W, H)
+    ck = tmp_path / "mid.gbuf"
+    for c in range(4):
+        rt.render(run.dev, g, run.camera, 0 if c == 0 else 1,
+                  rt.options(W, H, 1, adaptive=False, kernel=WF, overlap=True, wf_long_depth=8))
+    g.save(ck, 4)  # mid-chain: joins (drains) first
+    dev = rt.deviation_stats(reset=False)
+    assert dev["owed_pixels"] > 0, dev  # the chain was open with owed passes at the save
+    mid_ref, _ = helpers.oracle_render(trap, W, H, [1, 1, 1, 1])
+    g2 = rt.GBuffer(W, H, 12345)  # other seeds: everything must come from the file
+    assert g2.load(ck) == 4
+    helpers.assert_bitwise(g2.download(), mid_ref, what="checkpoint taken mid-chain")
+    for c in range(3):  # resume: chained calls again, on the loaded G_Buffer
+        rt.render(run.dev, g2, run.camera, 1, rt.options(W, H, 1, adaptive=False, kernel=WF, overlap=True,
+                                                         wf_long_depth=8))
+    ref, _ = helpers.oracle_render(trap, W, H, [1] * 7)
+    helpers.assert_bitwise(g2.download(), ref, what="resumed from a mid-chain checkpoint")
+
+
+@pytest.mark.parametrize("overlap", [False, True])
+def test_long_kernel_quit_is_reported(tmp_path, overlap):
+    """a failure of the hand-off must not pass silently.
+    RT_DEBUG_LONG_QUIT makes wf_long leave at once, as if its safety net had
+    fired: every pixel handed to it is stranded.  The join must say so
+    (RT_E_INCOMPLETE), RtDeviations must count the exits and the stranded
+    pixels, and the workspace must recover: the next render is exact."""
+    trap = helpers.make_trap_scene(str(tmp_path / "t"))
+    run = helpers.GpuRun(trap)
+    W, H = 96, 64
+    rt.deviation_stats(reset=True)
+    g = rt.GBuffer(W, H)
+    for c in range(2):
+        rt.render(run.dev, g, run.camera, 0 if c == 0 else 1,
+                  rt.options(W, H, 2, adaptive=False, kernel=WF, overlap=overlap, wf_long_depth=8,
+                             debug=rt.DEBUG_LONG_QUIT))
+    with pytest.raises(rt.RtError) as ei:
+        rt.join()
+    assert f"rt error {rt.E_INCOMPLETE}" in str(ei.value) and "stranded" in str(ei.value), str(ei.value)
+    dev = rt.deviation_stats(reset=True)
+    assert dev["long_safety_quits"] > 0 and dev["stranded_pixels"] > 0, dev
+    rt.join()  # reported once: the stranded pixels were released
+    gpu = _render_calls(run, W, H, [2, 2], overlap=overlap, wf_long_depth=8)
+    ref, _ = helpers.oracle_render(trap, W, H, [2, 2])
+    helpers.assert_bitwise(gpu, ref, what="render after a stranded frame")
+    dev = rt.deviation_stats(reset=True)
+    assert dev["stranded_pixels"] == 0 and dev["long_safety_quits"] == 0, dev
 
 
 def test_chained_adaptive_and_reads_between(tmp_path):

@@ -3,7 +3,9 @@ same seeds, for both kernel variants (megakernel, wavefront).  The bar is
 bit-exact accumulators (fb, sq, count, RNG state) and equal work counters;
 north_star's 1e-4 relative L-infinity is asserted too.
 """
+import ctypes
 import os
+import sys
 
 import numpy as np
 import pytest
@@ -270,13 +272,15 @@ def test_room2m_every_pixel_bench_options():
 
 @pytest.mark.timeout(240)
 def test_room2m_bench_configuration_sparse_pixels():
-    """bench.py's configuration exactly: room2m at 1920x1080, its warm-up
-    call of 64 passes (sample_count 0) then a timed call of 4 steps = 256
-    passes (sample_count 1), wavefront kernel with its defaults (3 pipelines,
-    long-path hand-off at depth 64, wide tails, cooperative finisher), no
-    counters (the bench's kernels).  Every 1031st pixel re-rendered by the
-    oracle over the same 320 spp.  A counted call of the same options must not
-    fire the 65,536-bounce watchdog."""
+    """The driver-default bench (`python bench.py`: 1 warm-up + 4 timed steps)
+    rendered UNCHAINED: room2m at 1920x1080, a call of 64 passes (sample_count
+    0) then one of 4 steps = 256 passes (sample_count 1), the default render
+    (bounded traversal, the whole call in one finisher, deep paths handed to
+    wf_long at depth 64, the run-time guard), no counters.  Every 1031st pixel
+    re-rendered by the oracle over the same 320 spp.  A counted call of the
+    same options must not fire the 2^24 - 1-bounce watchdog.  The
+    chained shape of `--steps 20 --warmup 5` is pinned by
+    test_room2m_bench_chained_shape_sparse_pixels."""
     run = helpers.GpuRun("room2m")
     W, H, P = 1920, 1080, 64
     calls = [P, 4 * P]
@@ -293,6 +297,68 @@ def test_room2m_bench_configuration_sparse_pixels():
     assert c["watchdog"] == 0, c
     assert c["sample"] == W * H * P
     assert c["maxdepth"] > 64  # glass paths run past the long-path hand-off depth
+
+
+@pytest.mark.timeout(420)
+def test_room2m_bench_chained_shape_sparse_pixels():
+    """the driver's bench command (`bench.py --steps 20
+    --warmup 5`) exactly, through bench.py's own call plan: warm-up calls of
+    256 + 64 passes (chained), the bench's rt_synchronize (a join), five
+    chained timed calls of 256 passes, and rt_tonemap without a stream as the
+    join that ends the timed region.  Every 4099th pixel re-rendered by the
+    oracle over the same 1,600 spp, bit for bit.  The owed-passes protocol must
+    really have fired (pixels skipped while out in wf_long, their passes run
+    later) and the hand-off must report no failure."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+
+    run = helpers.GpuRun("room2m")
+    W, H, P, spc, warmup, steps = 1920, 1080, 64, 4, 5, 20
+    chain = len(bench.call_plan(warmup, steps, spc)) > 1
+    assert chain
+    g = rt.GBuffer(W, H)
+    passes = []
+    rt.deviation_stats(reset=True)
+
+    def calls(first, count):
+        for start, k in bench.call_plan(first, count, spc):
+            rt.render(run.dev, g, run.camera, 0 if start == 0 else 1,
+                      rt.options(W, H, P * k, adaptive=False, kernel=rt.KERNEL_WAVEFRONT, overlap=chain))
+            passes.append(P * k)
+
+    calls(0, warmup)
+    rt.check(rt.lib().rt_synchronize())
+    calls(warmup, steps)
+    rgba = ctypes.c_void_p()
+    rt.check(rt.lib().rt_device_alloc(ctypes.byref(rgba), W * H * 4))
+    rt.check(rt.lib().rt_tonemap(g.g, rgba, W, H, None))
+    rt.check(rt.lib().rt_free(rgba))
+    dev = rt.deviation_stats(reset=True)
+    gpu = g.download()
+    assert passes == [256, 64, 256, 256, 256, 256, 256]
+    pixels = np.arange(0, W * H, 4099, dtype=np.int32)
+    ref, rcnt = helpers.oracle_render(run.path, W, H, passes, pixels=pixels)
+    helpers.assert_bitwise(gpu, ref, pixels=pixels, what="room2m, the bench's chained timed shape")
+    assert np.all(gpu[2] == sum(passes))
+    assert rcnt["watchdog"] == 0
+    assert dev["deep_paths"] > 0 and dev["owed_pixels"] > 0 and dev["owed_passes"] >= dev["owed_pixels"], dev
+    assert dev["stranded_pixels"] == 0 and dev["long_safety_quits"] == 0 and dev["check_dropped"] == 0, dev
+    assert dev["bounded_checked"] > 0 and dev["bounded_mismatches"] == 0, dev
+
+
+@pytest.mark.timeout(240)
+def test_room2m_single_pass_chained_calls():
+    """The reference's call granularity (one render() per pass,
+    rt/main.cu:114-122) through chained calls: room2m at 480x270, 16 chained
+    calls of 1 pass, then the join; every pixel against the oracle."""
+    run = helpers.GpuRun("room2m")
+    W, H = 480, 270
+    rt.deviation_stats(reset=True)
+    gpu, _, _ = run.render(W, H, [1] * 16, kernel=rt.KERNEL_WAVEFRONT, overlap=True)
+    dev = rt.deviation_stats(reset=True)
+    ref, _ = helpers.oracle_render(run.path, W, H, [1] * 16)
+    helpers.assert_bitwise(gpu, ref, what="room2m, 16 chained 1-pass calls")
+    assert dev["stranded_pixels"] == 0 and dev["long_safety_quits"] == 0, dev
 
 
 @pytest.mark.timeout(240)
