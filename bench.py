@@ -518,15 +518,13 @@ def main(argv=None, binding=None):
     chain = bool(args.overlap) and len(call_plan(args.warmup, args.steps, spc)) > 1
 
     def steps(first, count):
-        """render steps [first, first + count) in calls of up to spc steps"""
+        """render steps [first, first + count) in calls of up to spc steps (profiled: their kernel
+        times are read back after the timed region, rt_profile_history, so that no call waits)"""
         for start, k in call_plan(first, count, spc):
             rt.render(dscene, gb, host.camera, 0 if start == 0 else 1,
                       rt.options(W, H, P * k, profile=wavefront, overlap=chain, **render_kw))
-            if wavefront:
-                profiles.append(dict(rt.last_profile(), passes=P * k))
 
     steps(0, args.warmup)
-    profiles.clear()
     rt.check(rt.lib().rt_synchronize())
     cnt_before = int(gb.download()[2].sum(dtype=np.int64))  # accumulated samples (adaptive: actual)
     if dist:
@@ -539,6 +537,8 @@ def main(argv=None, binding=None):
     rt.check(rt.lib().rt_device_alloc(ctypes.byref(rgba), n * 4))
     rt.check(rt.lib().rt_synchronize())
     rt.deviation_stats(reset=True)  # always-on deviation statistics: the timed region only
+    if wavefront:
+        rt.profile_history(reset=True)  # (the warm-up calls' profiles dropped)
     if dist:
         dist.barrier()
     t0 = time.perf_counter()
@@ -557,6 +557,10 @@ def main(argv=None, binding=None):
         e = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
+    if wavefront:
+        plan = call_plan(args.warmup, args.steps, spc)
+        hist = rt.profile_history(reset=True)
+        profiles = [dict(h, passes=P * k) for h, (_, k) in zip(hist, plan)]
     dev = rt.deviation_stats(reset=False)
     if dist:  # every rank's statistics (sums; max of the longest path)
         import torch

@@ -57,7 +57,7 @@ extern "C" {
  * check_interval / debug, RtDeviations' bounded-traversal guard fields,
  * rt_join, rt_shutdown; 7 = RtDeviations' hand-off fields (owed passes,
  * safety-net exits, stranded pixels, dropped guard records, linger
- * expiries), RT_E_INCOMPLETE from the joins.  An integrator checks
+ * expiries), RT_E_INCOMPLETE from the joins, rt_profile_history.  An integrator checks
  * rt_abi_version() == RT_ABI_VERSION at start-up: a binary built against an
  * older header would otherwise link (C linkage) and mis-pass arguments. */
 #define RT_ABI_VERSION 7
@@ -461,14 +461,16 @@ typedef struct RtOptions {
      * kernel are not counted; the megakernel then runs its counting KD build). */
     int traversal;
     /* chained calls (default render only: bounded traversal, not counting).
-     * 0: the call is complete at its stream point.  1: the call's deep paths
-     * (glass loops of 10^4+ bounces, handed to the long-path kernel) may still
-     * run after its stream point, and the NEXT call of the same frame — same
-     * scene, G_Buffer, camera and frame options, sample_count != 0, overlap 1
-     * — starts at once: its pixels that are not still out run their passes,
-     * the ones still out are owed the passes and run them when they come
-     * back.  Every pixel's passes run in the reference's order, so the frame
-     * is bit-identical to unchained calls.  Whatever reads the frame in
+     * 0: the call is complete at its stream point.  1: the call is only
+     * enqueued — the caller's stream does not wait for it — and the NEXT call
+     * of the same frame — same scene, G_Buffer, camera and frame options,
+     * sample_count != 0, overlap 1 — starts at once: its kernel fills the
+     * slots the previous call's tail frees, its pixels that are free run its
+     * passes, and the ones still held (by the previous call's tail or the
+     * long-path kernel running a deep glass path of 10^4+ bounces) are owed
+     * the passes and run them before they are let go.  Every pixel's passes
+     * run in the reference's order, so the frame is bit-identical to
+     * unchained calls.  Whatever reads the frame in
      * between must join first: rt_join(stream), rt_synchronize, or the
      * library's own readers (rt_tonemap, rt_save_render, rt_gbuffer_save,
      * rt_reduce_shards, rt_deviation_stats), which join by themselves.  A
@@ -497,8 +499,9 @@ typedef struct RtOptions {
                                 * safety net fired, stranding every pixel handed to it */
 
 /* Per-call kernel timing of the last rt_render on this device with
- * RtOptions.profile = 1 (wavefront kernels; HIP events on the call's stream,
- * the call waits for its last event). */
+ * RtOptions.profile = 1 (wavefront kernels: HIP events on the pipelines'
+ * streams for the queue variants, the finisher's device span for the default
+ * render; reading it waits for that call's kernels). */
 typedef struct RtProfile {
     int iterations;      /* trace/shade queue iterations */
     int trace_launches, shade_launches, finish_launches;
@@ -512,6 +515,13 @@ typedef struct RtProfile {
     int pipelines;
 } RtProfile;
 int rt_last_profile(RtProfile *out);
+/* every profiled rt_render's RtProfile on this device since the last reset,
+ * oldest first: up to `cap` into out, the number recorded into *count.  For
+ * the default render (one finisher launch per call) finish_ms and call_ms are
+ * the finisher's span on the device, from its first wave's start to its last
+ * wave's end (chained calls' finishers overlap: their spans do too).  Waits
+ * for those calls' finishers. */
+int rt_profile_history(RtProfile *out, int cap, int *count, int reset);
 
 /* Always-on deviation statistics of every rt_render on the current device
  * since the last reset (recorded by every kernel, counting or not, at one

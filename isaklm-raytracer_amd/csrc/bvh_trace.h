@@ -36,6 +36,11 @@ __device__ unsigned long long g_phase_acc[8]; // wf_finish_bvh's per-phase sums 
 #else
 #define RT_PHASE_MID()
 #endif
+#if defined(RT_LOCKSTEP_PROF) && !defined(RT_PHASE_PROF)
+// lockstep profile (a -DRT_LOCKSTEP_PROF build, tools/lockstep_profile.py): the counting
+// finisher's per-query lane steps against the wave's (wavefront.hip wf_finish_bvh)
+__device__ unsigned long long g_phase_acc[8];
+#endif
 
 // Scene data is read-only for a kernel's lifetime: loaded through the
 // constant address space (a wave-uniform address becomes a scalar load

@@ -97,11 +97,11 @@ static_assert(WF_BLOCK % WF_TBLOCK == 0 && WF_TBLOCK % 64 == 0, "WF_TBLOCK must 
 #ifndef WF_CHECK_BLOCKS
 #define WF_CHECK_BLOCKS 256 // wf_check's grid (it runs beside the next call's finisher)
 #endif
-#ifndef WF_LONG_PINGPONG
-#define WF_LONG_PINGPONG 0 // whole-call mode: wf_long always on pipeline 1 (1: pipelines 1 and 2 alternately; +1.6 % with one grid, profiles/r04/ab)
-#endif
 #ifndef WF_FIN_BVH_WAVES
 #define WF_FIN_BVH_WAVES 5 // wf_finish_bvh occupancy target (5: +3 % over 6 with the 4-wide s_min query, profiles/r04)
+#endif
+#ifndef WF_FIN_SMALL_WAVES
+#define WF_FIN_SMALL_WAVES 3 // frames of at most this many finisher waves per SIMD take the unspilled build (151 VGPRs: 3 waves)
 #endif
 // per-thread spill entries: the deeper of the KD stack (past WF_LDS_STACK) and the BVH stack (past WF_BVH_LDS)
 #define WF_SPILL_ENTRIES \
@@ -145,13 +145,19 @@ static_assert(WF_BLOCK % WF_TBLOCK == 0 && WF_TBLOCK % 64 == 0, "WF_TBLOCK must 
 // room2m call, 4096 ~1 %, and still checks ~2M rays in the 20-step bench)
 #define WF_CHECK_INTERVAL_DEFAULT 4096u
 #define WF_CHECK_CAP (1u << 20)         // cross-check records per call (more are dropped: RT_DEV_CHK_DROP)
-// per-pixel hand-off word (WfState.pxo): a pixel handed to wf_long is OUT
-// until a finisher takes it back or wf_long finishes it (LONGDONE: its state
-// was written by the concurrently running wf_long, so the next reader
-// acquires first); the low bits count passes that later chained calls owe it
+// per-pixel ownership word (WfState.pxo) of the whole-call render: a pixel is
+// BUSY while a finisher lane runs its passes and OUT while wf_long holds it
+// (handed over, or in the return ring), until a finisher lane takes it back or
+// wf_long finishes it.  A call that finds its pixel held adds its passes to
+// the low bits (owed) and moves on; the holder runs them, in the pixel's order,
+// before it lets go.  Free: 0, or REL when the last holder may run concurrently
+// with the next one (a chained finisher, wf_long): its stores were released
+// before the word said so, and the next claimer acquires first.
 #define RT_PX_OUT 0x80000000u
-#define RT_PX_LONGDONE 0x40000000u
-#define RT_PX_PASSES 0x3FFFFFFFu
+#define RT_PX_REL 0x40000000u
+#define RT_PX_LONGDONE RT_PX_REL
+#define RT_PX_BUSY 0x20000000u
+#define RT_PX_PASSES 0x1FFFFFFFu
 
 struct WfState {
     int *passes_left;
@@ -191,8 +197,14 @@ struct WfState {
     // successor takes the returns), so that it never depends on wf_long
     uint32_t *ret_ctr;
     unsigned long long linger;
-    // per pixel: RT_PX_OUT | passes owed by later chained calls, RT_PX_LONGDONE, or 0
+    // per pixel: RT_PX_OUT / RT_PX_BUSY | passes owed by later chained calls, RT_PX_REL, or 0
     uint32_t *pxo;
+    // the whole-call finisher takes this call's pixels itself (no wf_start, no path list):
+    // fresh = 1; concurrent = 1 when the next chained call's finisher may run beside this
+    // one (a pixel is released with a release fence and marked RT_PX_REL)
+    int fresh, concurrent;
+    uint32_t fresh_n; // (fresh) entries: 256 per 16x16-pixel tile (fresh_pixel); 0 for a chain's drain
+    unsigned long long *span; // RtOptions.profile: {first wave start, last wave end} (s_memrealtime)
     // the persistent wf_long's producers: finisher waves of its call not yet
     // past their last hand-off (nullptr: wf_long runs in host-kicked slices)
     uint32_t *fin_live;
@@ -203,11 +215,6 @@ struct WfState {
     // the stream-queued successor blocked behind them).  Bounded: the drain's
     // clear may sit behind this very wf_long when streams share a hardware queue.
     uint32_t *chain_flag;
-    // pixels whose path went to wf_long in the previous call run first (their
-    // passes are the call's longest chains): wf_start puts them on path list 1,
-    // the whole-call finisher takes list 1 before list 0
-    uint8_t *heavy;
-    int heavy_first;
     // run-time exactness guard of the bounded traversal: the finisher records
     // every ray whose hash of (pixel, pass, depth, kind) hits chk_mask (3 RtF4:
     // {o, hit bits}, {d, bx}, {by, bz, -, -}); wf_check re-traces them with the
@@ -281,10 +288,7 @@ __device__ __forceinline__ void long_publish(const WfState &st, bool to_long, ui
 __device__ __forceinline__ void publish_long(const WfState &st, bool to_long, uint32_t slot, Vec3D o, Vec3D d)
 {
     uint32_t e = 0;
-    if (to_long) {
-        st.heavy[slot] = st.heavy[slot] | 1u;
-        e = __hip_atomic_fetch_add(st.long_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (to_long) e = __hip_atomic_fetch_add(st.long_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     long_publish(st, to_long, e, slot, o, d);
 }
 
@@ -319,10 +323,9 @@ __device__ __forceinline__ bool publish_long_capped(const WfState &st, bool to_l
     base = (uint32_t)__shfl((int)base, leader);
     if (base == 0xffffffffu) return false;
     const uint32_t e = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-    if (to_long) {
-        st.heavy[slot] = st.heavy[slot] | 1u;
-        if (st.long_return) __hip_atomic_store(st.pxo + slot, RT_PX_OUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    // (BUSY -> OUT, owed passes kept: one atomic)
+    if (to_long && st.long_return)
+        __hip_atomic_fetch_xor(st.pxo + slot, RT_PX_OUT ^ RT_PX_BUSY, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     long_publish(st, to_long, e, slot, o, d);
     return true;
 }
@@ -363,29 +366,10 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_start(RtDevFrame fr, RtDevCamera 
     const int x = (tile % tiles_x) * 16 + (wave & 1) * 8 + (lane & 7);
     const int y = (tile / tiles_x) * 16 + (wave >> 1) * 8 + (lane >> 3);
     const bool valid = x < fr.width && y < fr.height && rt_row_owned(fr, y);
-    if (st.long_log && blockIdx.x == 0 && tid == 0) st.long_log[0] = __builtin_amdgcn_s_memrealtime();
     const int slot = valid ? y * fr.width + x : 0;
     bool want = false;
     Vec3D ro = rt_v3(0, 0, 0), rd = rt_v3(0, 0, 0);
-    // whole-call mode: a pixel still OUT in wf_long (a chained call's deep
-    // sample, still running) is left to whoever holds it: its passes are
-    // owed (pxo), and the holder runs them.  One that wf_long finished
-    // concurrently (LONGDONE) is read after an acquire.
-    bool owned = valid && slot < n;
-    if (st.long_return && owned) {
-        uint32_t x = __hip_atomic_load(st.pxo + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        while (x & RT_PX_OUT) {
-            if (__hip_atomic_compare_exchange_strong(st.pxo + slot, &x, x + (uint32_t)fr.passes, __ATOMIC_RELAXED,
-                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                owned = false;
-                break;
-            }
-        }
-        const bool acq = owned && x == RT_PX_LONGDONE;
-        if (__any(acq)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        if (acq) __hip_atomic_store(st.pxo + slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (owned) {
+    if (valid && slot < n) {
         Vec3D fb = rt_v3(0.0f, 0.0f, 0.0f);
         float sq = 0.0f;
         int count = 0;
@@ -409,20 +393,9 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_start(RtDevFrame fr, RtDevCamera 
         st.ro[slot] = ro;
         st.cont[slot] = rd;
     }
-    if (st.heavy_first) { // the whole-call finisher: no ray queue; heavy pixels on list 1
-        bool h = false;
-        if (owned) {
-            const uint8_t v = st.heavy[slot];
-            h = v != 0;
-            if (v & 1u) st.heavy[slot] = v & 2u; // bit 0: set again by this call's hand-offs (bit 1 stays)
-        }
-        enqueue_path(st, 1, want && h, (uint32_t)slot);
-        enqueue_path(st, 0, want && !h, (uint32_t)slot);
-    } else {
-        const uint32_t e = enqueue_ray(st, 0, want, ro, rd);
-        if (want) st.e_ext[slot] = e;
-        enqueue_path(st, 0, want, (uint32_t)slot);
-    }
+    const uint32_t e = enqueue_ray(st, 0, want, ro, rd);
+    if (want) st.e_ext[slot] = e;
+    enqueue_path(st, 0, want, (uint32_t)slot);
     if (COUNT) flush_counters(c, fr.counters);
 }
 
@@ -1026,6 +999,37 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_finish(RtDevScene sc, RtDevFrame 
     }
 }
 
+namespace {
+
+// fresh entry e of the whole-call finisher's pixel list -> its pixel: 256
+// entries per 16x16-pixel tile, 64 per 8x8-pixel wave tile (wf_start's
+// layout); false for a pixel outside the frame or in a row another shard owns
+__device__ __forceinline__ bool fresh_pixel(const RtDevFrame &fr, uint32_t e, int &slot)
+{
+    const uint32_t tiles_x = (uint32_t)(fr.width + 15) / 16u;
+    const uint32_t t = e >> 8, w = (e >> 6) & 3u, l = e & 63u;
+    const int x = (int)((t % tiles_x) * 16u + (w & 1u) * 8u + (l & 7u));
+    const int y = (int)((t / tiles_x) * 16u + (w >> 1) * 8u + (l >> 3));
+    if (x >= fr.width || y >= fr.height || !rt_row_owned(fr, y)) return false;
+    slot = y * fr.width + x;
+    return true;
+}
+
+// a sample's path state at its camera ray (trace_path's start, rt/path_tracing.cuh:270-277)
+__device__ __forceinline__ void begin_path(PathRegs &p)
+{
+    p.T = rt_v3(1.0f, 1.0f, 1.0f);
+    p.L = rt_v3(0.0f, 0.0f, 0.0f);
+    p.inside = false;
+    p.prev_type = PRIMARY;
+    p.depth = 1;
+    p.shadow = false;
+    p.dual = false;
+    p.ext_live = false;
+}
+
+} // namespace
+
 // Finisher with the BVH-bounded traversal (bvh_trace.h): every lane runs one
 // path to the end of its pixel's passes (trace + shade in registers,
 // megakernel style) and then takes the next queued path (wave-aggregated
@@ -1033,9 +1037,13 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_finish(RtDevScene sc, RtDevFrame 
 // With the bounded traversal this runs the WHOLE call (wf_start's path list:
 // no queue iterations), see rt_launch_wavefront.  COUNT: the traversal's own
 // work (trace_bvh) and the reference's shading counters.
-template <bool COUNT>
-__global__ void __launch_bounds__(WF_BLOCK, WF_FIN_BVH_WAVES) wf_finish_bvh(RtDevScene sc, RtDevFrame fr, RtDevCamera cam,
-                                                                       WfState st, int q)
+// WAVES: the occupancy it is built for — WF_FIN_BVH_WAVES (96 VGPRs, the rest
+// spilled) when the chip is full of its waves; 1 (no register cap, no spills)
+// for a frame whose pixels fill at most WF_FIN_SMALL_WAVES waves per SIMD, where
+// the occupancy is the pixel count's anyway and every spill's latency shows
+template <bool COUNT, int WAVES = WF_FIN_BVH_WAVES>
+__global__ void __launch_bounds__(WF_BLOCK, WAVES) wf_finish_bvh(RtDevScene sc, RtDevFrame fr, RtDevCamera cam,
+                                                                 WfState st, int q)
 {
     __shared__ uint32_t s_node[WF_BVH_LDS * WF_BLOCK];
     __shared__ float s_entry[WF_BVH_LDS * WF_BLOCK];
@@ -1044,9 +1052,8 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_FIN_BVH_WAVES) wf_finish_bvh(RtDe
     Stack<WF_BVH_LDS> stk{s_node + tid, s_entry + tid, WF_BLOCK, st.spill + gtid, st.spill_threads};
     Cnt c;
     if (COUNT) c.zero();
-    // paths of path list q (heavy_first: list 1's, the heavy pixels, first)
-    const uint32_t n1 = st.heavy_first ? st.counts[6 + 1] : 0u;
-    const uint32_t n = st.counts[6 + q] + n1;
+    // fresh: this call's pixels, 256 entries per 16x16-pixel tile (fresh_pixel); else the paths of path list q
+    const uint32_t n = st.fresh ? st.fresh_n : st.counts[6 + q];
     uint32_t *fetch = st.counts + 4;
     const int limit = fr.max_depth > 0 ? fr.max_depth : RT_WATCHDOG_BOUNCES;
     const int lane = __lane_id();
@@ -1054,6 +1061,10 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_FIN_BVH_WAVES) wf_finish_bvh(RtDe
     uint32_t *const ret_claimed = st.ret_ctr + 2;
     if (st.long_return && lane == 0) // this wave is alive: wf_long may return pixels to it
         __hip_atomic_fetch_add(ret_word, 1ull << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0) {
+        if (st.span) atomicMin(st.span, __builtin_amdgcn_s_memrealtime());
+        if (st.long_log && blockIdx.x == 0 && threadIdx.x == 0) st.long_log[0] = __builtin_amdgcn_s_memrealtime();
+    }
 #ifdef RT_PHASE_PROF
     // wave-time per phase (s_memtime, scalar): loop overhead, BVH query, KD phase, shading + guard + hand-off;
     // iterations and active lanes at the ray query
@@ -1064,12 +1075,47 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_FIN_BVH_WAVES) wf_finish_bvh(RtDe
     p.slot = 0;
     p.ro = p.rd = rt_v3(0, 0, 0);
     bool active = false, exhausted = false; // exhausted: this lane found the path list empty
+    bool rel = false;                       // (fresh) the lane's pixel has no passes left: let it go
     unsigned long long idle_since = 0;      // (lane 0) when the wave first had nothing to do
     bool seated = false;                    // (lane 0) holds a linger seat
     while (true) {
 #ifdef RT_PHASE_PROF
         const unsigned long long t0 = __builtin_amdgcn_s_memtime();
 #endif
+        // (fresh) pixels whose passes are done are let go — unless a later chained call queued
+        // passes for them meanwhile: those run next, in the pixel's order (its state is this lane's)
+        while (st.fresh && __any(rel)) {
+            if (st.concurrent) { // the pixel's stores visible before the word says it is free
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            if (rel) {
+                uint32_t x = RT_PX_BUSY;
+                if (__hip_atomic_compare_exchange_strong(st.pxo + p.slot, &x, st.concurrent ? RT_PX_REL : 0u,
+                                                         __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT)) {
+                    rel = false;
+                } else {
+                    x = __hip_atomic_exchange(st.pxo + p.slot, RT_PX_BUSY, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const uint32_t owed = x & RT_PX_PASSES;
+                    __hip_atomic_fetch_max(st.ret_ctr + 5, owed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_fetch_add(st.ret_ctr + 6, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    atomicAdd(fr.dev_stats + RT_DEV_OWED_PIXELS, 1ull);
+                    atomicAdd(fr.dev_stats + RT_DEV_OWED_PASSES, (unsigned long long)owed);
+                    p.passes_left = (int)owed;
+                    const Vec3D fb = fr.fb[p.slot];
+                    const float sq = fr.sq[p.slot];
+                    const int count = fr.count[p.slot];
+                    if (start_sample<COUNT>(fr, cam, (int)p.slot, p.passes_left, p.rng, fb, sq, count, p.ro, p.rd,
+                                            c)) {
+                        begin_path(p);
+                        rel = false;
+                        active = true;
+                    }
+                }
+            }
+        }
         if (st.long_return) {
             // free lanes take pixels wf_long returned BEFORE fresh ones (one
             // compare-and-swap per wave): a returned pixel is mid-chain — it may
@@ -1110,8 +1156,9 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_FIN_BVH_WAVES) wf_finish_bvh(RtDe
                     __hip_atomic_fetch_sub(st.ret_ctr + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     active = true;
                     first_ray(st, fr, (uint32_t)v, p);
-                    // back from wf_long: no longer OUT; plus the passes chained calls queued meanwhile
-                    const uint32_t owed = __hip_atomic_exchange(st.pxo + (uint32_t)v, 0u, __ATOMIC_RELAXED,
+                    // back from wf_long: no longer OUT but BUSY (this lane's); plus the passes chained
+                    // calls queued meanwhile
+                    const uint32_t owed = __hip_atomic_exchange(st.pxo + (uint32_t)v, RT_PX_BUSY, __ATOMIC_RELAXED,
                                                                 __HIP_MEMORY_SCOPE_AGENT);
                     p.passes_left += (int)(owed & RT_PX_PASSES);
                     if (owed & RT_PX_PASSES) { // (RT_DEBUG_CALL_LOG: most passes owed, pixels owed; RtDeviations)
@@ -1123,24 +1170,89 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_FIN_BVH_WAVES) wf_finish_bvh(RtDe
                 }
             }
         }
-        const bool need = !active && !exhausted;
-        const unsigned long long m = __ballot(need);
-        if (m) {
-            const int leader = __ffsll((long long)m) - 1;
-            uint32_t base = 0;
-            if (lane == leader) base = atomicAdd(fetch, (uint32_t)__popcll(m));
-            base = __shfl(base, leader);
-            if (need) {
-                const uint32_t e = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-                if (e >= n) {
-                    exhausted = true;
+        if (st.fresh) {
+            // this call's pixels (wf_start's work, in its 8x8-pixel wave tiles): a lane claims its
+            // pixel (BUSY) unless another holder still has it — a previous chained call's finisher
+            // lane or wf_long —, which then owes it this call's passes and runs them next
+            bool claim = !active && !exhausted && !rel, started = false;
+            while (__any(claim)) {
+                const unsigned long long m = __ballot(claim);
+                const int leader = __ffsll((long long)m) - 1;
+                uint32_t base = 0;
+                if (lane == leader) base = atomicAdd(fetch, (uint32_t)__popcll(m));
+                base = __shfl(base, leader);
+                bool acq = false;
+                if (claim) {
+                    const uint32_t e = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+                    int slot = 0;
+                    if (e >= n) {
+                        exhausted = true;
+                        claim = false;
+                    } else if (fresh_pixel(fr, e, slot)) {
+                        uint32_t x = __hip_atomic_load(st.pxo + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        while (true) {
+                            if (x & (RT_PX_OUT | RT_PX_BUSY)) { // held: owed this call's passes
+                                if (__hip_atomic_compare_exchange_strong(st.pxo + slot, &x, x + (uint32_t)fr.passes,
+                                                                         __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                                         __HIP_MEMORY_SCOPE_AGENT))
+                                    break;
+                            } else if (__hip_atomic_compare_exchange_strong(st.pxo + slot, &x, RT_PX_BUSY,
+                                                                            __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                                            __HIP_MEMORY_SCOPE_AGENT)) {
+                                acq = x != 0u; // (released by a possibly concurrent holder)
+                                claim = false;
+                                started = true;
+                                p.slot = (uint32_t)slot;
+                                break;
+                            }
+                        }
+                    }
+                }
+                if (__any(acq)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            }
+            if (started) { // the pixel's state (after the acquire), and its first pass (wf_start's)
+                const uint32_t slot = p.slot;
+                p.rng = fr.rng[slot];
+                Vec3D fb = rt_v3(0.0f, 0.0f, 0.0f);
+                float sq = 0.0f;
+                int count = 0;
+                if (fr.reset) { // reset_frame (rt/render.cuh:18-34)
+                    fr.fb[slot] = fb;
+                    fr.sq[slot] = sq;
+                    fr.count[slot] = count;
                 } else {
+                    fb = fr.fb[slot];
+                    sq = fr.sq[slot];
+                    count = fr.count[slot];
+                }
+                p.passes_left = fr.passes;
+                if (start_sample<COUNT>(fr, cam, (int)slot, p.passes_left, p.rng, fb, sq, count, p.ro, p.rd, c)) {
+                    begin_path(p);
                     active = true;
-                    first_ray(st, fr, e < n1 ? st.q_slot[1][e] : st.q_slot[q][e - n1], p);
+                } else {
+                    rel = true; // no sample this call (adaptive test): let it go
+                }
+            }
+        } else {
+            const bool need = !active && !exhausted;
+            const unsigned long long m = __ballot(need);
+            if (m) {
+                const int leader = __ffsll((long long)m) - 1;
+                uint32_t base = 0;
+                if (lane == leader) base = atomicAdd(fetch, (uint32_t)__popcll(m));
+                base = __shfl(base, leader);
+                if (need) {
+                    const uint32_t e = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+                    if (e >= n) {
+                        exhausted = true;
+                    } else {
+                        active = true;
+                        first_ray(st, fr, st.q_slot[q][e], p);
+                    }
                 }
             }
         }
-        if (!__any(active)) {
+        if (!__any(active || rel)) {
             if (!st.long_return) break; // every lane exhausted
             if (st.linger == 0ull) { // chained: returns left are the next call's (or the drain's)
                 if (lane == 0) __hip_atomic_fetch_sub(ret_word, 1ull << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1178,6 +1290,11 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_FIN_BVH_WAVES) wf_finish_bvh(RtDe
         }
         idle_since = 0;
         bool to_long = false;
+#ifdef RT_LOCKSTEP_PROF
+        uint32_t lk_db = 0, lk_dk = 0;
+        unsigned long long lk_t = 0;
+        const unsigned long long lk_act = (unsigned long long)__popcll(__ballot(active));
+#endif
 #ifdef RT_PHASE_PROF
         const unsigned long long t1 = __builtin_amdgcn_s_memtime();
         ph[0] += t1 - t0;
@@ -1187,7 +1304,19 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_FIN_BVH_WAVES) wf_finish_bvh(RtDe
 #endif
         if (active) {
             float bx = 0.0f, by = 0.0f, bz = 0.0f;
+#ifdef RT_LOCKSTEP_PROF
+            // the query's lane steps (BVH nodes + plane batches of 4, KD nodes + batches) against the
+            // wave's: the BVH phase and the KD phase each run until the wave's slowest lane is done
+            const unsigned long long lb0 = c.v[RT_CNT_B_BVH_NODE] * 4 + c.v[RT_CNT_B_BVH_TRI],
+                                     lk0 = c.v[RT_CNT_NODE] * 4 + c.v[RT_CNT_TRI];
+            const unsigned long long lt0 = __builtin_amdgcn_s_memtime();
+#endif
             const int hit = trace_bvh<COUNT>(sc, p.ro, p.rd, bx, by, bz, stk, c);
+#ifdef RT_LOCKSTEP_PROF
+            lk_t = __builtin_amdgcn_s_memtime() - lt0;
+            lk_db = (uint32_t)((c.v[RT_CNT_B_BVH_NODE] * 4 + c.v[RT_CNT_B_BVH_TRI] - lb0 + 3) / 4);
+            lk_dk = (uint32_t)((c.v[RT_CNT_NODE] * 4 + c.v[RT_CNT_TRI] - lk0 + 3) / 4);
+#endif
 #ifdef RT_PHASE_PROF
             {
                 const unsigned long long t2 = __builtin_amdgcn_s_memtime();
@@ -1218,19 +1347,41 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_FIN_BVH_WAVES) wf_finish_bvh(RtDe
                     }
                 }
             }
-            const bool cam_ray = !p.shadow && p.depth == 1;
             const bool want = shade_step<COUNT>(sc, fr, cam, p, hit, bx, by, bz, limit, c);
-            // heavy-first ordering: a pixel whose camera ray enters glass (where the
-            // deep total-internal-reflection paths start) is marked for later calls
-            if (st.heavy_first && cam_ray && want && p.inside && !(st.heavy[p.slot] & 2u)) st.heavy[p.slot] |= 2u;
             // a path deeper than long_depth goes on in wf_long (64 lanes per ray)
             to_long = want && st.long_depth > 0 && p.depth > st.long_depth;
             if (!want || to_long) store_regs(st, fr, p);
-            if (!want) active = false;
+            if (!want) {
+                active = false;
+                rel = st.fresh != 0; // (the pixel's passes are done: let go at the top of the loop)
+            }
 #ifdef RT_PHASE_PROF
             ph[3] += __builtin_amdgcn_s_memtime() - t2s;
 #endif
         }
+#ifdef RT_LOCKSTEP_PROF
+        if (COUNT) { // (every lane converged here: inactive lanes add 0)
+            uint32_t mb = lk_db, mk = lk_dk, sb = lk_db, sk = lk_dk;
+            for (int off = 32; off > 0; off >>= 1) {
+                mb = max(mb, (uint32_t)__shfl_xor((int)mb, off));
+                mk = max(mk, (uint32_t)__shfl_xor((int)mk, off));
+                sb += (uint32_t)__shfl_xor((int)sb, off);
+                sk += (uint32_t)__shfl_xor((int)sk, off);
+            }
+            unsigned long long tt = lk_t;
+            for (int off = 32; off > 0; off >>= 1) tt = max(tt, (unsigned long long)__shfl_xor(tt, off));
+            if (lane == 0) {
+                atomicAdd(g_phase_acc + 0, 1ull); // (wave-level ray queries)
+                atomicAdd(g_phase_acc + 1, (unsigned long long)(sb + sk));
+                atomicAdd(g_phase_acc + 2, 64ull * mb);
+                atomicAdd(g_phase_acc + 3, (unsigned long long)sb);
+                atomicAdd(g_phase_acc + 4, 64ull * mk);
+                atomicAdd(g_phase_acc + 5, (unsigned long long)sk);
+                atomicAdd(g_phase_acc + 6, lk_act);
+                atomicAdd(g_phase_acc + 7, tt);
+            }
+        }
+#endif
         if (__any(to_long) && publish_long_capped(st, to_long, p.slot, p.ro, p.rd) && to_long) active = false;
     }
 #ifdef RT_PHASE_PROF
@@ -1238,6 +1389,7 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_FIN_BVH_WAVES) wf_finish_bvh(RtDe
         for (int k = 0; k < 7; ++k) atomicAdd(g_phase_acc + k, ph[k]);
 #endif
     if (COUNT) flush_counters(c, fr.counters);
+    if (st.span && lane == 0) atomicMax(st.span + 1, __builtin_amdgcn_s_memrealtime());
     if (st.fin_live) { // this wave's hand-offs are published: the persistent wf_long may stop once all are past here
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -1294,7 +1446,8 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_check(RtDevScene sc, WfState st, 
 
 // The join's check of the hand-off protocol (after every finisher, wf_long and
 // drain of the workspace is done): a pixel still OUT was handed to wf_long and
-// never came back — its frame misses passes.  Counts such pixels (and releases
+// never came back, one still BUSY was never let go by a finisher lane — its
+// frame misses passes.  Counts such pixels (and releases
 // them, so later calls run them again) and the protocol's counters that must
 // be balanced by now: pixels out, returns reserved but unclaimed, hand-off
 // entries reserved but unclaimed, finisher waves still registered alive.
@@ -1304,8 +1457,8 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_verify(WfState st, uint32_t n, ui
     uint32_t out = 0;
     for (uint32_t i = blockIdx.x * WF_BLOCK + threadIdx.x; i < n; i += gridDim.x * WF_BLOCK) {
         const uint32_t x = st.pxo[i];
-        if (x & RT_PX_OUT) {
-            ++out;
+        if (x) { // (free-after-a-concurrent-holder words become plain free: the join ordered everything)
+            out += (x & (RT_PX_OUT | RT_PX_BUSY)) ? 1u : 0u;
             st.pxo[i] = 0u;
         }
     }
@@ -1691,7 +1844,7 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_LONG_WAVES) wf_long(RtDevScene sc
 // time of wf_finish_bvh since the last reset (zeros in other builds)
 extern "C" int rt_debug_phase_profile(unsigned long long *out8, int reset)
 {
-#ifdef RT_PHASE_PROF
+#if defined(RT_PHASE_PROF) || defined(RT_LOCKSTEP_PROF)
     if (hipDeviceSynchronize() != hipSuccess ||
         hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_phase_acc), 8 * sizeof(unsigned long long)) != hipSuccess)
         return RT_E_HIP;
@@ -1764,10 +1917,18 @@ struct Workspace {
     bool verify_unread = false;
     int cus = 0;                                // compute units of the device (the finisher's grid)
     unsigned long long *long_log_buf = nullptr; // RT_DEBUG_LONG_LOG records
-    // the guard runs on pipeline 2's stream beside the next call's finisher: records and counter
-    // per call parity, and the event after each parity's wf_check (the call two later waits for it)
-    hipEvent_t chk_done[2] = {};
-    bool chk_rec[2] = {false, false};
+    int fin_flip = 0; // the next chained call's finisher runs on pipeline 2 (1) or 0 (0)
+    // RtOptions.profile of whole calls: per profiled call its finisher's span on the device
+    // ({first wave start, last wave end}, s_memrealtime) in a ring of WF_PROF_SLOTS, resolved
+    // into RtProfile records by rt_last_profile / rt_profile_history (they join first)
+    unsigned long long *spans = nullptr;
+    unsigned long long prof_seq = 0;
+    struct PendingProf {
+        unsigned long long seq;
+        int passes;
+    };
+    std::vector<PendingProf> prof_pending;
+    std::vector<RtProfile> prof_hist; // resolved, since the last rt_profile_history reset
     unsigned long long call_seq = 0;
     bool chain_open = false; // the last call was a whole-call call with RtOptions.overlap
     ChainKey key{};
@@ -1803,8 +1964,6 @@ int ensure_streams(Workspace &w, int npipes)
         if (hipEventCreateWithFlags(&w.fork, hipEventDisableTiming) != hipSuccess) return -1;
         if (hipEventCreateWithFlags(&w.fin_ready, hipEventDisableTiming) != hipSuccess) return -1;
         if (hipEventCreateWithFlags(&w.long_ev, hipEventDisableTiming) != hipSuccess) return -1;
-        for (auto &e : w.chk_done)
-            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return -1;
         if (hipEventCreate(&w.ev0) != hipSuccess || hipEventCreate(&w.ev1) != hipSuccess) return -1;
         if (hipMalloc((void **)&w.verify_res, 64) != hipSuccess || hipMemset(w.verify_res, 0, 64) != hipSuccess)
             return -1;
@@ -1827,6 +1986,51 @@ int ensure_streams(Workspace &w, int npipes)
 }
 
 int launch_drain(Workspace &w);
+
+#define WF_PROF_SLOTS 256 // profiled whole calls in flight before their spans are read back
+
+// RtOptions.profile of a whole call: a span slot ({~0, 0}: the finisher's waves atomicMin their
+// start and atomicMax their end into it), reset on the finisher's stream
+int resolve_profiles(Workspace &w);
+int prof_slot(Workspace &w, hipStream_t s, unsigned long long **span, int passes)
+{
+    if (!w.spans && hipMalloc((void **)&w.spans, 2 * sizeof(unsigned long long) * WF_PROF_SLOTS) != hipSuccess) {
+        w.spans = nullptr;
+        return -1;
+    }
+    if (w.prof_pending.size() >= WF_PROF_SLOTS && resolve_profiles(w) != 0) return -1;
+    unsigned long long *p = w.spans + 2 * (size_t)(w.prof_seq % WF_PROF_SLOTS);
+    if (hipMemsetD32Async((hipDeviceptr_t)p, (int)0xFFFFFFFF, 2, s) != hipSuccess ||
+        hipMemsetAsync(p + 1, 0, 8, s) != hipSuccess)
+        return -1;
+    w.prof_pending.push_back({w.prof_seq, passes});
+    ++w.prof_seq;
+    *span = p;
+    return 0;
+}
+
+// the pending profiled whole calls' spans -> RtProfile records (waits for their finishers)
+int resolve_profiles(Workspace &w)
+{
+    if (w.prof_pending.empty()) return 0;
+    for (int pi : {0, 2})
+        if (w.pipe[pi].stream && hipStreamSynchronize(w.pipe[pi].stream) != hipSuccess) return -1;
+    std::vector<unsigned long long> sp(2 * WF_PROF_SLOTS);
+    if (hipMemcpy(sp.data(), w.spans, sp.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
+        return -1;
+    for (const auto &q : w.prof_pending) {
+        const unsigned long long a = sp[2 * (q.seq % WF_PROF_SLOTS)], b = sp[2 * (q.seq % WF_PROF_SLOTS) + 1];
+        RtProfile P{};
+        P.finish_launches = 1;
+        P.pipelines = 1;
+        P.finish_ms = b > a ? (float)((double)(b - a) * 1e-5) : 0.0f; // (s_memrealtime: 100 MHz)
+        P.call_ms = P.finish_ms;
+        w.prof_hist.push_back(P);
+        w.prof = P;
+    }
+    w.prof_pending.clear();
+    return 0;
+}
 
 int ensure(Workspace &w, size_t slots, int grid, int npipes)
 {
@@ -1854,7 +2058,7 @@ int ensure(Workspace &w, size_t slots, int grid, int npipes)
                  o_ro = take(slots * 12), o_es = take(slots * 4), o_ee = take(slots * 4), o_px = take(slots * 4);
     // long-path hand-off (shared by the pipelines), wf_long's stack-free wide traversal needs no spill
     const size_t o_le = take(slots * 8), o_lr = take(slots * 32), o_lc = take(256), o_rr = take(slots * 8),
-                 o_rc = take(256), o_hv = take(slots), o_ctl = take(256);
+                 o_rc = take(256), o_ctl = take(256);
     // per pipeline (path lists sized for every pixel: a pipeline never holds
     // more; ray queues for two rays per path: a shadow and an extension ray)
     size_t o_qs0[WF_MAX_PIPES], o_qs1[WF_MAX_PIPES], o_qr0[WF_MAX_PIPES], o_qr1[WF_MAX_PIPES], o_h[WF_MAX_PIPES],
@@ -1873,7 +2077,6 @@ int ensure(Workspace &w, size_t slots, int grid, int npipes)
         return -1;
     }
     char *b = (char *)w.blob;
-    if (hipMemset(b + o_hv, 0, slots) != hipSuccess) return -1; // no history yet
     if (hipMemset(b + o_px, 0, slots * 4) != hipSuccess) return -1; // no pixel out
     if (hipMemset(b + o_ctl, 0, 256) != hipSuccess) return -1;
     w.fin_live = (uint32_t *)(b + o_ctl);
@@ -1912,8 +2115,10 @@ int ensure(Workspace &w, size_t slots, int grid, int npipes)
         st.pxo = (uint32_t *)(b + o_px);
         st.fin_live = nullptr;
         st.chain_flag = (uint32_t *)(b + o_ctl + 128);
-        st.heavy = (uint8_t *)(b + o_hv);
-        st.heavy_first = 0;
+        st.fresh = 0;
+        st.concurrent = 0;
+        st.fresh_n = 0;
+        st.span = nullptr;
         st.chk = nullptr; // (whole-call mode only: launch_whole)
         st.chk_ctr = nullptr;
         st.chk_mask = 0;
@@ -1963,18 +2168,21 @@ int join_all(Workspace &w, hipStream_t stream)
 int debug_long_log(Workspace &w, unsigned long long *buf);
 
 // The whole call in one persistent finisher (bounded traversal, the default):
-// wf_start seeds every pixel's first ray, wf_finish_bvh runs every pixel to
-// the end of its passes (one path per lane), deep paths go to ONE persistent
-// wf_long beside it, and wf_check re-traces the guard's sample.  Nothing here
-// waits on the host: the call is enqueued and returns.
+// wf_finish_bvh takes the call's pixels itself (a lane claims a pixel, runs
+// its passes to the end, one path at a time, and takes the next pixel), deep
+// paths go to ONE persistent wf_long beside it, and wf_check re-traces the
+// guard's sample after it.  Nothing here waits on the host: the call is
+// enqueued and returns.
 //
 // RtOptions.overlap (chained calls): a call of the same frame as the previous
-// overlapping call does not wait for that call's wf_long — pixels still out
-// in it are skipped by wf_start and owed this call's passes (pxo), which the
-// finisher that takes them back (or wf_long itself) runs — and its own
-// wf_long is left running past the call's stream point: rt_join and the
-// library's readers of the frame wait for it.  Results are bit-identical to
-// unchained calls: a pixel's passes run in order whoever runs them.
+// overlapping call does not wait for that call at all.  Its finisher runs on
+// the other of two finisher streams (pipelines 0 and 2), so it starts in the
+// slots the previous finisher's tail frees, and a pixel still held there —
+// by a previous finisher lane (BUSY) or by wf_long (OUT) — is owed this
+// call's passes, which its holder runs before it lets go.  The caller's stream
+// does not wait for the call either: rt_join and the library's readers of the
+// frame do.  Results are bit-identical to unchained calls: a pixel's passes run
+// in order whoever runs them.
 int launch_whole(Workspace &w, int dev, const RtDevScene &sc, const RtDevFrame &fr, const RtDevCamera &cam,
                  hipStream_t stream, int long_depth, bool prof, bool overlap, uint32_t check_mask, int debug,
                  bool count)
@@ -2012,15 +2220,23 @@ int launch_whole(Workspace &w, int dev, const RtDevScene &sc, const RtDevFrame &
     // workspace first (before a larger frame's workspace replaces the old one)
     if (!chained && join_all(w, stream) != 0) return -1;
     if (ensure(w, slots, grid, 1) != 0) return -1;
-    Pipe &pp = w.pipe[0];
+    if (!chained) w.fin_flip = 0;
+    // the finisher's stream: chained calls alternate between pipelines 0 and 2 (the
+    // previous finisher's tail and this one's bulk share the chip); its counters, its
+    // stack spill area and its guard records go with it
+    const int fpi = w.fin_flip ? 2 : 0;
+    w.fin_flip ^= overlap ? 1 : 0;
+    Pipe &pp = w.pipe[fpi];
     WfState st = pp.st;
     const int long_return = long_depth > 0 ? 1 : 0;
     st.long_depth = long_depth;
     st.long_return = long_return;
-    st.heavy_first = long_return;
+    st.fresh = 1;
+    st.concurrent = overlap ? 1 : 0;
+    st.fresh_n = (uint32_t)(((fr.width + 15) / 16) * ((fr.height + 15) / 16)) * 256u;
     st.linger = overlap ? 0ull : WF_FIN_LINGER;
     st.chk_mask = check_mask;
-    const int par = (int)(w.call_seq & 1);
+    const int par = fpi / 2;
     // (the guard's records: allocated by the first call that samples rays)
     if (check_mask != 0xFFFFFFFFu && !w.chk &&
         hipMalloc((void **)&w.chk, 2 * (size_t)WF_CHECK_CAP * 3 * sizeof(RtF4)) != hipSuccess) {
@@ -2058,64 +2274,52 @@ int launch_whole(Workspace &w, int dev, const RtDevScene &sc, const RtDevFrame &
         if (st.long_log && hipMemsetAsync(long_log_buf, 0, 8 * 4 * 65536, stream) != hipSuccess) return -1;
     }
     ++w.call_seq;
-    // fork: the pipeline stream starts after the caller's stream
+    // fork: the finisher's stream starts after the caller's stream
     const hipStream_t s = pp.stream;
     if (hipEventRecord(w.fork, stream) != hipSuccess || hipStreamWaitEvent(s, w.fork, 0) != hipSuccess) return -1;
-    if (prof && hipEventRecord(w.ev0, stream) != hipSuccess) return -1;
-    auto mark = [&](int i) { return !prof || hipEventRecord(pp.ev[i], s) == hipSuccess; };
-    if (!mark(0)) return -1;
     if (hipMemsetAsync(st.counts, 0, 256, s) != hipSuccess) return -1;
     if (st.fin_live && hipMemsetD32Async((hipDeviceptr_t)st.fin_live, (int)(fgrid * (WF_BLOCK / 64)), 1, s) != hipSuccess)
         return -1;
-    if (st.chk) { // (this parity's records: after the wf_check of two calls ago)
-        if (w.chk_rec[par] && hipStreamWaitEvent(s, w.chk_done[par], 0) != hipSuccess) return -1;
-        if (hipMemsetAsync(st.chk_ctr, 0, 4, s) != hipSuccess) return -1;
-    }
+    if (st.chk && hipMemsetAsync(st.chk_ctr, 0, 4, s) != hipSuccess) return -1; // (its last wf_check is behind on s)
     if (long_return && hipMemsetD32Async((hipDeviceptr_t)st.chain_flag, overlap ? 1 : 0, 1, s) != hipSuccess) return -1;
-    const int tiles = ((fr.width + 15) / 16) * ((fr.height + 15) / 16);
-    if (count) hipLaunchKernelGGL(wf_start<true>, dim3(tiles), dim3(WF_BLOCK), 0, s, fr, cam, st, 0, 1);
-    else hipLaunchKernelGGL(wf_start<false>, dim3(tiles), dim3(WF_BLOCK), 0, s, fr, cam, st, 0, 1);
-    if (!mark(1) || !mark(2)) return -1;
+    // RtOptions.profile: the finisher's span on the device (first wave start, last wave end)
+    st.span = nullptr;
+    if (prof) {
+        if (prof_slot(w, s, &st.span, fr.passes) != 0) return -1;
+    }
     if (hipEventRecord(w.fin_ready, s) != hipSuccess) return -1;
     // (the finisher is launched before its wf_long: on a shared hardware queue
     // it then completes first, and wf_long finds its producers done.  Counting:
     // the finisher's own work; wf_long's deep paths are not counted)
     if (count) hipLaunchKernelGGL(wf_finish_bvh<true>, dim3(fgrid), dim3(WF_BLOCK), 0, s, sc, fr, cam, st, 0);
+    else if (fgrid <= w.cus * WF_FIN_SMALL_WAVES)
+        hipLaunchKernelGGL((wf_finish_bvh<false, 1>), dim3(fgrid), dim3(WF_BLOCK), 0, s, sc, fr, cam, st, 0);
     else hipLaunchKernelGGL(wf_finish_bvh<false>, dim3(fgrid), dim3(WF_BLOCK), 0, s, sc, fr, cam, st, 0);
-    if (hipGetLastError() != hipSuccess || !mark(3)) return -1;
+    if (hipGetLastError() != hipSuccess) return -1;
     Pipe *lp = nullptr;
     if (long_return) {
-        lp = &w.pipe[1 + (WF_LONG_PINGPONG ? (int)(w.call_seq & 1) : 0)];
+        lp = &w.pipe[1];
         if (hipStreamWaitEvent(lp->stream, w.fin_ready, 0) != hipSuccess) return -1;
         hipLaunchKernelGGL(wf_long<false>, dim3(WF_LONG_BLOCKS), dim3(WF_BLOCK), 0, lp->stream, sc, fr, cam, st, 1);
         if (hipGetLastError() != hipSuccess) return -1;
         if (hipEventRecord(lp->long_done, lp->stream) != hipSuccess) return -1;
         lp->long_rec = true;
     }
-    if (!mark(4)) return -1;
     if (st.chk) {
-        // the guard's re-traces beside the next call (pipeline 2): latency-bound single-lane KD
+        // the guard's re-traces after the finisher on its stream (its KD stacks in the finisher's
+        // spill area), beside the next chained call's finisher: latency-bound single-lane KD
         // traversals, 256 blocks
-        // (its KD stacks spill into pipeline 2's area: pipeline 0's belongs to the next finisher)
-        Pipe &cp = w.pipe[2];
-        WfState cs = st;
-        cs.spill = cp.st.spill;
-        if (!cs.spill) return -1;
-        if (hipEventRecord(pp.fin_done, s) != hipSuccess || hipStreamWaitEvent(cp.stream, pp.fin_done, 0) != hipSuccess)
-            return -1;
-        hipLaunchKernelGGL(wf_check, dim3(WF_CHECK_BLOCKS), dim3(WF_BLOCK), 0, cp.stream, sc, cs, fr.dev_stats);
+        hipLaunchKernelGGL(wf_check, dim3(WF_CHECK_BLOCKS), dim3(WF_BLOCK), 0, s, sc, st, fr.dev_stats);
         if (hipGetLastError() != hipSuccess) return -1;
-        if (hipEventRecord(w.chk_done[par], cp.stream) != hipSuccess || hipEventRecord(cp.join, cp.stream) != hipSuccess)
-            return -1;
-        w.chk_rec[par] = true;
-        cp.joined = true;
     }
     if (hipEventRecord(pp.join, s) != hipSuccess) return -1;
     pp.joined = true;
-    // join: the caller's stream continues after the finisher — and, unless the
-    // call overlaps the next one, after its wf_long
-    if (hipStreamWaitEvent(stream, pp.join, 0) != hipSuccess) return -1;
-    if (!overlap && lp && hipStreamWaitEvent(stream, lp->long_done, 0) != hipSuccess) return -1;
+    // join: unless the call overlaps the next one, the caller's stream continues after the
+    // finisher (and the guard) and after its wf_long
+    if (!overlap) {
+        if (hipStreamWaitEvent(stream, pp.join, 0) != hipSuccess) return -1;
+        if (lp && hipStreamWaitEvent(stream, lp->long_done, 0) != hipSuccess) return -1;
+    }
     w.chain_open = overlap && long_return;
     w.verify_pending = w.verify_pending || long_return;
     w.key = key;
@@ -2125,19 +2329,6 @@ int launch_whole(Workspace &w, int dev, const RtDevScene &sc, const RtDevFrame &
     w.last_cam = cam;
     w.last_long_depth = long_depth;
     w.last_debug = debug;
-    if (prof) {
-        if (hipEventRecord(w.ev1, stream) != hipSuccess || hipEventSynchronize(pp.ev[4]) != hipSuccess ||
-            hipEventSynchronize(w.ev1) != hipSuccess)
-            return -1;
-        RtProfile P{};
-        P.iterations = 0;
-        P.finish_launches = 1;
-        P.start_ms = elapsed_ms(pp.ev[0], pp.ev[1]);
-        P.finish_ms = elapsed_ms(pp.ev[2], pp.ev[3]);
-        P.call_ms = elapsed_ms(w.ev0, w.ev1);
-        P.pipelines = 1;
-        w.prof = P;
-    }
     if (debug & RT_DEBUG_CALL_LOG) {
         (void)hipStreamSynchronize(s);
         timespec ts;
@@ -2157,11 +2348,12 @@ int launch_whole(Workspace &w, int dev, const RtDevScene &sc, const RtDevFrame &
 
 // The drain of an open chain (join_all, i.e. rt_join and every reader of the
 // frame, or the next call that does not continue it): a chained call's
-// finisher leaves pixels wf_long hands back after its path list ran out to the
-// next call; here one more finisher with an empty path list takes them, runs
-// their remaining passes (handing deep samples to its own wf_long again) and
-// lingers while any pixel is still out.  Enqueued on pipeline 0 after the
-// chain's last finisher; join_all then waits for it and every wf_long.
+// finisher leaves pixels wf_long hands back after its pixel list ran out to
+// the next call; here one more finisher with no pixels of its own takes them,
+// runs their remaining passes (handing deep samples to its own wf_long again)
+// and lingers while any pixel is still out.  Enqueued on pipeline 0 after the
+// chain's last finishers on both finisher streams; join_all then waits for it
+// and every wf_long.
 int launch_drain(Workspace &w)
 {
     if (!w.chain_open) return 0;
@@ -2172,7 +2364,10 @@ int launch_drain(Workspace &w)
     WfState st = pp.st;
     st.long_depth = w.last_long_depth;
     st.long_return = 1;
-    st.heavy_first = 1;
+    st.fresh = 1;
+    st.fresh_n = 0; // (no pixels of its own)
+    st.concurrent = 0;
+    st.span = nullptr;
     st.linger = WF_FIN_LINGER; // (a pixel still out after it: wf_long runs it to the end)
     st.chk = nullptr;
     st.chk_mask = 0;
@@ -2185,15 +2380,18 @@ int launch_drain(Workspace &w)
     st.fin_live = w.fin_live + (uint32_t)(w.call_seq % 8);
     ++w.call_seq;
     const hipStream_t s = pp.stream;
-    // an empty path list (counts[6], counts[7] = 0), no linger seat taken yet
+    if (w.pipe[2].joined && hipStreamWaitEvent(s, w.pipe[2].join, 0) != hipSuccess) return -1;
+    // no pixels (counts[4] = 0 of fresh_n 0), no linger seat taken yet
     if (hipMemsetAsync(st.counts, 0, 256, s) != hipSuccess) return -1;
     if (hipMemsetAsync(st.ret_ctr + 4, 0, 4, s) != hipSuccess) return -1;
     if (hipMemsetAsync(st.chain_flag, 0, 4, s) != hipSuccess) return -1; // the chain's wf_longs may leave once idle
     if (hipMemsetD32Async((hipDeviceptr_t)st.fin_live, (int)(fgrid * (WF_BLOCK / 64)), 1, s) != hipSuccess) return -1;
     if (hipEventRecord(w.fin_ready, s) != hipSuccess) return -1;
-    hipLaunchKernelGGL(wf_finish_bvh<false>, dim3(fgrid), dim3(WF_BLOCK), 0, s, w.last_sc, fr, w.last_cam, st, 0);
+    if (fgrid <= w.cus * WF_FIN_SMALL_WAVES)
+        hipLaunchKernelGGL((wf_finish_bvh<false, 1>), dim3(fgrid), dim3(WF_BLOCK), 0, s, w.last_sc, fr, w.last_cam, st, 0);
+    else hipLaunchKernelGGL(wf_finish_bvh<false>, dim3(fgrid), dim3(WF_BLOCK), 0, s, w.last_sc, fr, w.last_cam, st, 0);
     if (hipGetLastError() != hipSuccess) return -1;
-    Pipe &lp = w.pipe[1 + (WF_LONG_PINGPONG ? (int)(w.call_seq & 1) : 0)];
+    Pipe &lp = w.pipe[1];
     if (hipStreamWaitEvent(lp.stream, w.fin_ready, 0) != hipSuccess) return -1;
     hipLaunchKernelGGL(wf_long<false>, dim3(WF_LONG_BLOCKS), dim3(WF_BLOCK), 0, lp.stream, w.last_sc, fr, w.last_cam, st, 1);
     if (hipGetLastError() != hipSuccess) return -1;
@@ -2339,7 +2537,7 @@ void rt_wavefront_shutdown()
         if (w->blob) (void)launch_drain(*w); // (an open chain's wf_longs leave only after its drain)
         (void)hipDeviceSynchronize();
         if (w->blob) (void)hipFree(w->blob);
-        for (void *p : {(void *)w->chk, (void *)w->verify_res, (void *)w->long_log_buf})
+        for (void *p : {(void *)w->chk, (void *)w->verify_res, (void *)w->long_log_buf, (void *)w->spans})
             if (p) (void)hipFree(p);
         for (int i = WF_MAX_PIPES - 1; i >= 0; --i) {
             Pipe &p = w->pipe[i];
@@ -2351,7 +2549,7 @@ void rt_wavefront_shutdown()
             if (p.host_count) (void)hipHostFree(p.host_count);
             if (p.stream) (void)hipStreamDestroy(p.stream);
         }
-        for (hipEvent_t e : {w->chk_done[1], w->chk_done[0], w->ev1, w->ev0, w->long_ev, w->fin_ready, w->fork})
+        for (hipEvent_t e : {w->ev1, w->ev0, w->long_ev, w->fin_ready, w->fork})
             if (e) (void)hipEventDestroy(e);
         delete w;
         kv.second = nullptr;
@@ -2367,7 +2565,29 @@ extern "C" int rt_last_profile(RtProfile *out)
     if (hipGetDevice(&dev) != hipSuccess) return RT_E_HIP;
     std::lock_guard<std::mutex> g(g_ws_mu);
     auto it = g_ws.find(dev);
-    *out = it == g_ws.end() || !it->second ? RtProfile{} : it->second->prof;
+    if (it == g_ws.end() || !it->second) {
+        *out = RtProfile{};
+        return RT_OK;
+    }
+    if (resolve_profiles(*it->second) != 0) return RT_E_HIP;
+    *out = it->second->prof;
+    return RT_OK;
+}
+
+extern "C" int rt_profile_history(RtProfile *out, int cap, int *count, int reset)
+{
+    if ((!out && cap > 0) || cap < 0 || !count) return RT_E_INVALID;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return RT_E_HIP;
+    std::lock_guard<std::mutex> g(g_ws_mu);
+    auto it = g_ws.find(dev);
+    *count = 0;
+    if (it == g_ws.end() || !it->second) return RT_OK;
+    Workspace &w = *it->second;
+    if (resolve_profiles(w) != 0) return RT_E_HIP;
+    *count = (int)w.prof_hist.size();
+    for (int i = 0; i < cap && i < *count; ++i) out[i] = w.prof_hist[i];
+    if (reset) w.prof_hist.clear();
     return RT_OK;
 }
 
@@ -2458,7 +2678,6 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
         WfState &st = w.pipe[pi].st;
         st.long_depth = long_depth;
         st.long_return = 0;
-        st.heavy_first = 0;
         st.fin_live = nullptr;
         st.long_log = nullptr;
     }
@@ -2707,6 +2926,7 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
         if (hi > lo) P.trace_union_ms += hi - lo;
         P.pipelines = npipes;
         w.prof = P;
+        w.prof_hist.push_back(P);
     }
     return 0;
 }

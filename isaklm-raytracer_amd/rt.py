@@ -74,6 +74,16 @@ def last_profile():
     return {k: getattr(p, k) for k, _ in RtProfile._fields_}
 
 
+def profile_history(reset=False):
+    """RtProfile of every profiled rt_render since the last reset, oldest first
+    (rt_profile_history: waits for those calls' kernels, not for the chain)."""
+    n = ctypes.c_int(0)
+    check(lib().rt_profile_history(None, 0, ctypes.byref(n), 0))
+    buf = (RtProfile * max(n.value, 1))()
+    check(lib().rt_profile_history(buf, n.value, ctypes.byref(n), int(reset)))
+    return [{k: getattr(buf[i], k) for k, _ in RtProfile._fields_} for i in range(n.value)]
+
+
 DEV_HIST_BINS = 18
 
 
@@ -183,6 +193,7 @@ def lib():
         L.rt_save_render.argtypes = [G_Buffer, i, i, ctypes.c_char_p]
         L.rt_deviation_stats.argtypes = [ctypes.POINTER(RtDeviations), i]
         L.rt_join.argtypes = [vp]
+        L.rt_profile_history.argtypes = [ctypes.POINTER(RtProfile), i, ctypes.POINTER(i), i]
         L.rt_shutdown.restype = None
         L.rt_abi_version.restype = i
         if L.rt_abi_version() != ABI_VERSION:

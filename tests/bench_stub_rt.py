@@ -121,10 +121,21 @@ def render(dscene, gb, camera, sample_count, opt):
     ms = (time.perf_counter() - t) * 1e3
     _last.update(iterations=1, trace_launches=1, shade_launches=1, finish_launches=0, start_ms=0.0, trace_ms=ms,
                  shade_ms=0.0, finish_ms=0.0, call_ms=ms, trace_union_ms=ms, pipelines=1)
+    _hist.append(dict(_last))
+
+
+_hist = []
 
 
 def last_profile():
     return dict(_last)
+
+
+def profile_history(reset=False):
+    out = [dict(h) for h in _hist]
+    if reset:
+        _hist.clear()
+    return out
 
 
 class DeviceCounters:
