@@ -457,6 +457,249 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_BVH_WAVES) wf_trace_bvh(RtDevScen
     if (COUNT) flush_counters(c, counters);
 }
 
+// trace_bvh (bvh_trace.h) with dynamic ray fetch: every lane runs its own ray
+// through the same steps — the s_min query over the 4-wide BVH, then the
+// bounded KD phase — but a round advances each lane by at most `cap` node
+// steps of its current phase and one leaf, and a lane whose ray is done takes
+// the next queued ray at the start of the next round (Aila & Laine's
+// persistent while-while with per-lane refill), so a wave is not held for its
+// slowest ray.  Same per-ray arithmetic and visiting order as trace_bvh: the
+// same hits, bit for bit.  (Rays that lie in a KD split plane — zero direction
+// components — take the plain KD traversal, as in trace_bvh: s_min = -inf.)
+#ifndef WF_DYN_WAVES
+#define WF_DYN_WAVES 6
+#endif
+#ifndef WF_BVH_DYN
+#define WF_BVH_DYN 1 // the queue path's bounded trace launches: per-lane refill (0: wf_trace_bvh, lockstep rays)
+#endif
+#ifndef WF_BVH_DYN_CAP
+#define WF_BVH_DYN_CAP 8 // node steps per phase per round
+#endif
+template <bool COUNT>
+__global__ void __launch_bounds__(WF_BLOCK, WF_DYN_WAVES) wf_trace_bvh_dyn(RtDevScene sc, WfState st, int q,
+                                                                          unsigned long long *counters, int cap)
+{
+    Cnt c;
+    if (COUNT) c.zero();
+    __shared__ uint32_t s_node[WF_BVH_LDS * WF_BLOCK];
+    __shared__ float s_entry[WF_BVH_LDS * WF_BLOCK];
+    const int tid = threadIdx.x;
+    const int gtid = blockIdx.x * WF_BLOCK + tid;
+    Stack<WF_BVH_LDS> stk{s_node + tid, s_entry + tid, WF_BLOCK, st.spill + gtid, st.spill_threads};
+    const uint32_t n = st.counts[q];
+    const RtF4 *rays = st.q_ray[q];
+    uint32_t *fetch = st.counts + 2 + q;
+    const int lane = __lane_id();
+    // per lane: 0 no ray, 1 s_min query (cur: BVH4 reference), 2 KD phase (node, nd: its words once loaded)
+    int phase = 0;
+    bool exhausted = false;
+    uint32_t e = 0, cur = 0, node = 0;
+    uint2 nd = make_uint2(0u, 0u);
+    bool nd_ok = false; // nd holds node's words
+    int sp = 0;
+    Vec3D o = rt_v3(0, 0, 0), d = rt_v3(0, 0, 0), inv = rt_v3(0, 0, 0);
+    float m = 0.0f, best = 0.0f, entry = 0.0f, exit_ = 0.0f, root_exit = 0.0f, s_min = 0.0f;
+    while (true) {
+        // ---- refill: lanes without a ray take the next queued one
+        const bool need = phase == 0 && !exhausted;
+        const unsigned long long mm = __ballot(need);
+        if (mm) {
+            const int leader = __ffsll((long long)mm) - 1;
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(fetch, (uint32_t)__popcll(mm));
+            base = __shfl(base, leader);
+            if (need) {
+                e = base + (uint32_t)__popcll(mm & ((1ull << lane) - 1ull));
+                if (e >= n) {
+                    exhausted = true;
+                } else {
+                    o = ld3(ldf4(rays + 2 * (size_t)e));
+                    d = ld3(ldf4(rays + 2 * (size_t)e + 1));
+                    if (COUNT) c.v[RT_CNT_RAY]++;
+                    if (!bbox_hit(sc, o, d, entry, exit_)) {
+                        *reinterpret_cast<float4 *>(st.hits + e) = miss_record();
+                    } else {
+                        root_exit = exit_;
+                        sp = 0;
+                        if (rt_bounded_ray(o, d, sc.split_vals, sc.split_off)) {
+                            phase = 1;
+                            m = rt_ray_margin(o.x, o.y, o.z, sc.bvh_scale);
+                            inv = rt_v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+                            best = exit_;
+                            cur = 0;
+                        } else {
+                            phase = 2; // the plain KD traversal
+                            s_min = -INFINITY;
+                            node = 0;
+                            nd_ok = false;
+                        }
+                    }
+                }
+            }
+        }
+        if (!__any(phase != 0)) {
+            if (__all(exhausted)) break;
+            continue;
+        }
+        // ---- s_min query: up to `cap` inner nodes, then a leaf (bvh4_bound)
+        for (int i = 0; i < cap; ++i) {
+            const bool step = phase == 1 && !(cur & RT_BVH_LEAF);
+            if (!__any(step)) break;
+            if (step) {
+                if (COUNT) c.v[RT_CNT_B_BVH_NODE]++;
+                const Vec3D om = rt_v3(o.x + m, o.y + m, o.z + m), op = rt_v3(o.x - m, o.y - m, o.z - m);
+                const RtF4 *p4 = sc.bvh4 + 8 * (size_t)cur;
+                const RtF4 lx = ldc4(p4), ly = ldc4(p4 + 1), lz = ldc4(p4 + 2), hx = ldc4(p4 + 3),
+                           hy = ldc4(p4 + 4), hz = ldc4(p4 + 5);
+                const uint4 rf = ldc_u4(reinterpret_cast<const uint32_t *>(p4 + 6));
+                float t0, t1, t2, t3;
+                uint32_t r0 = rf.x, r1 = rf.y, r2 = rf.z, r3 = rf.w;
+                if (!(rt_bvh_box(lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, om, op, inv, best, t0) && r0 != RT_BVH_EMPTY)) {
+                    t0 = INFINITY;
+                    r0 = RT_BVH_EMPTY;
+                }
+                if (!(rt_bvh_box(lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, om, op, inv, best, t1) && r1 != RT_BVH_EMPTY)) {
+                    t1 = INFINITY;
+                    r1 = RT_BVH_EMPTY;
+                }
+                if (!(rt_bvh_box(lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, om, op, inv, best, t2) && r2 != RT_BVH_EMPTY)) {
+                    t2 = INFINITY;
+                    r2 = RT_BVH_EMPTY;
+                }
+                if (!(rt_bvh_box(lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, om, op, inv, best, t3) && r3 != RT_BVH_EMPTY)) {
+                    t3 = INFINITY;
+                    r3 = RT_BVH_EMPTY;
+                }
+                auto cswap = [](float &ta, uint32_t &ra, float &tb, uint32_t &rb) {
+                    const bool sw = tb < ta || (ra == RT_BVH_EMPTY && rb != RT_BVH_EMPTY);
+                    const float t = sw ? tb : ta, u = sw ? ta : tb;
+                    const uint32_t r = sw ? rb : ra, qq = sw ? ra : rb;
+                    ta = t;
+                    tb = u;
+                    ra = r;
+                    rb = qq;
+                };
+                cswap(t0, r0, t1, r1);
+                cswap(t2, r2, t3, r3);
+                cswap(t0, r0, t2, r2);
+                cswap(t1, r1, t3, r3);
+                cswap(t1, r1, t2, r2);
+                if (r3 != RT_BVH_EMPTY) stk.put(sp++, r3, t3);
+                if (r2 != RT_BVH_EMPTY) stk.put(sp++, r2, t2);
+                if (r1 != RT_BVH_EMPTY) stk.put(sp++, r1, t1);
+                if (r0 != RT_BVH_EMPTY) {
+                    cur = r0;
+                } else { // pop the next subtree that may still hold a smaller s
+                    cur = RT_BVH_EMPTY;
+                    while (sp > 0) {
+                        uint32_t nn;
+                        float tn;
+                        stk.get(--sp, nn, tn);
+                        if (tn <= best) {
+                            cur = nn;
+                            break;
+                        }
+                    }
+                }
+            }
+        }
+        // (cur == RT_BVH_EMPTY carries the leaf bit: such a lane is done with the query)
+        const bool bleaf = phase == 1 && (cur & RT_BVH_LEAF) && cur != RT_BVH_EMPTY;
+        if (__any(bleaf) && bleaf) {
+            const uint32_t first = (cur & ~RT_BVH_LEAF) >> 3, end = first + (cur & 7u) + 1u;
+            if (COUNT) c.v[RT_CNT_B_BVH_TRI] += end - first;
+            float bx, by, bz;
+            (void)leaf_scan<COUNT>(sc.bvh_a, sc.bvh_bary, first, end, o, d, best, bx, by, bz, c);
+            cur = RT_BVH_EMPTY;
+            while (sp > 0) {
+                uint32_t nn;
+                float tn;
+                stk.get(--sp, nn, tn);
+                if (tn <= best) {
+                    cur = nn;
+                    break;
+                }
+            }
+        }
+        if (phase == 1 && cur == RT_BVH_EMPTY) { // the query is over: s_min, then the KD phase (or a miss)
+            s_min = best;
+            if (!(s_min < root_exit)) {
+                *reinterpret_cast<float4 *>(st.hits + e) = miss_record();
+                phase = 0;
+            } else {
+                phase = 2;
+                node = 0;
+                nd_ok = false;
+                sp = 0;
+                exit_ = root_exit; // (entry: the scene box's, unchanged since the refill)
+            }
+        }
+        // ---- KD phase (trace_bvh's): up to `cap` node fetches, then the leaf
+        for (int i = 0; i < cap; ++i) {
+            const bool step = phase == 2 && !(nd_ok && (nd.y & 3u) == RT_LEAF_TAG);
+            if (!__any(step)) break;
+            if (step) {
+                if (nd_ok) { // an inner node: the reference's split step
+                    const uint32_t axis = nd.y & 3u;
+                    const float split = as_float(nd.x);
+                    const float oax = axis == 0 ? o.x : (axis == 1 ? o.y : o.z);
+                    const float dax = axis == 0 ? d.x : (axis == 1 ? d.y : d.z);
+                    const float yax = rt_recip_guard(dax);
+                    uint32_t near_c = node + 1, far_c = nd.y >> 2;
+                    if (oax >= split) { // ray_behind_plane (rt/trace_ray.cuh:174-188)
+                        near_c = nd.y >> 2;
+                        far_c = node + 1;
+                    }
+                    const float t = rt_div_by(split - oax, dax, yax); // intersect_plane (:190-210)
+                    if (t >= exit_ || t < 0) {
+                        node = near_c;
+                    } else if (t <= entry) {
+                        node = far_c;
+                    } else if (t <= s_min) { // the near side holds no hit: its leaves' exits are <= t
+                        node = far_c;
+                        entry = t;
+                    } else {
+                        stk.put(sp++, far_c, t);
+                        node = near_c;
+                        exit_ = t;
+                    }
+                }
+                nd = ldc_u2(sc.nodes + 2 * (size_t)node);
+                nd_ok = true;
+                if (COUNT) c.v[RT_CNT_NODE]++;
+            }
+        }
+        const bool kleaf = phase == 2 && nd_ok && (nd.y & 3u) == RT_LEAF_TAG;
+        if (__any(kleaf) && kleaf) {
+            const uint32_t count = nd.y >> 2;
+            int best_tri = -1;
+            float bx = 0.0f, by = 0.0f, bz = 0.0f;
+            if (count > 0 && exit_ > s_min) { // trace_leaf_node (:115-172): closest starts at the leaf's exit
+                float smallest = exit_;
+                if (COUNT) c.v[RT_CNT_TRI] += count;
+                const int be = leaf_scan<COUNT>(sc.isect_a, sc.isect_bary, nd.x, nd.x + count, o, d, smallest, bx, by,
+                                                bz, c);
+                best_tri = be >= 0 ? (int)ldc_u2(&sc.isect_bary[be].rd).y : -1;
+            }
+            if (best_tri >= 0) {
+                if (COUNT) c.v[RT_CNT_HIT]++;
+                *reinterpret_cast<float4 *>(st.hits + e) = make_float4(__int_as_float(best_tri), bx, by, bz);
+                phase = 0;
+            } else if (sp == 0) {
+                *reinterpret_cast<float4 *>(st.hits + e) = miss_record();
+                phase = 0;
+            } else {
+                --sp;
+                node = stk.node_at(sp);
+                entry = stk.entry_at(sp);
+                exit_ = sp > 0 ? stk.entry_at(sp - 1) : root_exit;
+                nd_ok = false;
+            }
+        }
+    }
+    if (COUNT) flush_counters(c, counters);
+}
+
 // Persistent trace with dynamic ray fetch: every lane runs rays one leaf at a
 // time; a lane whose ray is done writes its hit and takes the next queued ray
 // at the next leaf boundary (one wave-aggregated atomic), so a wave is never
@@ -2813,7 +3056,14 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
             if (hipMemsetAsync(st.counts + 6 + (q ^ 1), 0, 4, s) != hipSuccess) return -1; // next path list
             if (hipMemsetAsync(st.counts + 2 + q, 0, 4, s) != hipSuccess) return -1; // fetch cursor
             if (!mark(4)) return -1;
-            if (bounded) {
+            if (bounded && WF_BVH_DYN) {
+                if (count)
+                    hipLaunchKernelGGL(wf_trace_bvh_dyn<true>, dim3(grid), dim3(WF_BLOCK), 0, s, sc, st, q, fr.counters,
+                                       WF_BVH_DYN_CAP);
+                else
+                    hipLaunchKernelGGL(wf_trace_bvh_dyn<false>, dim3(grid), dim3(WF_BLOCK), 0, s, sc, st, q, nullptr,
+                                       WF_BVH_DYN_CAP);
+            } else if (bounded) {
                 if (count)
                     hipLaunchKernelGGL(wf_trace_bvh<true>, dim3(grid), dim3(WF_BLOCK), 0, s, sc, st, q, fr.counters);
                 else

@@ -95,6 +95,19 @@ def test_wavefront_finisher_modes(scene, tail, waves, wide):
     assert gcnt == rcnt
 
 
+@pytest.mark.parametrize("scene", ["room_small", "cornell_blob", "room2m"])
+def test_bounded_queue_path(scene):
+    """The queue path with the bounded traversal (wf_tail = 1: trace / shade
+    iterations to the end, no finisher): its trace launches run
+    wf_trace_bvh_dyn (per-lane ray refill, capped steps per round), which
+    must give trace_bvh's hits bit for bit — every pixel against the oracle."""
+    run = helpers.GpuRun(scene)
+    W, H, P = (160, 90, 3) if scene == "room2m" else (48, 27, 3)
+    gpu, _, _ = run.render(W, H, P, calls=2, kernel=rt.KERNEL_WAVEFRONT, wf_tail=1)
+    ref, _ = helpers.oracle_render(run.path, W, H, P, calls=2)
+    helpers.assert_bitwise(gpu, ref, what=f"{scene} bounded queue path")
+
+
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("scene", ["room_small", "cornell_blob"])
 @pytest.mark.parametrize("long_depth,pipes", [(1, 3), (3, 1), (-1, 2)],
