@@ -609,9 +609,20 @@ def main(argv=None, binding=None):
             cprof = rt.last_profile()
             kname = "wf_finish_bvh<false>"
             launches = sum(p["finish_launches"] for p in profiles)
-            avg_launch_ms = sum(p["finish_ms"] for p in profiles) / max(launches, 1)
+            # per call: the finishers' busy time (the union of their device spans: chained calls'
+            # finishers overlap, and a finisher goes on with the next issued call's pixels) over the
+            # timed calls — the time one launch's worth of work (a call's W x H x passes samples) took
+            busy, hi = 0.0, None
+            for a, b in sorted((p["start_ms"], p["start_ms"] + p["finish_ms"]) for p in profiles):
+                if hi is None or a > hi:
+                    busy += b - a
+                    hi = b
+                elif b > hi:
+                    busy += b - hi
+                    hi = b
+            avg_launch_ms = busy / max(launches, 1)
             counted_launches = cprof["finish_launches"]
-            # per launch: the counted bytes per sample x the samples one timed launch runs
+            # per launch: the counted bytes per sample x the samples one timed call runs
             # (every pixel's passes of its call: W x H x passes-per-call, adaptive off)
             samples_per_launch = n * sum(p["passes"] for p in profiles) / max(launches, 1)
             trace_bytes = bounded_kernel_bytes(bc) / max(bc["sample"], 1) * samples_per_launch
@@ -646,6 +657,8 @@ def main(argv=None, binding=None):
             "trace_ms_per_call": round(float(np.mean([p["trace_ms"] for p in profiles])), 3),
             "shade_ms_per_call": round(float(np.mean([p["shade_ms"] for p in profiles])), 3),
             "finish_ms_per_call": round(float(np.mean([p["finish_ms"] for p in profiles])), 3),
+            "finisher_spans_ms": [[round(p["start_ms"], 1), round(p["start_ms"] + p["finish_ms"], 1)] for p in profiles]
+            if bounded else None,
             "call_ms": round(float(np.mean([p["call_ms"] for p in profiles])), 3),
             "iterations_per_call": round(float(np.mean([p["iterations"] for p in profiles])), 1),
             "passes_per_call": round(float(np.mean([p["passes"] for p in profiles])), 1),

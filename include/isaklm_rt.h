@@ -519,8 +519,10 @@ int rt_last_profile(RtProfile *out);
  * oldest first: up to `cap` into out, the number recorded into *count.  For
  * the default render (one finisher launch per call) finish_ms and call_ms are
  * the finisher's span on the device, from its first wave's start to its last
- * wave's end (chained calls' finishers overlap: their spans do too).  Waits
- * for those calls' finishers. */
+ * wave's end (chained calls' finishers overlap: their spans do too), and
+ * start_ms its start relative to the earliest start among the calls resolved
+ * together (by this call or rt_last_profile).  Waits for those calls'
+ * finishers. */
 int rt_profile_history(RtProfile *out, int cap, int *count, int reset);
 
 /* Always-on deviation statistics of every rt_render on the current device

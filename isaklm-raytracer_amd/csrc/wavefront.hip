@@ -100,6 +100,16 @@ static_assert(WF_BLOCK % WF_TBLOCK == 0 && WF_TBLOCK % 64 == 0, "WF_TBLOCK must 
 #ifndef WF_FIN_BVH_WAVES
 #define WF_FIN_BVH_WAVES 5 // wf_finish_bvh occupancy target (5: +3 % over 6 with the 4-wide s_min query, profiles/r04)
 #endif
+#define WF_CALL_RING 16      // chained calls' descriptor slots (call id % WF_CALL_RING)
+#define WF_CALL_CURSORS (1u << 20) // their pixel-list cursors (call id % WF_CALL_CURSORS, epoch-tagged): a
+                                   // wave would have to lag 2^20 calls behind to meet a reused one
+#define WF_CALLS_IN_FLIGHT 8 // a call is issued once the call this many before it has run its list out
+#ifndef WF_FIN_FENCE
+#define WF_FIN_FENCE 1 // (A/B only: 0 drops the release fence of pixels let go beside a concurrent finisher)
+#endif
+#ifndef WF_FIN_ALT
+#define WF_FIN_ALT 1 // chained finishers alternate between pipelines 0 and 2 (0: all on pipeline 0)
+#endif
 #ifndef WF_FIN_SMALL_WAVES
 #define WF_FIN_SMALL_WAVES 3 // frames of at most this many finisher waves per SIMD take the unspilled build (151 VGPRs: 3 waves)
 #endif
@@ -144,7 +154,8 @@ static_assert(WF_BLOCK % WF_TBLOCK == 0 && WF_TBLOCK % 64 == 0, "WF_TBLOCK must 
 // (a KD re-trace costs ~50 bounded queries: 1024 took 4 % of a 256-pass
 // room2m call, 4096 ~1 %, and still checks ~2M rays in the 20-step bench)
 #define WF_CHECK_INTERVAL_DEFAULT 4096u
-#define WF_CHECK_CAP (1u << 20)         // cross-check records per call (more are dropped: RT_DEV_CHK_DROP)
+#define WF_CHECK_CAP (1u << 22)         // cross-check records per launch (more are dropped: RT_DEV_CHK_DROP;
+                                        // a chained launch may run several calls' pixels)
 // per-pixel ownership word (WfState.pxo) of the whole-call render: a pixel is
 // BUSY while a finisher lane runs its passes and OUT while wf_long holds it
 // (handed over, or in the return ring), until a finisher lane takes it back or
@@ -205,6 +216,17 @@ struct WfState {
     int fresh, concurrent;
     uint32_t fresh_n; // (fresh) entries: 256 per 16x16-pixel tile (fresh_pixel); 0 for a chain's drain
     unsigned long long *span; // RtOptions.profile: {first wave start, last wave end} (s_memrealtime)
+    // chained calls (RtOptions.overlap): a finisher whose call's pixel list has run out goes on
+    // with the next call of the chain, if the host has issued it — so a chain runs without a
+    // kernel boundary between its calls, and the finisher launched by a later call only adds
+    // lanes.  call_id: this launch's call; call_ring (pinned host memory): issued calls,
+    // slot id % WF_CALL_RING = id << 32 | passes; call_ctr: per call (id % WF_CALL_CURSORS),
+    // id << 32 | entries taken of its pixel list (epoch-tagged: the call's first lane claims it);
+    // call_exh (pinned host memory): a call's id once its list ran out (the host's bound on
+    // calls in flight).  nullptr: an unchained call (its list is counts[4] of fresh_n).
+    uint32_t call_id;
+    unsigned long long *call_ring, *call_ctr;
+    uint32_t *call_exh;
     // the persistent wf_long's producers: finisher waves of its call not yet
     // past their last hand-off (nullptr: wf_long runs in host-kicked slices)
     uint32_t *fin_live;
@@ -1244,6 +1266,12 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_finish(RtDevScene sc, RtDevFrame 
 
 namespace {
 
+// a 4-byte load past the CU's L1 (global_load sc1: L2-served), for data another CU released
+__device__ __forceinline__ uint32_t ld_sc1(const uint32_t *p)
+{
+    return __hip_atomic_load(const_cast<uint32_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // fresh entry e of the whole-call finisher's pixel list -> its pixel: 256
 // entries per 16x16-pixel tile, 64 per 8x8-pixel wave tile (wf_start's
 // layout); false for a pixel outside the frame or in a row another shard owns
@@ -1319,6 +1347,8 @@ __global__ void __launch_bounds__(WF_BLOCK, WAVES) wf_finish_bvh(RtDevScene sc, 
     p.ro = p.rd = rt_v3(0, 0, 0);
     bool active = false, exhausted = false; // exhausted: this lane found the path list empty
     bool rel = false;                       // (fresh) the lane's pixel has no passes left: let it go
+    // (fresh) the wave's call: this launch's, then the chain's later issued calls
+    uint32_t cur = st.call_id, cur_passes = (uint32_t)fr.passes;
     unsigned long long idle_since = 0;      // (lane 0) when the wave first had nothing to do
     bool seated = false;                    // (lane 0) holds a linger seat
     while (true) {
@@ -1328,7 +1358,7 @@ __global__ void __launch_bounds__(WF_BLOCK, WAVES) wf_finish_bvh(RtDevScene sc, 
         // (fresh) pixels whose passes are done are let go — unless a later chained call queued
         // passes for them meanwhile: those run next, in the pixel's order (its state is this lane's)
         while (st.fresh && __any(rel)) {
-            if (st.concurrent) { // the pixel's stores visible before the word says it is free
+            if (WF_FIN_FENCE && st.concurrent) { // the pixel's stores visible before the word says it is free
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1417,58 +1447,105 @@ __global__ void __launch_bounds__(WF_BLOCK, WAVES) wf_finish_bvh(RtDevScene sc, 
             // this call's pixels (wf_start's work, in its 8x8-pixel wave tiles): a lane claims its
             // pixel (BUSY) unless another holder still has it — a previous chained call's finisher
             // lane or wf_long —, which then owes it this call's passes and runs them next
-            bool claim = !active && !exhausted && !rel, started = false;
+            bool claim = !active && !rel, started = false;
+            uint32_t my_passes = 0, my_call = 0;
+            exhausted = false;
             while (__any(claim)) {
                 const unsigned long long m = __ballot(claim);
                 const int leader = __ffsll((long long)m) - 1;
                 uint32_t base = 0;
-                if (lane == leader) base = atomicAdd(fetch, (uint32_t)__popcll(m));
+                int ok = 1;
+                if (lane == leader) {
+                    if (st.call_ctr) { // the wave's call's cursor, claimed for it by its first user
+                        unsigned long long *ctr = st.call_ctr + cur % WF_CALL_CURSORS;
+                        unsigned long long v = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        while ((uint32_t)(v >> 32) < cur &&
+                               !__hip_atomic_compare_exchange_strong(ctr, &v, (unsigned long long)cur << 32,
+                                                                     __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                                     __HIP_MEMORY_SCOPE_AGENT)) {
+                        }
+                        if ((uint32_t)(v >> 32) > cur) {
+                            ok = 0; // (a later call holds the slot: a wave 2^20 calls behind)
+                        } else {
+                            const unsigned long long o = __hip_atomic_fetch_add(
+                                ctr, (unsigned long long)__popcll(m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            base = (uint32_t)o;
+                            ok = (uint32_t)(o >> 32) == cur;
+                        }
+                    } else {
+                        base = atomicAdd(fetch, (uint32_t)__popcll(m));
+                    }
+                }
                 base = __shfl(base, leader);
-                bool acq = false;
+                ok = __shfl(ok, leader);
+                bool ran_out = false;
                 if (claim) {
                     const uint32_t e = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
                     int slot = 0;
-                    if (e >= n) {
-                        exhausted = true;
-                        claim = false;
+                    if (!ok || e >= n) {
+                        ran_out = true;
+                        if (st.call_exh && ok && e == n) // (the lane that ran the list out tells the host)
+                            __hip_atomic_store(st.call_exh + cur % WF_CALL_RING, cur, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_SYSTEM);
                     } else if (fresh_pixel(fr, e, slot)) {
                         uint32_t x = __hip_atomic_load(st.pxo + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         while (true) {
                             if (x & (RT_PX_OUT | RT_PX_BUSY)) { // held: owed this call's passes
-                                if (__hip_atomic_compare_exchange_strong(st.pxo + slot, &x, x + (uint32_t)fr.passes,
+                                if (__hip_atomic_compare_exchange_strong(st.pxo + slot, &x, x + cur_passes,
                                                                          __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                                          __HIP_MEMORY_SCOPE_AGENT))
                                     break;
                             } else if (__hip_atomic_compare_exchange_strong(st.pxo + slot, &x, RT_PX_BUSY,
                                                                             __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                                             __HIP_MEMORY_SCOPE_AGENT)) {
-                                acq = x != 0u; // (released by a possibly concurrent holder)
                                 claim = false;
                                 started = true;
+                                my_passes = cur_passes;
+                                my_call = cur;
                                 p.slot = (uint32_t)slot;
                                 break;
                             }
                         }
                     }
                 }
-                if (__any(acq)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                if (__any(ran_out)) {
+                    // the wave's call has run its list out: on to the chain's next call if it is issued
+                    uint32_t nxt = 0;
+                    if (lane == 0 && st.call_ring) {
+                        const unsigned long long v = __hip_atomic_load(st.call_ring + (cur + 1u) % WF_CALL_RING,
+                                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        if ((uint32_t)(v >> 32) == cur + 1u) nxt = (uint32_t)v | 0x80000000u;
+                    }
+                    nxt = (uint32_t)__builtin_amdgcn_readfirstlane((int)nxt);
+                    if (nxt) {
+                        ++cur;
+                        cur_passes = nxt & 0x7FFFFFFFu;
+                    } else if (ran_out) {
+                        claim = false;
+                        exhausted = true;
+                    }
+                }
             }
-            if (started) { // the pixel's state (after the acquire), and its first pass (wf_start's)
+            if (started) { // the pixel's state and its first pass (wf_start's)
+                // (its last holder may have been a concurrent finisher or wf_long, which released
+                // its stores before the word said free: read them past this CU's L1 — sc1 loads —
+                // instead of an acquire, which would drop every wave's L1 lines on the CU)
                 const uint32_t slot = p.slot;
-                p.rng = fr.rng[slot];
+                p.rng = ld_sc1(fr.rng + slot);
                 Vec3D fb = rt_v3(0.0f, 0.0f, 0.0f);
                 float sq = 0.0f;
                 int count = 0;
-                if (fr.reset) { // reset_frame (rt/render.cuh:18-34)
+                if (fr.reset && my_call == st.call_id) { // reset_frame (rt/render.cuh:18-34)
                     fr.fb[slot] = fb;
                     fr.sq[slot] = sq;
                     fr.count[slot] = count;
                 } else {
-                    fb = fr.fb[slot];
-                    sq = fr.sq[slot];
-                    count = fr.count[slot];
+                    const uint32_t *f3 = reinterpret_cast<const uint32_t *>(fr.fb + slot);
+                    fb = rt_v3(__uint_as_float(ld_sc1(f3)), __uint_as_float(ld_sc1(f3 + 1)), __uint_as_float(ld_sc1(f3 + 2)));
+                    sq = __uint_as_float(ld_sc1(reinterpret_cast<const uint32_t *>(fr.sq + slot)));
+                    count = (int)ld_sc1(reinterpret_cast<const uint32_t *>(fr.count + slot));
                 }
-                p.passes_left = fr.passes;
+                p.passes_left = (int)my_passes;
                 if (start_sample<COUNT>(fr, cam, (int)slot, p.passes_left, p.rng, fb, sq, count, p.ro, p.rd, c)) {
                     begin_path(p);
                     active = true;
@@ -2161,6 +2238,15 @@ struct Workspace {
     int cus = 0;                                // compute units of the device (the finisher's grid)
     unsigned long long *long_log_buf = nullptr; // RT_DEBUG_LONG_LOG records
     int fin_flip = 0; // the next chained call's finisher runs on pipeline 2 (1) or 0 (0)
+    // chained calls (WfState.call_ring): the issued calls' descriptors and the lists that ran out
+    // (pinned host memory, WF_CALL_RING each), the epoch-tagged list cursors (device), the open
+    // chain's first call id, and per call slot the event after its launch
+    unsigned long long *call_ring = nullptr;
+    uint32_t *call_exh = nullptr;
+    unsigned long long *call_ctr = nullptr;
+    uint32_t chain_first = 0;
+    hipEvent_t call_ev[WF_CALL_RING] = {};
+    bool call_ev_rec[WF_CALL_RING] = {};
     // RtOptions.profile of whole calls: per profiled call its finisher's span on the device
     // ({first wave start, last wave end}, s_memrealtime) in a ring of WF_PROF_SLOTS, resolved
     // into RtProfile records by rt_last_profile / rt_profile_history (they join first)
@@ -2210,6 +2296,17 @@ int ensure_streams(Workspace &w, int npipes)
         if (hipEventCreate(&w.ev0) != hipSuccess || hipEventCreate(&w.ev1) != hipSuccess) return -1;
         if (hipMalloc((void **)&w.verify_res, 64) != hipSuccess || hipMemset(w.verify_res, 0, 64) != hipSuccess)
             return -1;
+        // chained calls: descriptors and ran-out marks in pinned host memory (the host writes the
+        // one, the device the other, both while kernels run), the list cursors on the device
+        if (hipHostMalloc((void **)&w.call_ring, WF_CALL_RING * 8, hipHostMallocCoherent) != hipSuccess ||
+            hipHostMalloc((void **)&w.call_exh, WF_CALL_RING * 4, hipHostMallocCoherent) != hipSuccess ||
+            hipMalloc((void **)&w.call_ctr, (size_t)WF_CALL_CURSORS * 8) != hipSuccess ||
+            hipMemset(w.call_ctr, 0, (size_t)WF_CALL_CURSORS * 8) != hipSuccess)
+            return -1;
+        memset(w.call_ring, 0, WF_CALL_RING * 8);
+        memset(w.call_exh, 0, WF_CALL_RING * 4);
+        for (auto &e : w.call_ev)
+            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return -1;
         w.streams_ok = true;
     }
     for (int i = 0; i < npipes && i < WF_MAX_PIPES; ++i) {
@@ -2261,9 +2358,12 @@ int resolve_profiles(Workspace &w)
     std::vector<unsigned long long> sp(2 * WF_PROF_SLOTS);
     if (hipMemcpy(sp.data(), w.spans, sp.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
         return -1;
+    unsigned long long base = ~0ull; // (start_ms: relative to the earliest finisher start of the batch)
+    for (const auto &q : w.prof_pending) base = std::min(base, sp[2 * (q.seq % WF_PROF_SLOTS)]);
     for (const auto &q : w.prof_pending) {
         const unsigned long long a = sp[2 * (q.seq % WF_PROF_SLOTS)], b = sp[2 * (q.seq % WF_PROF_SLOTS) + 1];
         RtProfile P{};
+        P.start_ms = b > a ? (float)((double)(a - base) * 1e-5) : 0.0f;
         P.finish_launches = 1;
         P.pipelines = 1;
         P.finish_ms = b > a ? (float)((double)(b - a) * 1e-5) : 0.0f; // (s_memrealtime: 100 MHz)
@@ -2362,6 +2462,9 @@ int ensure(Workspace &w, size_t slots, int grid, int npipes)
         st.concurrent = 0;
         st.fresh_n = 0;
         st.span = nullptr;
+        st.call_id = 0;
+        st.call_ring = st.call_ctr = nullptr;
+        st.call_exh = nullptr;
         st.chk = nullptr; // (whole-call mode only: launch_whole)
         st.chk_ctr = nullptr;
         st.chk_mask = 0;
@@ -2467,7 +2570,7 @@ int launch_whole(Workspace &w, int dev, const RtDevScene &sc, const RtDevFrame &
     // the finisher's stream: chained calls alternate between pipelines 0 and 2 (the
     // previous finisher's tail and this one's bulk share the chip); its counters, its
     // stack spill area and its guard records go with it
-    const int fpi = w.fin_flip ? 2 : 0;
+    const int fpi = WF_FIN_ALT && w.fin_flip ? 2 : 0;
     w.fin_flip ^= overlap ? 1 : 0;
     Pipe &pp = w.pipe[fpi];
     WfState st = pp.st;
@@ -2504,6 +2607,32 @@ int launch_whole(Workspace &w, int dev, const RtDevScene &sc, const RtDevFrame &
     fgrid = fgrid > fmax ? fmax : fgrid;
     const uint32_t k = (uint32_t)(w.call_seq % 8);
     st.fin_live = long_return ? w.fin_live + k : nullptr;
+    st.call_id = (uint32_t)w.call_seq + 1u;
+    st.call_ring = st.call_ctr = nullptr;
+    st.call_exh = nullptr;
+    if (overlap) {
+        // issue the call: lanes of the chain's running finishers may take its pixels from now on.
+        // (Bound: the call WF_CALLS_IN_FLIGHT before it has run its list out, so no cursor slot
+        // is still in use by a call WF_CALL_RING before.)
+        if (!chained) w.chain_first = st.call_id;
+        const uint32_t old = st.call_id - WF_CALLS_IN_FLIGHT;
+        if (chained && st.call_id > WF_CALLS_IN_FLIGHT && old >= w.chain_first) {
+            const int oi = (int)(old % WF_CALL_RING);
+            while (__atomic_load_n(w.call_exh + oi, __ATOMIC_ACQUIRE) != old) {
+                if (w.call_ev_rec[oi]) {
+                    const hipError_t q = hipEventQuery(w.call_ev[oi]);
+                    if (q == hipSuccess) break; // (its launch ended: every list it could take ran out)
+                    if (q != hipErrorNotReady) return -1;
+                }
+                std::this_thread::sleep_for(std::chrono::microseconds(20));
+            }
+        }
+        st.call_ring = w.call_ring;
+        st.call_ctr = w.call_ctr;
+        st.call_exh = w.call_exh;
+        __atomic_store_n(w.call_ring + st.call_id % WF_CALL_RING,
+                         (unsigned long long)st.call_id << 32 | (uint32_t)fr.passes, __ATOMIC_RELEASE);
+    }
     if (!chained) {
         // the hand-off state from zero (nothing of it is in flight now)
         if (long_return) {
@@ -2539,6 +2668,11 @@ int launch_whole(Workspace &w, int dev, const RtDevScene &sc, const RtDevFrame &
         hipLaunchKernelGGL((wf_finish_bvh<false, 1>), dim3(fgrid), dim3(WF_BLOCK), 0, s, sc, fr, cam, st, 0);
     else hipLaunchKernelGGL(wf_finish_bvh<false>, dim3(fgrid), dim3(WF_BLOCK), 0, s, sc, fr, cam, st, 0);
     if (hipGetLastError() != hipSuccess) return -1;
+    if (overlap) {
+        const int ci = (int)(st.call_id % WF_CALL_RING);
+        if (hipEventRecord(w.call_ev[ci], s) != hipSuccess) return -1;
+        w.call_ev_rec[ci] = true;
+    }
     Pipe *lp = nullptr;
     if (long_return) {
         lp = &w.pipe[1];
@@ -2780,8 +2914,13 @@ void rt_wavefront_shutdown()
         if (w->blob) (void)launch_drain(*w); // (an open chain's wf_longs leave only after its drain)
         (void)hipDeviceSynchronize();
         if (w->blob) (void)hipFree(w->blob);
-        for (void *p : {(void *)w->chk, (void *)w->verify_res, (void *)w->long_log_buf, (void *)w->spans})
+        for (void *p : {(void *)w->chk, (void *)w->verify_res, (void *)w->long_log_buf, (void *)w->spans,
+                        (void *)w->call_ctr})
             if (p) (void)hipFree(p);
+        for (void *p : {(void *)w->call_ring, (void *)w->call_exh})
+            if (p) (void)hipHostFree(p);
+        for (hipEvent_t e : w->call_ev)
+            if (e) (void)hipEventDestroy(e);
         for (int i = WF_MAX_PIPES - 1; i >= 0; --i) {
             Pipe &p = w->pipe[i];
             for (auto &e : p.ev)
