@@ -470,7 +470,8 @@ typedef struct RtOptions {
      * long-path kernel running a deep glass path of 10^4+ bounces) are owed
      * the passes and run them before they are let go.  Every pixel's passes
      * run in the reference's order, so the frame is bit-identical to
-     * unchained calls.  Whatever reads the frame in
+     * unchained calls.  A call with sample_count 0 (reset_frame) is never
+     * chained: it completes before the next call starts.  Whatever reads the frame in
      * between must join first: rt_join(stream), rt_synchronize, or the
      * library's own readers (rt_tonemap, rt_save_render, rt_gbuffer_save,
      * rt_reduce_shards, rt_deviation_stats), which join by themselves.  A

@@ -104,11 +104,20 @@ static_assert(WF_BLOCK % WF_TBLOCK == 0 && WF_TBLOCK % 64 == 0, "WF_TBLOCK must 
 #define WF_CALL_CURSORS (1u << 20) // their pixel-list cursors (call id % WF_CALL_CURSORS, epoch-tagged): a
                                    // wave would have to lag 2^20 calls behind to meet a reused one
 #define WF_CALLS_IN_FLIGHT 8 // a call is issued once the call this many before it has run its list out
-#ifndef WF_FIN_FENCE
-#define WF_FIN_FENCE 1 // (A/B only: 0 drops the release fence of pixels let go beside a concurrent finisher)
+#ifndef WF_FIN_CONTINUE
+// chained calls: 0 = their finishers run one after the other on pipeline 0 (a kernel boundary
+// between calls: a pixel's state crosses it for free); 1 = a finisher goes on with the chain's
+// next issued calls (no tail between calls, but every pixel let go needs an agent-scope release,
+// and a claimer on another XCD may share the pixel's cache lines with a third: measured slower
+// and, with write-through publication, not exact — profiles/r05/overlap_ab.md)
+#define WF_FIN_CONTINUE 0
+#endif
+#ifndef WF_FIN_PUBLISH
+#define WF_FIN_PUBLISH 0 // (WF_FIN_CONTINUE) a pixel let go: 0 = release fence; 1 = state re-stored write-through
 #endif
 #ifndef WF_FIN_ALT
-#define WF_FIN_ALT 1 // chained finishers alternate between pipelines 0 and 2 (0: all on pipeline 0)
+#define WF_FIN_ALT 0 // chained finishers alternate between pipelines 0 and 2 (0: all on pipeline 0 — the
+                     // running one takes the later calls' pixels; a second one beside it competes for them)
 #endif
 #ifndef WF_FIN_SMALL_WAVES
 #define WF_FIN_SMALL_WAVES 3 // frames of at most this many finisher waves per SIMD take the unspilled build (151 VGPRs: 3 waves)
@@ -1272,6 +1281,12 @@ __device__ __forceinline__ uint32_t ld_sc1(const uint32_t *p)
     return __hip_atomic_load(const_cast<uint32_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// a 4-byte write-through store (global_store sc1), for data another CU will read
+__device__ __forceinline__ void st_sc1(uint32_t *p, uint32_t v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // fresh entry e of the whole-call finisher's pixel list -> its pixel: 256
 // entries per 16x16-pixel tile, 64 per 8x8-pixel wave tile (wf_start's
 // layout); false for a pixel outside the frame or in a row another shard owns
@@ -1358,12 +1373,29 @@ __global__ void __launch_bounds__(WF_BLOCK, WAVES) wf_finish_bvh(RtDevScene sc, 
         // (fresh) pixels whose passes are done are let go — unless a later chained call queued
         // passes for them meanwhile: those run next, in the pixel's order (its state is this lane's)
         while (st.fresh && __any(rel)) {
-            if (WF_FIN_FENCE && st.concurrent) { // the pixel's stores visible before the word says it is free
+            if (!WF_FIN_PUBLISH && st.concurrent) { // (A/B: every dirty line of the XCD's L2 written back)
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
             if (rel) {
+                if (WF_FIN_PUBLISH && st.concurrent) {
+                    // the pixel's state — its 24 bytes, all a later claimer reads (with sc1 loads) —
+                    // re-stored write-through (sc1) and drained before the word says it is free: a
+                    // claimer on another XCD reads them from memory, without a write-back of the
+                    // whole L2 (MI355X_MICROARCH.md, visibility: sc1 payload, drained, atomic flag)
+                    uint32_t *f3 = reinterpret_cast<uint32_t *>(fr.fb + p.slot);
+                    const uint32_t a0 = f3[0], a1 = f3[1], a2 = f3[2];
+                    const uint32_t sqb = *reinterpret_cast<const uint32_t *>(fr.sq + p.slot);
+                    const uint32_t cnb = *reinterpret_cast<const uint32_t *>(fr.count + p.slot);
+                    st_sc1(f3, a0);
+                    st_sc1(f3 + 1, a1);
+                    st_sc1(f3 + 2, a2);
+                    st_sc1(reinterpret_cast<uint32_t *>(fr.sq + p.slot), sqb);
+                    st_sc1(reinterpret_cast<uint32_t *>(fr.count + p.slot), cnb);
+                    st_sc1(fr.rng + p.slot, p.rng);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
                 uint32_t x = RT_PX_BUSY;
                 if (__hip_atomic_compare_exchange_strong(st.pxo + p.slot, &x, st.concurrent ? RT_PX_REL : 0u,
                                                          __ATOMIC_RELAXED, __ATOMIC_RELAXED,
@@ -2238,6 +2270,10 @@ struct Workspace {
     int cus = 0;                                // compute units of the device (the finisher's grid)
     unsigned long long *long_log_buf = nullptr; // RT_DEBUG_LONG_LOG records
     int fin_flip = 0; // the next chained call's finisher runs on pipeline 2 (1) or 0 (0)
+    // the guard's wf_check per record parity on pipeline 2 (!WF_FIN_ALT): the event after it (the
+    // call two later, whose finisher writes the same records, waits for it)
+    hipEvent_t chk_done[2] = {};
+    bool chk_rec[2] = {false, false};
     // chained calls (WfState.call_ring): the issued calls' descriptors and the lists that ran out
     // (pinned host memory, WF_CALL_RING each), the epoch-tagged list cursors (device), the open
     // chain's first call id, and per call slot the event after its launch
@@ -2306,6 +2342,8 @@ int ensure_streams(Workspace &w, int npipes)
         memset(w.call_ring, 0, WF_CALL_RING * 8);
         memset(w.call_exh, 0, WF_CALL_RING * 4);
         for (auto &e : w.call_ev)
+            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return -1;
+        for (auto &e : w.chk_done)
             if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return -1;
         w.streams_ok = true;
     }
@@ -2534,6 +2572,9 @@ int launch_whole(Workspace &w, int dev, const RtDevScene &sc, const RtDevFrame &
                  bool count)
 {
     const size_t slots = (size_t)fr.width * fr.height;
+    // a resetting call (sample_count 0) neither continues nor opens a chain: its reset of a pixel
+    // must come before any later pass, and a chained lane may reach a pixel before it does
+    overlap = overlap && !fr.reset;
     // every wave slot at the finisher's occupancy (MI355X: 256 CUs x 4 SIMDs x 5 waves / 4 waves per
     // block = 1,280 blocks), the last WF_LONG_BLOCKS of them left to wf_long
     if (!w.cus) {
@@ -2578,11 +2619,12 @@ int launch_whole(Workspace &w, int dev, const RtDevScene &sc, const RtDevFrame &
     st.long_depth = long_depth;
     st.long_return = long_return;
     st.fresh = 1;
-    st.concurrent = overlap ? 1 : 0;
+    st.concurrent = overlap && WF_FIN_CONTINUE ? 1 : 0;
     st.fresh_n = (uint32_t)(((fr.width + 15) / 16) * ((fr.height + 15) / 16)) * 256u;
     st.linger = overlap ? 0ull : WF_FIN_LINGER;
     st.chk_mask = check_mask;
-    const int par = fpi / 2;
+    // the guard's records per call parity (WF_FIN_ALT: per finisher stream, its wf_check behind it)
+    const int par = WF_FIN_ALT ? fpi / 2 : (int)(w.call_seq & 1);
     // (the guard's records: allocated by the first call that samples rays)
     if (check_mask != 0xFFFFFFFFu && !w.chk &&
         hipMalloc((void **)&w.chk, 2 * (size_t)WF_CHECK_CAP * 3 * sizeof(RtF4)) != hipSuccess) {
@@ -2610,7 +2652,7 @@ int launch_whole(Workspace &w, int dev, const RtDevScene &sc, const RtDevFrame &
     st.call_id = (uint32_t)w.call_seq + 1u;
     st.call_ring = st.call_ctr = nullptr;
     st.call_exh = nullptr;
-    if (overlap) {
+    if (overlap && WF_FIN_CONTINUE) {
         // issue the call: lanes of the chain's running finishers may take its pixels from now on.
         // (Bound: the call WF_CALLS_IN_FLIGHT before it has run its list out, so no cursor slot
         // is still in use by a call WF_CALL_RING before.)
@@ -2652,7 +2694,10 @@ int launch_whole(Workspace &w, int dev, const RtDevScene &sc, const RtDevFrame &
     if (hipMemsetAsync(st.counts, 0, 256, s) != hipSuccess) return -1;
     if (st.fin_live && hipMemsetD32Async((hipDeviceptr_t)st.fin_live, (int)(fgrid * (WF_BLOCK / 64)), 1, s) != hipSuccess)
         return -1;
-    if (st.chk && hipMemsetAsync(st.chk_ctr, 0, 4, s) != hipSuccess) return -1; // (its last wf_check is behind on s)
+    if (st.chk) { // (this parity's records: after the wf_check that last read them)
+        if (!WF_FIN_ALT && w.chk_rec[par] && hipStreamWaitEvent(s, w.chk_done[par], 0) != hipSuccess) return -1;
+        if (hipMemsetAsync(st.chk_ctr, 0, 4, s) != hipSuccess) return -1;
+    }
     if (long_return && hipMemsetD32Async((hipDeviceptr_t)st.chain_flag, overlap ? 1 : 0, 1, s) != hipSuccess) return -1;
     // RtOptions.profile: the finisher's span on the device (first wave start, last wave end)
     st.span = nullptr;
@@ -2682,12 +2727,27 @@ int launch_whole(Workspace &w, int dev, const RtDevScene &sc, const RtDevFrame &
         if (hipEventRecord(lp->long_done, lp->stream) != hipSuccess) return -1;
         lp->long_rec = true;
     }
-    if (st.chk) {
+    if (st.chk && WF_FIN_ALT) {
         // the guard's re-traces after the finisher on its stream (its KD stacks in the finisher's
         // spill area), beside the next chained call's finisher: latency-bound single-lane KD
         // traversals, 256 blocks
         hipLaunchKernelGGL(wf_check, dim3(WF_CHECK_BLOCKS), dim3(WF_BLOCK), 0, s, sc, st, fr.dev_stats);
         if (hipGetLastError() != hipSuccess) return -1;
+    } else if (st.chk) {
+        // ... on pipeline 2's stream after the finisher, beside whatever follows it on pipeline 0
+        // (the next call's finisher, a chain's drain); its KD stacks in pipeline 2's spill area
+        Pipe &cp = w.pipe[2];
+        WfState cs = st;
+        cs.spill = cp.st.spill;
+        if (!cs.spill) return -1;
+        if (hipEventRecord(pp.fin_done, s) != hipSuccess || hipStreamWaitEvent(cp.stream, pp.fin_done, 0) != hipSuccess)
+            return -1;
+        hipLaunchKernelGGL(wf_check, dim3(WF_CHECK_BLOCKS), dim3(WF_BLOCK), 0, cp.stream, sc, cs, fr.dev_stats);
+        if (hipGetLastError() != hipSuccess) return -1;
+        if (hipEventRecord(w.chk_done[par], cp.stream) != hipSuccess || hipEventRecord(cp.join, cp.stream) != hipSuccess)
+            return -1;
+        w.chk_rec[par] = true;
+        cp.joined = true;
     }
     if (hipEventRecord(pp.join, s) != hipSuccess) return -1;
     pp.joined = true;
@@ -2757,7 +2817,7 @@ int launch_drain(Workspace &w)
     st.fin_live = w.fin_live + (uint32_t)(w.call_seq % 8);
     ++w.call_seq;
     const hipStream_t s = pp.stream;
-    if (w.pipe[2].joined && hipStreamWaitEvent(s, w.pipe[2].join, 0) != hipSuccess) return -1;
+    if (WF_FIN_ALT && w.pipe[2].joined && hipStreamWaitEvent(s, w.pipe[2].join, 0) != hipSuccess) return -1;
     // no pixels (counts[4] = 0 of fresh_n 0), no linger seat taken yet
     if (hipMemsetAsync(st.counts, 0, 256, s) != hipSuccess) return -1;
     if (hipMemsetAsync(st.ret_ctr + 4, 0, 4, s) != hipSuccess) return -1;
@@ -2931,7 +2991,7 @@ void rt_wavefront_shutdown()
             if (p.host_count) (void)hipHostFree(p.host_count);
             if (p.stream) (void)hipStreamDestroy(p.stream);
         }
-        for (hipEvent_t e : {w->ev1, w->ev0, w->long_ev, w->fin_ready, w->fork})
+        for (hipEvent_t e : {w->chk_done[1], w->chk_done[0], w->ev1, w->ev0, w->long_ev, w->fin_ready, w->fork})
             if (e) (void)hipEventDestroy(e);
         delete w;
         kv.second = nullptr;
