@@ -175,14 +175,35 @@ __device__ __forceinline__ float bvh_bound(const RtDevScene &sc, Vec3D o, Vec3D 
 #ifndef RT_BVH4
 #define RT_BVH4 1 // trace_bvh's s_min query on the 4-wide collapse (0: the binary tree)
 #endif
-template <bool COUNT, typename STACK>
-__device__ __forceinline__ float bvh4_bound(const RtDevScene &sc, Vec3D o, Vec3D d, float best, STACK &stk, Cnt &cn)
+//
+// The query's state between two node steps is (cur, sp, best) plus the stack
+// (LDS / spill area): PARK stops the query before its cap-th node step and
+// hands that state back (returns false), and a later call with resume picks
+// it up where it stopped — the same visiting order, the same s_min.  The
+// whole-call finisher parks a lane's long query so that the rest of its wave
+// goes on with shading instead of waiting for that one lane (wf_finish_bvh).
+struct BvhPark {
+    uint32_t cur;
+    int sp;
+    float best;
+};
+
+template <bool COUNT, bool PARK, typename STACK>
+__device__ __forceinline__ bool bvh4_query(const RtDevScene &sc, Vec3D o, Vec3D d, float best0, STACK &stk, Cnt &cn,
+                                           int cap, bool resume, BvhPark &pk)
 {
     const float m = rt_ray_margin(o.x, o.y, o.z, sc.bvh_scale);
     const Vec3D om = rt_v3(o.x + m, o.y + m, o.z + m), op = rt_v3(o.x - m, o.y - m, o.z - m);
     const Vec3D inv = rt_v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     int sp = 0;
     uint32_t cur = 0; // the root (always an inner node)
+    float best = best0;
+    if (PARK && resume) {
+        sp = pk.sp;
+        cur = pk.cur;
+        best = pk.best;
+    }
+    int steps = 0;
     auto pop = [&]() -> uint32_t {
         while (sp > 0) {
             --sp;
@@ -195,6 +216,15 @@ __device__ __forceinline__ float bvh4_bound(const RtDevScene &sc, Vec3D o, Vec3D
     };
     while (true) {
         while (!(cur & RT_BVH_LEAF)) {
+            if (PARK) {
+                if (steps >= cap) {
+                    pk.cur = cur;
+                    pk.sp = sp;
+                    pk.best = best;
+                    return false;
+                }
+                ++steps;
+            }
             if (COUNT) cn.v[RT_CNT_B_BVH_NODE]++;
             const RtF4 *nd = sc.bvh4 + 8 * (size_t)cur;
             const RtF4 lx = ldc4(nd), ly = ldc4(nd + 1), lz = ldc4(nd + 2), hx = ldc4(nd + 3), hy = ldc4(nd + 4),
@@ -247,35 +277,34 @@ __device__ __forceinline__ float bvh4_bound(const RtDevScene &sc, Vec3D o, Vec3D
             }
             cur = r0 != RT_BVH_EMPTY ? r0 : pop();
         }
-        if (cur == RT_BVH_EMPTY) return best;
+        if (cur == RT_BVH_EMPTY) break;
         const uint32_t first = (cur & ~RT_BVH_LEAF) >> 3, end = first + (cur & 7u) + 1u;
         if (COUNT) cn.v[RT_CNT_B_BVH_TRI] += end - first;
         float bx, by, bz;
         (void)leaf_scan<COUNT>(sc.bvh_a, sc.bvh_bary, first, end, o, d, best, bx, by, bz, cn);
         cur = pop();
-        if (cur == RT_BVH_EMPTY) return best;
+        if (cur == RT_BVH_EMPTY) break;
     }
+    pk.best = best;
+    return true;
 }
 
-// trace_ray with the bound: returns the triangle index or -1 and the hit's
-// barycentric coordinates, bit-identical to trace().  COUNT (RT_TRAVERSAL_
-// BOUNDED_COUNTED): this traversal's own work — RT_CNT_RAY, RT_CNT_NODE / _TRI
-// (KD nodes / plane tests), RT_CNT_B_* (BVH nodes / plane tests, barycentric
-// records of both phases)
 template <bool COUNT, typename STACK>
-__device__ __forceinline__ int trace_bvh(const RtDevScene &sc, const Vec3D o, const Vec3D d, float &hbx, float &hby,
-                                         float &hbz, STACK &stk, Cnt &c)
+__device__ __forceinline__ float bvh4_bound(const RtDevScene &sc, Vec3D o, Vec3D d, float best, STACK &stk, Cnt &cn)
 {
-    if (COUNT) c.v[RT_CNT_RAY]++;
-    float entry, exit_;
-    if (!bbox_hit(sc, o, d, entry, exit_)) return -1;
-    const float root_exit = exit_;
-    float s_min = -INFINITY; // (the plain KD traversal)
-    if (rt_bounded_ray(o, d, sc.split_vals, sc.split_off)) {
-        s_min = RT_BVH4 ? bvh4_bound<COUNT>(sc, o, d, exit_, stk, c) : bvh_bound<COUNT>(sc, o, d, exit_, stk, c);
-        RT_PHASE_MID();
-        if (!(s_min < root_exit)) return -1;
-    }
+    BvhPark pk;
+    (void)bvh4_query<COUNT, false>(sc, o, d, best, stk, cn, 0, false, pk);
+    return pk.best;
+}
+
+// step 3: the reference's KD traversal with the skip bound s_min (-inf: the
+// plain traversal), from the scene box's [entry, root_exit]
+template <bool COUNT, typename STACK>
+__device__ __forceinline__ int kd_bounded(const RtDevScene &sc, const Vec3D o, const Vec3D d, float entry,
+                                          const float root_exit, const float s_min, float &hbx, float &hby, float &hbz,
+                                          STACK &stk, Cnt &c)
+{
+    float exit_ = root_exit;
     const float yx = rt_recip_guard(d.x), yy = rt_recip_guard(d.y), yz = rt_recip_guard(d.z);
     int sp = 0;
     uint32_t node = 0;
@@ -332,6 +361,53 @@ __device__ __forceinline__ int trace_bvh(const RtDevScene &sc, const Vec3D o, co
         entry = stk.entry_at(sp);
         exit_ = sp > 0 ? stk.entry_at(sp - 1) : root_exit;
     }
+}
+
+
+// trace_ray with the bound: returns the triangle index or -1 and the hit's
+// barycentric coordinates, bit-identical to trace().  COUNT (RT_TRAVERSAL_
+// BOUNDED_COUNTED): this traversal's own work — RT_CNT_RAY, RT_CNT_NODE / _TRI
+// (KD nodes / plane tests), RT_CNT_B_* (BVH nodes / plane tests, barycentric
+// records of both phases)
+template <bool COUNT, typename STACK>
+__device__ __forceinline__ int trace_bvh(const RtDevScene &sc, const Vec3D o, const Vec3D d, float &hbx, float &hby,
+                                         float &hbz, STACK &stk, Cnt &c)
+{
+    if (COUNT) c.v[RT_CNT_RAY]++;
+    float entry, exit_;
+    if (!bbox_hit(sc, o, d, entry, exit_)) return -1;
+    const float root_exit = exit_;
+    float s_min = -INFINITY; // (the plain KD traversal)
+    if (rt_bounded_ray(o, d, sc.split_vals, sc.split_off)) {
+        s_min = RT_BVH4 ? bvh4_bound<COUNT>(sc, o, d, exit_, stk, c) : bvh_bound<COUNT>(sc, o, d, exit_, stk, c);
+        RT_PHASE_MID();
+        if (!(s_min < root_exit)) return -1;
+    }
+    return kd_bounded<COUNT>(sc, o, d, entry, root_exit, s_min, hbx, hby, hbz, stk, c);
+}
+
+// trace_bvh with the s_min query parked after `cap` node steps (bvh4_query):
+// false = parked (pk holds the query's state; call again with resume), true =
+// done with the hit in `hit` (-1: miss) — trace_bvh's result, bit for bit
+template <bool COUNT, typename STACK>
+__device__ __forceinline__ bool trace_bvh_park(const RtDevScene &sc, const Vec3D o, const Vec3D d, int &hit, float &hbx,
+                                               float &hby, float &hbz, STACK &stk, Cnt &c, int cap, bool resume,
+                                               BvhPark &pk)
+{
+    if (COUNT && !resume) c.v[RT_CNT_RAY]++;
+    hit = -1;
+    float entry, exit_;
+    if (!bbox_hit(sc, o, d, entry, exit_)) return true;
+    const float root_exit = exit_;
+    float s_min = -INFINITY; // (the plain KD traversal)
+    if (rt_bounded_ray(o, d, sc.split_vals, sc.split_off)) {
+        if (!bvh4_query<COUNT, true>(sc, o, d, exit_, stk, c, cap, resume, pk)) return false;
+        s_min = pk.best;
+        RT_PHASE_MID();
+        if (!(s_min < root_exit)) return true;
+    }
+    hit = kd_bounded<COUNT>(sc, o, d, entry, root_exit, s_min, hbx, hby, hbz, stk, c);
+    return true;
 }
 
 } // namespace rtk

@@ -99,6 +99,64 @@ __device__ __forceinline__ bool bbox_hit(const RtDevScene &sc, Vec3D o, Vec3D d,
     return t1 <= t2;
 }
 
+// The same stack addressed from a wave-uniform base plus the lane id (v_mbcnt,
+// recomputed where it is used): no per-lane base address has to stay live —
+// or be spilled — across a long loop around the traversal.
+// the lane id, computed where it is used (volatile: not hoisted into a register that lives across the loop)
+__device__ __forceinline__ int lane_id_here()
+{
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
+
+template <int LDS_DEPTH>
+struct LaneStack {
+    uint32_t *lds_node; // wave-uniform: this wave's column 0
+    float *lds_entry;
+    int stride;
+    uint2 *spill; // wave-uniform
+    int spill_stride;
+    __device__ __forceinline__ void put(int k, uint32_t node, float t)
+    {
+        const int l = lane_id_here();
+        if (k < LDS_DEPTH) {
+            lds_node[k * stride + l] = node;
+            lds_entry[k * stride + l] = t;
+        } else {
+            spill[(size_t)(k - LDS_DEPTH) * spill_stride + l] = make_uint2(node, __float_as_uint(t));
+        }
+    }
+    __device__ __forceinline__ void get(int k, uint32_t &node, float &entry) const
+    {
+        const int l = lane_id_here();
+        if (k < LDS_DEPTH) {
+            node = lds_node[k * stride + l];
+            entry = lds_entry[k * stride + l];
+        } else {
+            unsigned long long *p =
+                reinterpret_cast<unsigned long long *>(spill + (size_t)(k - LDS_DEPTH) * spill_stride + l);
+            const unsigned long long v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+            node = (uint32_t)v;
+            entry = __uint_as_float((uint32_t)(v >> 32));
+        }
+    }
+    __device__ __forceinline__ uint32_t node_at(int k) const
+    {
+        uint32_t n;
+        float e;
+        get(k, n, e);
+        return n;
+    }
+    __device__ __forceinline__ float entry_at(int k) const
+    {
+        uint32_t n;
+        float e;
+        get(k, n, e);
+        return e;
+    }
+};
+
 // Traversal stack of (node, entry t).  Entries [0, LDS_DEPTH) live in LDS at
 // lds[k * stride]; deeper ones (rare) in a per-thread global spill area at
 // spill[(k - LDS_DEPTH) * spill_stride].  The exit t of an entry equals the

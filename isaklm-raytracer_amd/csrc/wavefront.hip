@@ -97,6 +97,9 @@ static_assert(WF_BLOCK % WF_TBLOCK == 0 && WF_TBLOCK % 64 == 0, "WF_TBLOCK must 
 #ifndef WF_CHECK_BLOCKS
 #define WF_CHECK_BLOCKS 256 // wf_check's grid (it runs beside the next call's finisher)
 #endif
+#ifndef WF_BVH_PARK
+#define WF_BVH_PARK 8 // wf_finish_bvh: BVH node steps per loop trip before a lane's query parks (0: never)
+#endif
 #ifndef WF_FIN_BVH_WAVES
 #define WF_FIN_BVH_WAVES 5 // wf_finish_bvh occupancy target (5: +3 % over 6 with the 4-wide s_min query, profiles/r04)
 #endif
@@ -1334,8 +1337,9 @@ __global__ void __launch_bounds__(WF_BLOCK, WAVES) wf_finish_bvh(RtDevScene sc, 
     __shared__ uint32_t s_node[WF_BVH_LDS * WF_BLOCK];
     __shared__ float s_entry[WF_BVH_LDS * WF_BLOCK];
     const int tid = threadIdx.x;
-    const int gtid = blockIdx.x * WF_BLOCK + tid;
-    Stack<WF_BVH_LDS> stk{s_node + tid, s_entry + tid, WF_BLOCK, st.spill + gtid, st.spill_threads};
+    const int wbase = __builtin_amdgcn_readfirstlane(tid & ~63); // (wave-uniform)
+    LaneStack<WF_BVH_LDS> stk{s_node + wbase, s_entry + wbase, WF_BLOCK, st.spill + (blockIdx.x * WF_BLOCK + wbase),
+                              st.spill_threads};
     Cnt c;
     if (COUNT) c.zero();
     // fresh: this call's pixels, 256 entries per 16x16-pixel tile (fresh_pixel); else the paths of path list q
@@ -1366,6 +1370,14 @@ __global__ void __launch_bounds__(WF_BLOCK, WAVES) wf_finish_bvh(RtDevScene sc, 
     uint32_t cur = st.call_id, cur_passes = (uint32_t)fr.passes;
     unsigned long long idle_since = 0;      // (lane 0) when the wave first had nothing to do
     bool seated = false;                    // (lane 0) holds a linger seat
+#if WF_BVH_PARK
+    // a lane whose s_min query ran WF_BVH_PARK node steps parks it (its state in LDS, the stack in
+    // place) and resumes it in the wave's next loop trip: the rest of the wave shades meanwhile
+    __shared__ uint32_t s_pk_cur[WF_BLOCK];
+    __shared__ int s_pk_sp[WF_BLOCK];
+    __shared__ float s_pk_best[WF_BLOCK];
+    bool parked = false;
+#endif
     while (true) {
 #ifdef RT_PHASE_PROF
         const unsigned long long t0 = __builtin_amdgcn_s_memtime();
@@ -1663,7 +1675,21 @@ __global__ void __launch_bounds__(WF_BLOCK, WAVES) wf_finish_bvh(RtDevScene sc, 
                                      lk0 = c.v[RT_CNT_NODE] * 4 + c.v[RT_CNT_TRI];
             const unsigned long long lt0 = __builtin_amdgcn_s_memtime();
 #endif
+#if WF_BVH_PARK
+            int hit;
+            BvhPark pk{0u, 0, 0.0f};
+            if (parked) pk = BvhPark{s_pk_cur[tid], s_pk_sp[tid], s_pk_best[tid]};
+            const bool done = trace_bvh_park<COUNT>(sc, p.ro, p.rd, hit, bx, by, bz, stk, c, WF_BVH_PARK, parked, pk);
+            parked = !done;
+            if (parked) {
+                s_pk_cur[tid] = pk.cur;
+                s_pk_sp[tid] = pk.sp;
+                s_pk_best[tid] = pk.best;
+            }
+#else
             const int hit = trace_bvh<COUNT>(sc, p.ro, p.rd, bx, by, bz, stk, c);
+            const bool done = true;
+#endif
 #ifdef RT_LOCKSTEP_PROF
             lk_t = __builtin_amdgcn_s_memtime() - lt0;
             lk_db = (uint32_t)((c.v[RT_CNT_B_BVH_NODE] * 4 + c.v[RT_CNT_B_BVH_TRI] - lb0 + 3) / 4);
@@ -1682,7 +1708,7 @@ __global__ void __launch_bounds__(WF_BLOCK, WAVES) wf_finish_bvh(RtDevScene sc, 
 #endif
             // run-time exactness guard: a deterministic sample of the rays, with the
             // bounded result, is queued for wf_check's plain KD re-trace
-            if (!COUNT && st.chk) {
+            if (!COUNT && st.chk && done) {
                 uint32_t h = p.slot * 0x9E3779B1u ^ (uint32_t)p.passes_left * 0x85EBCA77u ^
                              (uint32_t)p.depth * 0xC2B2AE3Du ^ (p.shadow ? 0x27D4EB2Fu : 0u);
                 h ^= h >> 15;
@@ -1699,13 +1725,15 @@ __global__ void __launch_bounds__(WF_BLOCK, WAVES) wf_finish_bvh(RtDevScene sc, 
                     }
                 }
             }
-            const bool want = shade_step<COUNT>(sc, fr, cam, p, hit, bx, by, bz, limit, c);
-            // a path deeper than long_depth goes on in wf_long (64 lanes per ray)
-            to_long = want && st.long_depth > 0 && p.depth > st.long_depth;
-            if (!want || to_long) store_regs(st, fr, p);
-            if (!want) {
-                active = false;
-                rel = st.fresh != 0; // (the pixel's passes are done: let go at the top of the loop)
+            if (done) {
+                const bool want = shade_step<COUNT>(sc, fr, cam, p, hit, bx, by, bz, limit, c);
+                // a path deeper than long_depth goes on in wf_long (64 lanes per ray)
+                to_long = want && st.long_depth > 0 && p.depth > st.long_depth;
+                if (!want || to_long) store_regs(st, fr, p);
+                if (!want) {
+                    active = false;
+                    rel = st.fresh != 0; // (the pixel's passes are done: let go at the top of the loop)
+                }
             }
 #ifdef RT_PHASE_PROF
             ph[3] += __builtin_amdgcn_s_memtime() - t2s;
