@@ -126,6 +126,12 @@ int upload_prepared(const rt_host::PreparedHost &h, int ntris, int nindices, rt_
     dv.kd_rows = nullptr;
     dv.kd_cell = nullptr;
     dv.kd_grid = 0;
+    dv.kd_entry = nullptr;
+    dv.split_hash = nullptr;
+    for (int a = 0; a < 3; ++a) {
+        dv.split_hash_off[a] = h.split_hash_off[a];
+        dv.split_hash_mask[a] = h.split_hash_mask[a];
+    }
     for (int a = 0; a < 3; ++a) dv.kd_gscale[a] = h.kd_grid_scale[a];
     for (int a = 0; a < 4; ++a) dv.split_off[a] = h.split_off[a];
     if (h.bvh_depth >= 0 && ((rc = upload_vec(*s, h.bvh_nodes, &dv.bvh_nodes)) ||
@@ -143,6 +149,12 @@ int upload_prepared(const rt_host::PreparedHost &h, int ntris, int nindices, rt_
         return rc;
     }
     if (dv.kd_cell) dv.kd_grid = h.kd_grid;
+    // the bounded KD phase's entry: the cells' start nodes and boxes, the split hash sets
+    if (dv.kd_cell && h.bvh_depth >= 0 && !h.kd_entry.empty() && !h.split_hash.empty() &&
+        ((rc = upload_vec(*s, h.kd_entry, &dv.kd_entry)) || (rc = upload_vec(*s, h.split_hash, &dv.split_hash)))) {
+        release(s);
+        return rc;
+    }
     dv.nodes = nodes;
     dv.isect_a = a;
     dv.isect_bary = bary;

@@ -117,6 +117,10 @@ struct RtDevScene {
     const uint32_t *kd_cell;    // per cell of a kd_grid^3 grid over the scene box: {start node, row offset << 5 | depth}
     int kd_grid;                // cell of p: ((p - bmin) * kd_gscale), clamped to [0, kd_grid - 1]
     float kd_gscale[3];
+    // the bounded KD phase's entry (bvh_trace.h kd_bounded); nullptr: none
+    const RtF4 *kd_entry;       // per cell: {start node bits, its cell's lo.xyz}, {hi.xyz, 0}
+    const uint32_t *split_hash; // per axis a hash set of the split values (bvh_common.h rt_split_hash)
+    uint32_t split_hash_off[3], split_hash_mask[3];
 };
 
 // BVH child reference: an inner node's index, or RT_BVH_LEAF | first << 3 |

@@ -1491,7 +1491,7 @@ __global__ void __launch_bounds__(WF_BLOCK, WAVES) wf_finish_bvh(RtDevScene sc, 
             // this call's pixels (wf_start's work, in its 8x8-pixel wave tiles): a lane claims its
             // pixel (BUSY) unless another holder still has it — a previous chained call's finisher
             // lane or wf_long —, which then owes it this call's passes and runs them next
-            bool claim = !active && !rel, started = false;
+            bool claim = !active && !rel, started = false, acq = false;
             uint32_t my_passes = 0, my_call = 0;
             exhausted = false;
             while (__any(claim)) {
@@ -1544,6 +1544,7 @@ __global__ void __launch_bounds__(WF_BLOCK, WAVES) wf_finish_bvh(RtDevScene sc, 
                                                                             __HIP_MEMORY_SCOPE_AGENT)) {
                                 claim = false;
                                 started = true;
+                                acq = (x & RT_PX_REL) != 0u; // (released by a concurrent holder)
                                 my_passes = cur_passes;
                                 my_call = cur;
                                 p.slot = (uint32_t)slot;
@@ -1570,10 +1571,14 @@ __global__ void __launch_bounds__(WF_BLOCK, WAVES) wf_finish_bvh(RtDevScene sc, 
                     }
                 }
             }
+            // (a pixel whose last holder ran concurrently with this finisher — wf_long, or a
+            // chained finisher — released its stores with plain stores + an agent release before
+            // the word said free (REL / LONGDONE): read them after an agent acquire.  sc1 loads
+            // alone are no acquire for plain-stored bytes (MI355X_MICROARCH.md, Valid forms): this
+            // XCD's L2 may hold the line from a neighbouring pixel read earlier.  A pixel last held
+            // by an earlier launch needs none: the launch boundary is the release / acquire.)
+            if (__any(acq)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             if (started) { // the pixel's state and its first pass (wf_start's)
-                // (its last holder may have been a concurrent finisher or wf_long, which released
-                // its stores before the word said free: read them past this CU's L1 — sc1 loads —
-                // instead of an acquire, which would drop every wave's L1 lines on the CU)
                 const uint32_t slot = p.slot;
                 p.rng = ld_sc1(fr.rng + slot);
                 Vec3D fb = rt_v3(0.0f, 0.0f, 0.0f);

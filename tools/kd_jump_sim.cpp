@@ -347,6 +347,173 @@ float bvh8(const rt_host::PreparedHost &h, const std::vector<Node8> &N, const st
 }
 
 
+
+// ---- the stateless entry: descend from P's grid cell start node by the rule
+// "near iff t < 0 or t > s_min", certify the leaf by its cell faces (the rule
+// is monotone in the split value except at a split == the origin coordinate
+// with d > 0: those origins are looked up in the axis's split-value set), take
+// exit = min(root exit, face t > s_min), test the leaf; fall back to the root
+// descent if the leaf does not hit
+struct Cells {
+    std::vector<float> lo, hi; // per node: its cell (+-inf where no ancestor bounds it)
+    std::vector<std::vector<float>> vals; // per axis: sorted distinct split values
+};
+
+void build_cells(const rt_host::PreparedHost &h, Cells &C)
+{
+    const size_t nn = h.nodes.size() / 2;
+    C.lo.assign(3 * nn, -INFINITY);
+    C.hi.assign(3 * nn, INFINITY);
+    C.vals.assign(3, {});
+    std::vector<uint32_t> todo{0};
+    while (!todo.empty()) {
+        const uint32_t n = todo.back();
+        todo.pop_back();
+        const uint32_t y = h.nodes[2 * n + 1];
+        if ((y & 3u) == RT_LEAF_TAG) continue;
+        const int a = (int)(y & 3u);
+        const float sp = bitsf(h.nodes[2 * n]);
+        C.vals[a].push_back(sp == 0.0f ? 0.0f : sp);
+        const uint32_t l = n + 1, r = y >> 2;
+        for (int k = 0; k < 3; ++k) {
+            C.lo[3 * l + k] = C.lo[3 * n + k];
+            C.hi[3 * l + k] = C.hi[3 * n + k];
+            C.lo[3 * r + k] = C.lo[3 * n + k];
+            C.hi[3 * r + k] = C.hi[3 * n + k];
+        }
+        C.hi[3 * l + a] = std::min(C.hi[3 * l + a], sp); // left child: below the split (the tightest per side)
+        C.lo[3 * r + a] = std::max(C.lo[3 * r + a], sp);
+        todo.push_back(l);
+        todo.push_back(r);
+    }
+    for (auto &v : C.vals) {
+        std::sort(v.begin(), v.end());
+        v.erase(std::unique(v.begin(), v.end()), v.end());
+    }
+}
+
+// the child the bounded descent takes at split v on axis a (0 left, 1 right)
+int side(float v, float oa, float da, float s_min)
+{
+    const int near_c = oa >= v ? 1 : 0;
+    const float t = (v - oa) / da;
+    return (t < 0 || t > s_min) ? near_c : 1 - near_c;
+}
+
+long long g_sj_fail[6] = {0, 0, 0, 0, 0, 0}; // entry, cell, face, origin, miss, ok
+long long g_origin_checks = 0, g_below = 0;
+// the entry certified at the start node N: N's cell faces by the rule's
+// monotonicity (+ the origin lookups), then the exact rule below N with the
+// exit tracked (exit = min(exit, t) for every t > s_min)
+Hit stateless_trace(const rt_host::PreparedHost &h, const Cells &C, Vec3D o, Vec3D d, float t1, float t2, float s_min,
+                    Work &w, double &steps)
+{
+    auto full = [&]() { return kd_trace(h, o, d, t1, t2, s_min, w); };
+    if (!(s_min >= t1)) { ++g_sj_fail[0]; steps += 1; return full(); }
+    const Vec3D p = rt_v3(o.x + d.x * s_min, o.y + d.y * s_min, o.z + d.z * s_min);
+    size_t k;
+    if (!cell_of(h, p, k) || h.kd_cell[2 * k] == 0xFFFFFFFFu) { ++g_sj_fail[1]; steps += 1; return full(); }
+    uint32_t node = h.kd_cell[2 * k];
+    steps += 2; // the cell word, N's box (independent loads)
+    const float oo[3] = {o.x, o.y, o.z}, dd[3] = {d.x, d.y, d.z};
+    float ex = t2;
+    for (int a = 0; a < 3; ++a) {
+        const float lo = C.lo[3 * node + a], hi = C.hi[3 * node + a];
+        if (lo > -INFINITY) {
+            if (side(lo, oo[a], dd[a], s_min) != 1) { ++g_sj_fail[2]; return full(); }
+            const float t = (lo - oo[a]) / dd[a];
+            if (t > s_min) ex = std::min(ex, t);
+        }
+        if (hi < INFINITY) {
+            if (side(hi, oo[a], dd[a], s_min) != 0) { ++g_sj_fail[2]; return full(); }
+            const float t = (hi - oo[a]) / dd[a];
+            if (t > s_min) ex = std::min(ex, t);
+        }
+        if (dd[a] > 0 && lo > -INFINITY && oo[a] < lo) {
+            ++g_origin_checks;
+            const float v = oo[a] == 0.0f ? 0.0f : oo[a];
+            if (std::binary_search(C.vals[a].begin(), C.vals[a].end(), v)) { ++g_sj_fail[3]; return full(); }
+        }
+    }
+    while (true) {
+        const uint32_t x = h.nodes[2 * node], y = h.nodes[2 * node + 1];
+        steps += 1;
+        if ((y & 3u) == RT_LEAF_TAG) break;
+        ++g_below;
+        const int a = (int)(y & 3u);
+        const float v = bitsf(x);
+        const float t = (v - oo[a]) / dd[a];
+        if (t > s_min) ex = std::min(ex, t);
+        node = side(v, oo[a], dd[a], s_min) ? (y >> 2) : node + 1;
+    }
+    const uint32_t ny = h.nodes[2 * node + 1], nx = h.nodes[2 * node];
+    const uint32_t count = ny >> 2;
+    Hit hit;
+    if (count > 0 && ex > s_min) {
+        float smallest = ex;
+        for (uint32_t e = nx; e < nx + count; ++e) {
+            float s, b[3];
+            ++w.tests;
+            if (test(h.isect_a.data(), h.isect_bary.data(), e, o, d, smallest, s, b)) {
+                smallest = s;
+                hit.tri = (int)h.isect_bary[e].tri;
+                memcpy(hit.b, b, sizeof b);
+            }
+        }
+        steps += count / 4.0;
+    }
+    if (hit.tri >= 0) { ++g_sj_fail[5]; return hit; }
+    ++g_sj_fail[4];
+    return full();
+}
+
+// descent length from the deepest node holding P's cell of a G^3 grid (the start node) to P's leaf
+void grid_depth_stats(const rt_host::PreparedHost &h, const std::vector<float> &R, int G)
+{
+    const float bmin[3] = {h.bounds.min.x, h.bounds.min.y, h.bounds.min.z};
+    const float ext[3] = {h.bounds.max.x - h.bounds.min.x, h.bounds.max.y - h.bounds.min.y, h.bounds.max.z - h.bounds.min.z};
+    std::vector<int> rem;
+    double top = 0;
+    for (size_t i = 0; i < R.size() / 6; ++i) {
+        const float P[3] = {R[6 * i], R[6 * i + 1], R[6 * i + 2]}; // (the origins: a stand-in for hit points)
+        int c[3];
+        float lo[3], hi[3];
+        for (int a = 0; a < 3; ++a) {
+            const float f = (P[a] - bmin[a]) * ((float)G / ext[a]);
+            c[a] = f >= 0 ? (f < G - 1 ? (int)f : G - 1) : 0;
+            lo[a] = bmin[a] + ext[a] * (float)c[a] / (float)G;
+            hi[a] = bmin[a] + ext[a] * (float)(c[a] + 1) / (float)G;
+        }
+        uint32_t n = 0;
+        int dtop = 0;
+        while (true) {
+            const uint32_t x = h.nodes[2 * n], y = h.nodes[2 * n + 1];
+            if ((y & 3u) == RT_LEAF_TAG) break;
+            const int a = (int)(y & 3u);
+            const float sp = bitsf(x);
+            if (hi[a] < sp) n = n + 1;
+            else if (lo[a] > sp) n = y >> 2;
+            else break;
+            ++dtop;
+        }
+        int r = 0;
+        while (true) {
+            const uint32_t x = h.nodes[2 * n], y = h.nodes[2 * n + 1];
+            if ((y & 3u) == RT_LEAF_TAG) break;
+            const int a = (int)(y & 3u);
+            n = P[a] < bitsf(x) ? n + 1 : (y >> 2);
+            ++r;
+        }
+        rem.push_back(r);
+        top += dtop;
+    }
+    std::sort(rem.begin(), rem.end());
+    double m = 0;
+    for (int v : rem) m += v;
+    const size_t k = rem.size();
+    printf("grid %d: start depth %.1f, levels below start mean %.2f p50 %d p90 %d p99 %d max %d\n", G, top / k, m / k,
+           rem[k / 2], rem[k * 9 / 10], rem[k * 99 / 100], rem[k - 1]);
+}
 bool same(const Hit &a, const Hit &b) { return a.tri == b.tri && memcmp(a.b, b.b, sizeof a.b) == 0; }
 
 } // namespace
@@ -381,6 +548,8 @@ int main(int argc, char **argv)
                 if (!(N8.back().ref[k] & RT_BVH_LEAF)) todo.push_back(N8.back().ref[k]);
         }
     }
+    Cells C;
+    build_cells(h, C);
     FILE *f = fopen(argv[2], "rb");
     if (!f) return 2;
     std::vector<float> R;
@@ -388,10 +557,14 @@ int main(int argc, char **argv)
     while (fread(buf, sizeof buf, 1, f) == 1) R.insert(R.end(), buf, buf + 6);
     fclose(f);
     const size_t nr = R.size() / 6;
+    if (getenv("GRID_STATS")) {
+        for (int G : {64, 127, 256, 512, 1024, 2048}) grid_depth_stats(h, R, G);
+        return 0;
+    }
     printf("scene tris %d kd nodes %zu grid %d rows %zu rays %zu\n", n, h.nodes.size() / 2, h.kd_grid,
            h.kd_rows.size() / 4, nr);
     // per ray lane steps: bvh (nodes + tests/4), kd from the root, kd from P's cell (rows/4 + nodes + tests/4)
-    std::vector<double> sb(nr, 0), sk(nr, 0), sj(nr, 0), s8(nr, 0);
+    std::vector<double> sb(nr, 0), sk(nr, 0), sj(nr, 0), s8(nr, 0), ss(nr, 0);
     long long mism8 = 0;
     long long mism = 0, jumped = 0, fell = 0, bounded = 0, nodes_root = 0, nodes_jump = 0, rows = 0;
     for (size_t i = 0; i < nr; ++i) {
@@ -437,6 +610,13 @@ int main(int argc, char **argv)
             hj = kd_trace(h, o, d, t1, t2, s_min, wj);
         }
         if (!same(hj, plain)) ++mism;
+        {
+            Work ws;
+            double st = 0;
+            const Hit hs = stateless_trace(h, C, o, d, t1, t2, s_min, ws, st);
+            if (!same(hs, plain)) ++mism;
+            ss[i] = st + ws.nodes + (ws.tests > 0 && st == 0 ? 0 : 0) + (ws.nodes ? ws.tests / 4.0 : 0);
+        }
         sj[i] = wj.rows / 4.0 + wj.nodes + wj.tests / 4.0;
         nodes_jump += wj.nodes;
         rows += wj.rows;
@@ -492,6 +672,26 @@ int main(int argc, char **argv)
         fclose(o);
     }
     pct(sb, "bvh");
+    pct(ss, "kd_stateless");
+    {
+        double l = 0, wv = 0, nw = 0;
+        std::mt19937_64 r2(9);
+        std::vector<size_t> pm(nr);
+        for (size_t i = 0; i < nr; ++i) pm[i] = i;
+        for (int rep = 0; rep < 8; ++rep) {
+            std::shuffle(pm.begin(), pm.end(), r2);
+            for (size_t w0 = 0; w0 + 64 <= nr; w0 += 64) {
+                double m = 0;
+                for (size_t j = w0; j < w0 + 64; ++j) { l += ss[pm[j]]; m = std::max(m, ss[pm[j]]); }
+                wv += m;
+                nw += 1;
+            }
+        }
+        printf("kd_stateless: lane %.2f wave %.2f; fail entry %lld cell %lld face %lld origin %lld leafmiss %lld ok %lld"
+               " origin checks %lld levels below N %.2f\n",
+               l / (nw * 64), wv / nw, g_sj_fail[0], g_sj_fail[1], g_sj_fail[2], g_sj_fail[3], g_sj_fail[4],
+               g_sj_fail[5], g_origin_checks, (double)g_below / (g_sj_fail[4] + g_sj_fail[5]));
+    }
     pct(s8, "bvh8");
     printf("bvh8: nodes %zu s_min mismatches %lld lane %.2f wave %.2f eff %.3f\n", N8.size(), mism8, lane_8 / rays,
            wave_8 / waves, lane_8 / rays / (wave_8 / waves));
