@@ -27,8 +27,15 @@ threading.Thread(target=heartbeat, daemon=True).start()
 rt.check(rt.lib().rt_set_device(0))
 run = helpers.GpuRun(scene)
 g = rt.GBuffer(W, H)
-rt.render(run.dev, g, run.camera, 0, rt.options(W, H, 2, adaptive=False, kernel=rt.KERNEL_WAVEFRONT))
+dbg = int(os.environ.get("PROF_CALL_DEBUG", "0"))
+extra = dict(check_interval=int(os.environ.get("PROF_CALL_CHECK", "0")),
+             wf_long_depth=int(os.environ.get("PROF_CALL_LONG", "0")))
+rt.render(run.dev, g, run.camera, 0, rt.options(W, H, 2, adaptive=False, kernel=rt.KERNEL_WAVEFRONT, debug=dbg,
+                                                **extra))
+print("warm-up call issued", file=sys.stderr, flush=True)
 rt.join()
-rt.render(run.dev, g, run.camera, 1, rt.options(W, H, passes, adaptive=False, kernel=rt.KERNEL_WAVEFRONT))
+print("warm-up call joined", file=sys.stderr, flush=True)
+rt.render(run.dev, g, run.camera, 1, rt.options(W, H, passes, adaptive=False, kernel=rt.KERNEL_WAVEFRONT, debug=dbg,
+                                                 **extra))
 rt.join()
 print("done", flush=True)
