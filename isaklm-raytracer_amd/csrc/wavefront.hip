@@ -75,8 +75,8 @@ static_assert(WF_BLOCK % WF_TBLOCK == 0 && WF_TBLOCK % 64 == 0, "WF_TBLOCK must 
 #endif
 #ifndef WF_FIN_LINGER_WAVES
 #define WF_FIN_LINGER_WAVES 256u // finisher waves that linger for returned pixels
-#define WF_FIN_LINGER_TRIPS (1u << 20) // ... and at most this many idle loop trips (~1 s or more)
 #endif
+#define WF_FIN_QUIET_TRIPS 4096u // ... while wf_long ran a path within this many of their idle loop trips
 #ifndef WF_FIN_OCC
 #define WF_FIN_OCC 1 // wf_finish_coop occupancy floor (1: the compiler's choice, 2 waves/SIMD; 3: no change)
 #endif
@@ -1370,9 +1370,7 @@ __global__ void __launch_bounds__(WF_BLOCK, WAVES) wf_finish_bvh(RtDevScene sc, 
     // (fresh) the wave's call: this launch's, then the chain's later issued calls
     uint32_t cur = st.call_id, cur_passes = (uint32_t)fr.passes;
     unsigned long long idle_since = 0;      // (lane 0) when the wave first had nothing to do
-    uint32_t idle_trips = 0;                // (lane 0) ... and its idle loop trips since (the linger's
-                                            // bound also where the real-time clock stands still:
-                                            // under rocprofv3 counter collection it does)
+    uint32_t quiet_trips = 0;               // (lane 0) idle loop trips in a row with no wf_long path running
     bool seated = false;                    // (lane 0) holds a linger seat
 #if WF_BVH_PARK
     // a lane whose s_min query ran WF_BVH_PARK node steps parks it (its state in LDS, the stack in
@@ -1636,8 +1634,14 @@ __global__ void __launch_bounds__(WF_BLOCK, WAVES) wf_finish_bvh(RtDevScene sc, 
             int leave = 0;
             if (lane == 0) {
                 if (idle_since == 0) idle_since = __builtin_amdgcn_s_memrealtime();
-                ++idle_trips;
-                bool out = st.linger != 0 &&
+                // linger only while wf_long runs paths that may come back: where it cannot run beside
+                // the finisher (rocprofv3 counter collection serialises the two launches) lingering
+                // would only hold the finisher's end — and the next launch — up by st.linger per wave
+                if (__hip_atomic_load(st.long_ctr + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+                    ++quiet_trips;
+                else
+                    quiet_trips = 0;
+                bool out = st.linger != 0 && quiet_trips < WF_FIN_QUIET_TRIPS &&
                            __hip_atomic_load(st.ret_ctr + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
                 // only WF_FIN_LINGER_WAVES waves linger (a seat each, kept until they leave): the
                 // others leave their slots to wf_long, which the deep paths are waiting for
@@ -1651,7 +1655,7 @@ __global__ void __launch_bounds__(WF_BLOCK, WAVES) wf_finish_bvh(RtDevScene sc, 
                 unsigned long long w = __hip_atomic_load(ret_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 const uint32_t cl = __hip_atomic_load(ret_claimed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if ((uint32_t)w == cl &&
-                    (!out || __builtin_amdgcn_s_memrealtime() - idle_since > st.linger || idle_trips > WF_FIN_LINGER_TRIPS) &&
+                    (!out || __builtin_amdgcn_s_memrealtime() - idle_since > st.linger) &&
                     __hip_atomic_compare_exchange_strong(ret_word, &w, w - (1ull << 32), __ATOMIC_RELAXED,
                                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
                     leave = 1;
@@ -1664,7 +1668,7 @@ __global__ void __launch_bounds__(WF_BLOCK, WAVES) wf_finish_bvh(RtDevScene sc, 
             continue;
         }
         idle_since = 0;
-        idle_trips = 0;
+        quiet_trips = 0;
         bool to_long = false;
 #ifdef RT_LOCKSTEP_PROF
         uint32_t lk_db = 0, lk_dk = 0;
