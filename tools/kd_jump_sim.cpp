@@ -402,6 +402,7 @@ int side(float v, float oa, float da, float s_min)
 
 long long g_sj_fail[6] = {0, 0, 0, 0, 0, 0}; // entry, cell, face, origin, miss, ok
 long long g_origin_checks = 0, g_below = 0;
+int g_fine = 1; // (experiment) subgrid factor under the top grid
 // the entry certified at the start node N: N's cell faces by the rule's
 // monotonicity (+ the origin lookups), then the exact rule below N with the
 // exit tracked (exit = min(exit, t) for every t > s_min)
@@ -415,6 +416,31 @@ Hit stateless_trace(const rt_host::PreparedHost &h, const Cells &C, Vec3D o, Vec
     if (!cell_of(h, p, k) || h.kd_cell[2 * k] == 0xFFFFFFFFu) { ++g_sj_fail[1]; steps += 1; return full(); }
     uint32_t node = h.kd_cell[2 * k];
     steps += 2; // the cell word, N's box (independent loads)
+    if (g_fine > 1) { // a subgrid of g_fine^3 under P's top cell: the deepest node holding P's subcell
+        const float bmin[3] = {h.bounds.min.x, h.bounds.min.y, h.bounds.min.z};
+        const float ext[3] = {h.bounds.max.x - h.bounds.min.x, h.bounds.max.y - h.bounds.min.y,
+                              h.bounds.max.z - h.bounds.min.z};
+        const int G = h.kd_grid * g_fine;
+        const float q[3] = {p.x, p.y, p.z};
+        float lo[3], hi[3];
+        for (int a = 0; a < 3; ++a) {
+            const float f = (q[a] - bmin[a]) * ((float)G / ext[a]);
+            const int c = f >= 0 ? (f < G - 1 ? (int)f : G - 1) : 0;
+            lo[a] = bmin[a] + ext[a] * (float)c / (float)G;
+            hi[a] = bmin[a] + ext[a] * (float)(c + 1) / (float)G;
+        }
+        uint32_t n = 0;
+        while (true) {
+            const uint32_t x = h.nodes[2 * n], y = h.nodes[2 * n + 1];
+            if ((y & 3u) == RT_LEAF_TAG) break;
+            const int a = (int)(y & 3u);
+            const float sp = bitsf(x);
+            if (hi[a] < sp) n = n + 1;
+            else if (lo[a] > sp) n = y >> 2;
+            else break;
+        }
+        if (n != node) { node = n; steps += 1; } // (the subcell record: one more dependent load)
+    }
     const float oo[3] = {o.x, o.y, o.z}, dd[3] = {d.x, d.y, d.z};
     float ex = t2;
     for (int a = 0; a < 3; ++a) {
@@ -522,6 +548,7 @@ int main(int argc, char **argv)
 {
     if (argc < 3) return 2;
     if (getenv("MARGIN_SCALE")) g_margin_scale = (float)atof(getenv("MARGIN_SCALE"));
+    if (getenv("FINE")) g_fine = atoi(getenv("FINE"));
     RtHostScene scene;
     Camera cam;
     if (rt_host::load_scene_file(scene, argv[1], &cam) != RT_OK) return 2;
