@@ -76,7 +76,9 @@ static_assert(WF_BLOCK % WF_TBLOCK == 0 && WF_TBLOCK % 64 == 0, "WF_TBLOCK must 
 #ifndef WF_FIN_LINGER_WAVES
 #define WF_FIN_LINGER_WAVES 256u // finisher waves that linger for returned pixels
 #endif
+#ifndef WF_FIN_QUIET_TRIPS
 #define WF_FIN_QUIET_TRIPS 4096u // ... while wf_long ran a path within this many of their idle loop trips
+#endif
 #ifndef WF_FIN_OCC
 #define WF_FIN_OCC 1 // wf_finish_coop occupancy floor (1: the compiler's choice, 2 waves/SIMD; 3: no change)
 #endif
@@ -1493,9 +1495,12 @@ __global__ void __launch_bounds__(WF_BLOCK, WAVES) wf_finish_bvh(RtDevScene sc, 
             // this call's pixels (wf_start's work, in its 8x8-pixel wave tiles): a lane claims its
             // pixel (BUSY) unless another holder still has it — a previous chained call's finisher
             // lane or wf_long —, which then owes it this call's passes and runs them next
-            bool claim = !active && !rel, started = false, acq = false;
+            // (a lane that found the list run out stays out: idle trips must not keep adding to
+            // the cursor — a lingering wave's trips wrapped it past 2^32 and re-ran the call's
+            // pixels.  Continuation mode: a later issued call may still have pixels for it.)
+            if (st.call_ring) exhausted = false;
+            bool claim = !active && !rel && !exhausted, started = false, acq = false;
             uint32_t my_passes = 0, my_call = 0;
-            exhausted = false;
             while (__any(claim)) {
                 const unsigned long long m = __ballot(claim);
                 const int leader = __ffsll((long long)m) - 1;

@@ -259,3 +259,15 @@ def test_chain_left_open_at_exit(tmp_path):
     """)
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "enqueued" in r.stdout, r.stdout + r.stderr
+
+
+def test_unchained_long_calls_run_each_pass_once():
+    """Two unchained 256-pass room2m calls: every pixel ends with exactly 512
+    samples.  (Round 5 regression: a finisher's lingering waves kept claiming
+    from the exhausted pixel list on every idle trip, wrapped its 32-bit
+    cursor during a long linger and ran the call's pixels a second time; the
+    1,024-spp budget test caught it as a 1.25x frame.)"""
+    run = helpers.GpuRun("room2m")
+    W, H = 1920, 1080
+    gpu = _render_calls(run, W, H, [256, 256], overlap=False)
+    assert int(gpu[2].min()) == 512 and int(gpu[2].max()) == 512
