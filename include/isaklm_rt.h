@@ -464,11 +464,11 @@ typedef struct RtOptions {
      * 0: the call is complete at its stream point.  1: the call is only
      * enqueued — the caller's stream does not wait for it — and the NEXT call
      * of the same frame — same scene, G_Buffer, camera and frame options,
-     * sample_count != 0, overlap 1 — starts at once: its kernel fills the
-     * slots the previous call's tail frees, its pixels that are free run its
-     * passes, and the ones still held (by the previous call's tail or the
-     * long-path kernel running a deep glass path of 10^4+ bounces) are owed
-     * the passes and run them before they are let go.  Every pixel's passes
+     * sample_count != 0, overlap 1 — is enqueued right behind it: its path
+     * kernel starts when the previous one ends, without waiting for the
+     * long-path kernel, whose deep glass paths (10^4+ bounces) run on beside
+     * it; the pixels those paths still hold are owed the new call's passes and
+     * run them before they are let go.  Every pixel's passes
      * run in the reference's order, so the frame is bit-identical to
      * unchained calls.  A call with sample_count 0 (reset_frame) is never
      * chained: it completes before the next call starts.  Whatever reads the frame in

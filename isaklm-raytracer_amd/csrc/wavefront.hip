@@ -76,6 +76,10 @@ static_assert(WF_BLOCK % WF_TBLOCK == 0 && WF_TBLOCK % 64 == 0, "WF_TBLOCK must 
 #ifndef WF_FIN_LINGER_WAVES
 #define WF_FIN_LINGER_WAVES 256u // finisher waves that linger for returned pixels
 #endif
+#ifndef WF_HEAVY_FIRST
+#define WF_HEAVY_FIRST 1 // whole-call finisher: pixels whose paths went to wf_long before start the call
+#endif
+#define WF_HEAVY_BLOCKS 256
 #ifndef WF_FIN_QUIET_TRIPS
 #define WF_FIN_QUIET_TRIPS 4096u // ... while wf_long ran a path within this many of their idle loop trips
 #endif
@@ -225,6 +229,13 @@ struct WfState {
     unsigned long long linger;
     // per pixel: RT_PX_OUT / RT_PX_BUSY | passes owed by later chained calls, RT_PX_REL, or 0
     uint32_t *pxo;
+    // heavy pixels first (whole-call finisher): a pixel whose path went to wf_long is marked
+    // (heavy); before each call wf_heavy_list lists the marked pixels (heavy_list, count
+    // heavy_n) and tags them with the call (listed): the finisher's first entries are those
+    // pixels, and its tile entries skip a pixel listed for this call.  heavy_list == nullptr:
+    // no list (the tiles only)
+    uint8_t *heavy;
+    uint32_t *listed, *heavy_list, *heavy_n;
     // the whole-call finisher takes this call's pixels itself (no wf_start, no path list):
     // fresh = 1; concurrent = 1 when the next chained call's finisher may run beside this
     // one (a pixel is released with a release fence and marked RT_PX_REL)
@@ -1346,7 +1357,9 @@ __global__ void __launch_bounds__(WF_BLOCK, WAVES) wf_finish_bvh(RtDevScene sc, 
     Cnt c;
     if (COUNT) c.zero();
     // fresh: this call's pixels, 256 entries per 16x16-pixel tile (fresh_pixel); else the paths of path list q
-    const uint32_t n = st.fresh ? st.fresh_n : st.counts[6 + q];
+    // (fresh: the listed heavy pixels first, then the tiles)
+    const uint32_t n_heavy = st.fresh && st.heavy_list ? *st.heavy_n : 0u;
+    const uint32_t n = st.fresh ? n_heavy + st.fresh_n : st.counts[6 + q];
     uint32_t *fetch = st.counts + 4;
     const int limit = fr.max_depth > 0 ? fr.max_depth : RT_WATCHDOG_BOUNCES;
     const int lane = __lane_id();
@@ -1538,7 +1551,9 @@ __global__ void __launch_bounds__(WF_BLOCK, WAVES) wf_finish_bvh(RtDevScene sc, 
                         if (st.call_exh && ok && e == n) // (the lane that ran the list out tells the host)
                             __hip_atomic_store(st.call_exh + cur % WF_CALL_RING, cur, __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_SYSTEM);
-                    } else if (fresh_pixel(fr, e, slot)) {
+                    } else if (e < n_heavy ? (slot = (int)st.heavy_list[e], true)
+                                           : fresh_pixel(fr, e - n_heavy, slot) &&
+                                                 !(st.heavy_list && st.listed[slot] == st.call_id)) {
                         uint32_t x = __hip_atomic_load(st.pxo + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         while (true) {
                             if (x & (RT_PX_OUT | RT_PX_BUSY)) { // held: owed this call's passes
@@ -1783,7 +1798,10 @@ __global__ void __launch_bounds__(WF_BLOCK, WAVES) wf_finish_bvh(RtDevScene sc, 
             }
         }
 #endif
-        if (__any(to_long) && publish_long_capped(st, to_long, p.slot, p.ro, p.rd) && to_long) active = false;
+        if (__any(to_long) && publish_long_capped(st, to_long, p.slot, p.ro, p.rd) && to_long) {
+            active = false;
+            if (st.heavy) st.heavy[p.slot] = 1; // (first in the next call's list)
+        }
     }
 #ifdef RT_PHASE_PROF
     if (lane == 0)
@@ -1853,6 +1871,34 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_check(RtDevScene sc, WfState st, 
 // be balanced by now: pixels out, returns reserved but unclaimed, hand-off
 // entries reserved but unclaimed, finisher waves still registered alive.
 // res: [0] stranded pixels, [1..4] those counters (accumulated until the host reads them).
+// Heavy pixels first: the pixels marked heavy (a path of theirs went to wf_long
+// in an earlier call) that this call renders, listed (wave-aggregated atomic:
+// any order — a pixel's passes run in its own order whoever takes it first)
+// and tagged with the call so the finisher's tile entries skip them.  The
+// deep-path-prone pixels then start their chains at the call's start instead
+// of wherever their tile falls: their deep samples end inside the call rather
+// than in the chain's drain.
+__global__ void __launch_bounds__(WF_BLOCK) wf_heavy_list(RtDevFrame fr, WfState st, uint32_t call_id)
+{
+    const uint32_t n = (uint32_t)fr.width * (uint32_t)fr.height;
+    const int lane = __lane_id();
+    // (wave-uniform loop: every lane of the wave reaches the ballot)
+    for (uint32_t w0 = blockIdx.x * WF_BLOCK + (threadIdx.x & ~63u); w0 < n; w0 += WF_BLOCK * gridDim.x) {
+        const uint32_t i = w0 + (uint32_t)lane;
+        const bool take = i < n && st.heavy[i] && rt_row_owned(fr, (int)(i / (uint32_t)fr.width));
+        const unsigned long long m = __ballot(take);
+        if (!m) continue;
+        const int leader = __ffsll((long long)m) - 1;
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(st.heavy_n, (uint32_t)__popcll(m));
+        base = (uint32_t)__shfl((int)base, leader);
+        if (take) {
+            st.heavy_list[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = i;
+            st.listed[i] = call_id;
+        }
+    }
+}
+
 __global__ void __launch_bounds__(WF_BLOCK) wf_verify(WfState st, uint32_t n, uint32_t *res, unsigned long long *dev)
 {
     uint32_t out = 0;
@@ -2307,6 +2353,7 @@ struct Workspace {
     hipEvent_t long_ev = nullptr; // after the last wf_long slice on the caller's stream (queue mode)
     bool recorded = false;   // long_ev recorded by a previous call
     uint32_t *fin_live = nullptr; // 8 producer words (whole-call mode, one per call in flight: call % 8)
+    uint32_t *heavy_list = nullptr; // (WfState.heavy_list: every pixel at most once)
     RtF4 *chk = nullptr;          // the exactness guard's records (2 x WF_CHECK_CAP x 3 RtF4; allocated on
                                   // the first call with the guard on) and their counter
     uint32_t *chk_ctr = nullptr;
@@ -2485,7 +2532,8 @@ int ensure(Workspace &w, size_t slots, int grid, int npipes)
     // per pixel
     const size_t o_pl = take(slots * 4), o_fl = take(slots * 4), o_T = take(slots * 12), o_L = take(slots * 12),
                  o_c = take(slots * 12), o_n = take(slots * 12), o_rp = take(slots * 12), o_li = take(slots * 4),
-                 o_ro = take(slots * 12), o_es = take(slots * 4), o_ee = take(slots * 4), o_px = take(slots * 4);
+                 o_ro = take(slots * 12), o_es = take(slots * 4), o_ee = take(slots * 4), o_px = take(slots * 4),
+                 o_hv = take(slots), o_ls = take(slots * 4), o_hl = take(slots * 4), o_hn = take(256);
     // long-path hand-off (shared by the pipelines), wf_long's stack-free wide traversal needs no spill
     const size_t o_le = take(slots * 8), o_lr = take(slots * 32), o_lc = take(256), o_rr = take(slots * 8),
                  o_rc = take(256), o_ctl = take(256);
@@ -2508,6 +2556,9 @@ int ensure(Workspace &w, size_t slots, int grid, int npipes)
     }
     char *b = (char *)w.blob;
     if (hipMemset(b + o_px, 0, slots * 4) != hipSuccess) return -1; // no pixel out
+    if (hipMemset(b + o_hv, 0, slots) != hipSuccess || hipMemset(b + o_ls, 0, slots * 4) != hipSuccess ||
+        hipMemset(b + o_hn, 0, 256) != hipSuccess)
+        return -1; // no pixel heavy or listed yet
     if (hipMemset(b + o_ctl, 0, 256) != hipSuccess) return -1;
     w.fin_live = (uint32_t *)(b + o_ctl);
     w.chk_ctr = (uint32_t *)(b + o_ctl + 64);
@@ -2543,6 +2594,11 @@ int ensure(Workspace &w, size_t slots, int grid, int npipes)
         st.ret_ctr = (uint32_t *)(b + o_rc);
         st.linger = WF_FIN_LINGER;
         st.pxo = (uint32_t *)(b + o_px);
+        st.heavy = (uint8_t *)(b + o_hv);
+        st.listed = (uint32_t *)(b + o_ls);
+        st.heavy_list = nullptr; // (set per call by launch_whole)
+        w.heavy_list = (uint32_t *)(b + o_hl);
+        st.heavy_n = (uint32_t *)(b + o_hn);
         st.fin_live = nullptr;
         st.chain_flag = (uint32_t *)(b + o_ctl + 128);
         st.fresh = 0;
@@ -2752,6 +2808,14 @@ int launch_whole(Workspace &w, int dev, const RtDevScene &sc, const RtDevFrame &
     st.span = nullptr;
     if (prof) {
         if (prof_slot(w, s, &st.span, fr.passes) != 0) return -1;
+    }
+    // heavy pixels first (wf_heavy_list): listed and tagged with this call before the finisher
+    st.heavy_list = nullptr;
+    if (long_return && w.heavy_list && WF_HEAVY_FIRST && !WF_FIN_CONTINUE) {
+        st.heavy_list = w.heavy_list;
+        if (hipMemsetAsync(st.heavy_n, 0, 4, s) != hipSuccess) return -1;
+        hipLaunchKernelGGL(wf_heavy_list, dim3(WF_HEAVY_BLOCKS), dim3(WF_BLOCK), 0, s, fr, st, st.call_id);
+        if (hipGetLastError() != hipSuccess) return -1;
     }
     if (hipEventRecord(w.fin_ready, s) != hipSuccess) return -1;
     // (the finisher is launched before its wf_long: on a shared hardware queue
