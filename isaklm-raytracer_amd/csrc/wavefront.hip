@@ -80,6 +80,9 @@ static_assert(WF_BLOCK % WF_TBLOCK == 0 && WF_TBLOCK % 64 == 0, "WF_TBLOCK must 
 #define WF_HEAVY_FIRST 1 // whole-call finisher: pixels whose paths went to wf_long before start the call
 #endif
 #define WF_HEAVY_BLOCKS 256
+#ifndef WF_HEAVY_SPLIT
+#define WF_HEAVY_SPLIT 4 // hand-offs that put a pixel in the first class (1: one class)
+#endif
 #ifndef WF_FIN_QUIET_TRIPS
 #define WF_FIN_QUIET_TRIPS 4096u // ... while wf_long ran a path within this many of their idle loop trips
 #endif
@@ -1800,7 +1803,10 @@ __global__ void __launch_bounds__(WF_BLOCK, WAVES) wf_finish_bvh(RtDevScene sc, 
 #endif
         if (__any(to_long) && publish_long_capped(st, to_long, p.slot, p.ro, p.rd) && to_long) {
             active = false;
-            if (st.heavy) st.heavy[p.slot] = 1; // (first in the next call's list)
+            if (st.heavy) { // (first in the next call's list: the more hand-offs, the earlier)
+                const uint8_t h = st.heavy[p.slot];
+                if (h < 255) st.heavy[p.slot] = (uint8_t)(h + 1);
+            }
         }
     }
 #ifdef RT_PHASE_PROF
@@ -1878,14 +1884,17 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_check(RtDevScene sc, WfState st, 
 // deep-path-prone pixels then start their chains at the call's start instead
 // of wherever their tile falls: their deep samples end inside the call rather
 // than in the chain's drain.
-__global__ void __launch_bounds__(WF_BLOCK) wf_heavy_list(RtDevFrame fr, WfState st, uint32_t call_id)
+__global__ void __launch_bounds__(WF_BLOCK) wf_heavy_list(RtDevFrame fr, WfState st, uint32_t call_id,
+                                                           uint32_t lo, uint32_t hi)
 {
     const uint32_t n = (uint32_t)fr.width * (uint32_t)fr.height;
     const int lane = __lane_id();
     // (wave-uniform loop: every lane of the wave reaches the ballot)
     for (uint32_t w0 = blockIdx.x * WF_BLOCK + (threadIdx.x & ~63u); w0 < n; w0 += WF_BLOCK * gridDim.x) {
         const uint32_t i = w0 + (uint32_t)lane;
-        const bool take = i < n && st.heavy[i] && rt_row_owned(fr, (int)(i / (uint32_t)fr.width));
+        // (pixels handed over lo..hi-1 times so far: the heaviest are listed by the first launch)
+        const uint32_t h = i < n ? (uint32_t)st.heavy[i] : 0u;
+        const bool take = h >= lo && h < hi && rt_row_owned(fr, (int)(i / (uint32_t)fr.width));
         const unsigned long long m = __ballot(take);
         if (!m) continue;
         const int leader = __ffsll((long long)m) - 1;
@@ -2814,7 +2823,11 @@ int launch_whole(Workspace &w, int dev, const RtDevScene &sc, const RtDevFrame &
     if (long_return && w.heavy_list && WF_HEAVY_FIRST && !WF_FIN_CONTINUE) {
         st.heavy_list = w.heavy_list;
         if (hipMemsetAsync(st.heavy_n, 0, 4, s) != hipSuccess) return -1;
-        hipLaunchKernelGGL(wf_heavy_list, dim3(WF_HEAVY_BLOCKS), dim3(WF_BLOCK), 0, s, fr, st, st.call_id);
+        // two classes: pixels handed over WF_HEAVY_SPLIT+ times so far, then the others
+        hipLaunchKernelGGL(wf_heavy_list, dim3(WF_HEAVY_BLOCKS), dim3(WF_BLOCK), 0, s, fr, st, st.call_id,
+                           (uint32_t)WF_HEAVY_SPLIT, 256u);
+        hipLaunchKernelGGL(wf_heavy_list, dim3(WF_HEAVY_BLOCKS), dim3(WF_BLOCK), 0, s, fr, st, st.call_id, 1u,
+                           (uint32_t)WF_HEAVY_SPLIT);
         if (hipGetLastError() != hipSuccess) return -1;
     }
     if (hipEventRecord(w.fin_ready, s) != hipSuccess) return -1;
