@@ -1514,7 +1514,7 @@ __global__ void __launch_bounds__(WF_BLOCK, WAVES) wf_finish_bvh(RtDevScene sc, 
             // (a lane that found the list run out stays out: idle trips must not keep adding to
             // the cursor — a lingering wave's trips wrapped it past 2^32 and re-ran the call's
             // pixels.  Continuation mode: a later issued call may still have pixels for it.)
-            if (st.call_ring) exhausted = false;
+            if (WF_FIN_CONTINUE && st.call_ring) exhausted = false;
             bool claim = !active && !rel && !exhausted, started = false, acq = false;
             uint32_t my_passes = 0, my_call = 0;
             while (__any(claim)) {
@@ -1523,7 +1523,7 @@ __global__ void __launch_bounds__(WF_BLOCK, WAVES) wf_finish_bvh(RtDevScene sc, 
                 uint32_t base = 0;
                 int ok = 1;
                 if (lane == leader) {
-                    if (st.call_ctr) { // the wave's call's cursor, claimed for it by its first user
+                    if (WF_FIN_CONTINUE && st.call_ctr) { // the wave's call's cursor, claimed for it by its first user
                         unsigned long long *ctr = st.call_ctr + cur % WF_CALL_CURSORS;
                         unsigned long long v = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         while ((uint32_t)(v >> 32) < cur &&
@@ -1551,7 +1551,7 @@ __global__ void __launch_bounds__(WF_BLOCK, WAVES) wf_finish_bvh(RtDevScene sc, 
                     int slot = 0;
                     if (!ok || e >= n) {
                         ran_out = true;
-                        if (st.call_exh && ok && e == n) // (the lane that ran the list out tells the host)
+                        if (WF_FIN_CONTINUE && st.call_exh && ok && e == n) // (the lane that ran the list out tells the host)
                             __hip_atomic_store(st.call_exh + cur % WF_CALL_RING, cur, __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_SYSTEM);
                     } else if (e < n_heavy ? (slot = (int)st.heavy_list[e], true)
@@ -1581,7 +1581,7 @@ __global__ void __launch_bounds__(WF_BLOCK, WAVES) wf_finish_bvh(RtDevScene sc, 
                 if (__any(ran_out)) {
                     // the wave's call has run its list out: on to the chain's next call if it is issued
                     uint32_t nxt = 0;
-                    if (lane == 0 && st.call_ring) {
+                    if (WF_FIN_CONTINUE && lane == 0 && st.call_ring) {
                         const unsigned long long v = __hip_atomic_load(st.call_ring + (cur + 1u) % WF_CALL_RING,
                                                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                         if ((uint32_t)(v >> 32) == cur + 1u) nxt = (uint32_t)v | 0x80000000u;
