@@ -111,7 +111,9 @@ static_assert(WF_BLOCK % WF_TBLOCK == 0 && WF_TBLOCK % 64 == 0, "WF_TBLOCK must 
 #define WF_BVH_PARK 8 // wf_finish_bvh: BVH node steps per loop trip before a lane's query parks (0: never)
 #endif
 #ifndef WF_FIN_BVH_WAVES
-#define WF_FIN_BVH_WAVES 5 // wf_finish_bvh occupancy target (5: +3 % over 6 with the 4-wide s_min query, profiles/r04)
+#define WF_FIN_BVH_WAVES 5 // wf_finish_bvh occupancy target (round 5, with parked queries: 6 -9 %; 4 equal on the bench
+                           // with 65 % less write traffic (128 VGPRs, 29 spilled vs 96 / 117), but its rocprofv3 counter
+                           // passes ran past 240 s where 5 takes 5 s — not understood: kept at 5)
 #endif
 #define WF_CALL_RING 16      // chained calls' descriptor slots (call id % WF_CALL_RING)
 #define WF_CALL_CURSORS (1u << 20) // their pixel-list cursors (call id % WF_CALL_CURSORS, epoch-tagged): a
