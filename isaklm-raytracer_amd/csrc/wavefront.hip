@@ -113,7 +113,9 @@ static_assert(WF_BLOCK % WF_TBLOCK == 0 && WF_TBLOCK % 64 == 0, "WF_TBLOCK must 
 #ifndef WF_FIN_BVH_WAVES
 #define WF_FIN_BVH_WAVES 5 // wf_finish_bvh occupancy target (round 5, with parked queries: 6 -9 %; 4 equal on the bench
                            // with 65 % less write traffic (128 VGPRs, 29 spilled vs 96 / 117), but its rocprofv3 counter
-                           // passes ran past 240 s where 5 takes 5 s — not understood: kept at 5)
+                           // passes ran past 240 s where 5 takes 5 s — not understood; re-run on the final tree:
+                           // a 16-pass counter pass finishes in 8 s, but the bench's 256-pass WRITE_SIZE pass
+                           // still runs past 240 s and the bench then reads 446: kept at 5)
 #endif
 #define WF_CALL_RING 16      // chained calls' descriptor slots (call id % WF_CALL_RING)
 #define WF_CALL_CURSORS (1u << 20) // their pixel-list cursors (call id % WF_CALL_CURSORS, epoch-tagged): a
