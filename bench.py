@@ -229,6 +229,10 @@ def _window_sums(cc_csv, trace_csv):
     return total, per_kernel, len(dispatches), kt
 
 
+PMC_PASS_LIMIT_S = 120  # a counter pass of the default bench takes 5-6 s (profiles/r05/bench_pmc_summary.json)
+PMC_SETTLE_S = 30
+
+
 def measure_pmc(args, save_dir):
     """rocprofv3 counter passes over one render call (child processes, run
     before this process initialises the GPU).  Returns a dict or an error."""
@@ -243,7 +247,7 @@ def measure_pmc(args, save_dir):
     env = dict(os.environ, TMPDIR="/tmp")
     for tag, ctrs in (("fetch", ["FETCH_SIZE"]), ("write", ["WRITE_SIZE"]), ("sq", SQ_COUNTERS)):
         d = tempfile.mkdtemp(prefix=f"rtpmc_{tag}_", dir="/tmp")
-        cmd = ["timeout", "-s", "KILL", "240", "rocprofv3", "--pmc", *ctrs, "--kernel-trace", "-d", d, "-o", "run",
+        cmd = ["timeout", "-s", "KILL", str(PMC_PASS_LIMIT_S), "rocprofv3", "--pmc", *ctrs, "--kernel-trace", "-d", d, "-o", "run",
                "--output-format", "csv", "--", sys.executable, os.path.abspath(__file__)] + child
         t = time.perf_counter()
         print(f"[bench] counter pass '{tag}' ({' '.join(ctrs)})", file=sys.stderr, flush=True)
@@ -252,7 +256,14 @@ def measure_pmc(args, save_dir):
         r = subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.PIPE, text=True)
         if r.returncode != 0:
             shutil.rmtree(d, ignore_errors=True)
-            return {"error": f"rocprofv3 {tag} pass rc={r.returncode} (its log: this run's stderr): {r.stdout[-300:]}"}
+            # (a pass killed at its limit: round 5's two such runs read 420-446 in the timed region
+            # right after it, normal rates minutes later — give the killed process's GPU work time to
+            # drain before this process starts its own)
+            print(f"[bench] counter pass '{tag}' failed (rc={r.returncode}): skipping the rest, "
+                  f"{PMC_SETTLE_S} s settle before the timed region", file=sys.stderr, flush=True)
+            time.sleep(PMC_SETTLE_S)
+            return {"error": f"rocprofv3 {tag} pass rc={r.returncode} (its log: this run's stderr): {r.stdout[-300:]}",
+                    "settle_s": PMC_SETTLE_S}
         cc, kt = _collect_csv(d, "counter_collection"), _collect_csv(d, "kernel_trace")
         try:
             total, per_kernel, ndisp, ktrace = _window_sums(cc, kt)
@@ -697,6 +708,8 @@ def main(argv=None, binding=None):
             kernel_detail["hbm_frac_per_launch"] = round(kernel_detail["hbm_GBps_per_launch"] / HBM_PEAK_GBPS, 4)
     elif pmc:
         roof["pmc_error"] = pmc["error"]
+        if "settle_s" in pmc:
+            roof["pmc_settle_s"] = pmc["settle_s"]
     roof.update({
         "definition": "achieved = counter-measured HBM bytes per sample (FETCH_SIZE x2 + WRITE_SIZE over every "
                       "dispatch of one profiled call) x timed samples/s; chip-wide, call-level",
