@@ -1844,16 +1844,7 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_check(RtDevScene sc, WfState st, 
     if (n > WF_CHECK_CAP && gtid == 0) atomicAdd(dev + RT_DEV_CHK_DROP, (unsigned long long)(n - WF_CHECK_CAP));
     n = n < WF_CHECK_CAP ? n : WF_CHECK_CAP;
     unsigned long long checked = 0, bad = 0;
-    // a small call's few records (<= 4 per wave) over the waves first (record e on wave e % waves,
-    // lane e / waves): each re-trace's node fetches nearly alone in its wave, not 64 in lockstep in
-    // the first waves (the slowest re-trace bounds the kernel, and the next chained call but one
-    // waits for it: its records reuse this parity).  More records stay contiguous per wave: rays
-    // appended together, coherent in lockstep
-    const uint32_t waves = gridDim.x * (WF_BLOCK / 64);
-    const uint32_t first = n <= 4u * waves
-                               ? (uint32_t)(tid & 63) * waves + blockIdx.x * (WF_BLOCK / 64) + (uint32_t)(tid >> 6)
-                               : (uint32_t)gtid;
-    for (uint32_t e = first; e < n; e += gridDim.x * WF_BLOCK) {
+    for (uint32_t e = gtid; e < n; e += gridDim.x * WF_BLOCK) {
         const RtF4 a = st.chk[3 * (size_t)e], b = st.chk[3 * (size_t)e + 1], q = st.chk[3 * (size_t)e + 2];
         const Vec3D o = rt_v3(a.x, a.y, a.z), d = rt_v3(b.x, b.y, b.z);
         float bx = 0.0f, by = 0.0f, bz = 0.0f;
