@@ -57,10 +57,11 @@ extern "C" {
  * check_interval / debug, RtDeviations' bounded-traversal guard fields,
  * rt_join, rt_shutdown; 7 = RtDeviations' hand-off fields (owed passes,
  * safety-net exits, stranded pixels, dropped guard records, linger
- * expiries), RT_E_INCOMPLETE from the joins, rt_profile_history.  An integrator checks
+ * expiries), RT_E_INCOMPLETE from the joins, rt_profile_history; 8 =
+ * RtDeviations.long_closed (the struct grew).  An integrator checks
  * rt_abi_version() == RT_ABI_VERSION at start-up: a binary built against an
  * older header would otherwise link (C linkage) and mis-pass arguments. */
-#define RT_ABI_VERSION 7
+#define RT_ABI_VERSION 8
 
 /* CUDA uchar4, used for texels (rt/scene.cuh:18) */
 typedef struct RtUChar4 { uint8_t x, y, z, w; } RtUChar4;
@@ -498,6 +499,9 @@ typedef struct RtOptions {
 #define RT_DEBUG_CHECK_FAULT 4 /* tests of the guard: every checked ray is recorded with a wrong result */
 #define RT_DEBUG_LONG_QUIT 8   /* tests of the failure path: the long-path kernel leaves at once, as if its
                                 * safety net fired, stranding every pixel handed to it */
+#define RT_DEBUG_SERIAL_LONG_FIRST 16 /* tests of serialised dispatch (a profiler's counter collection): the
+                                       * long-path kernel runs to its end before the path kernel starts */
+#define RT_DEBUG_SERIAL_FIN_FIRST 32  /* ... the path kernel runs to its end before the long-path kernel starts */
 
 /* Per-call kernel timing of the last rt_render on this device with
  * RtOptions.profile = 1 (wavefront kernels: HIP events on the pipelines'
@@ -560,13 +564,19 @@ typedef struct RtDeviations {
      * run); check_dropped: rays the guard sampled past its per-call record
      * capacity (not re-traced).  linger_expiries: finisher waves that stopped
      * waiting (1 s) for pixels out in the long-path kernel, which then
-     * finishes those pixels itself (a slow tail, not an error). */
+     * finishes those pixels itself (a slow tail, not an error).
+     * long_closed (ABI 8): long-path kernels that found their call's path
+     * kernel not started within their bound (a profiler serialising
+     * dispatches, a shared chip) and closed the hand-off until the next
+     * unchained call: the path kernel then runs its deep paths itself
+     * (identical results, a slower tail). */
     unsigned long long owed_pixels;
     unsigned long long owed_passes;
     unsigned long long long_safety_quits;
     unsigned long long stranded_pixels;
     unsigned long long check_dropped;
     unsigned long long linger_expiries;
+    unsigned long long long_closed;
 } RtDeviations;
 int rt_deviation_stats(RtDeviations *out, int reset);
 

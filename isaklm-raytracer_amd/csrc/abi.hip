@@ -26,7 +26,7 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
                         int pipes, int long_depth, int traversal, int overlap, int check_interval, int debug);
 
 int rt_wavefront_device_init();
-int rt_wavefront_join(void *stream);
+int rt_wavefront_join(void *stream, int consume);
 void rt_wavefront_shutdown();
 void rt_path_shutdown();
 
@@ -56,9 +56,10 @@ const char *rt_wavefront_incomplete_msg();
 // rt_wavefront_join with the ABI's status: RT_E_INCOMPLETE when the join's
 // hand-off check found stranded pixels (a chained render's frame misses
 // passes), RT_E_HIP on a HIP failure; `who` names the entry point
-static int join_status(void *stream, const char *who)
+// (consume = 0: a stranded-pixel result is left for the next reporting join)
+static int join_status(void *stream, const char *who, int consume = 1)
 {
-    const int rc = rt_wavefront_join(stream);
+    const int rc = rt_wavefront_join(stream, consume);
     if (rc == 0) return RT_OK;
     if (rc == RT_WAVEFRONT_INCOMPLETE) {
         rt_set_error("%s: %s", who, rt_wavefront_incomplete_msg());
@@ -126,12 +127,6 @@ int upload_prepared(const rt_host::PreparedHost &h, int ntris, int nindices, rt_
     dv.kd_rows = nullptr;
     dv.kd_cell = nullptr;
     dv.kd_grid = 0;
-    dv.kd_entry = nullptr;
-    dv.split_hash = nullptr;
-    for (int a = 0; a < 3; ++a) {
-        dv.split_hash_off[a] = h.split_hash_off[a];
-        dv.split_hash_mask[a] = h.split_hash_mask[a];
-    }
     for (int a = 0; a < 3; ++a) dv.kd_gscale[a] = h.kd_grid_scale[a];
     for (int a = 0; a < 4; ++a) dv.split_off[a] = h.split_off[a];
     if (h.bvh_depth >= 0 && ((rc = upload_vec(*s, h.bvh_nodes, &dv.bvh_nodes)) ||
@@ -149,12 +144,6 @@ int upload_prepared(const rt_host::PreparedHost &h, int ntris, int nindices, rt_
         return rc;
     }
     if (dv.kd_cell) dv.kd_grid = h.kd_grid;
-    // the bounded KD phase's entry: the cells' start nodes and boxes, the split hash sets
-    if (dv.kd_cell && h.bvh_depth >= 0 && !h.kd_entry.empty() && !h.split_hash.empty() &&
-        ((rc = upload_vec(*s, h.kd_entry, &dv.kd_entry)) || (rc = upload_vec(*s, h.split_hash, &dv.split_hash)))) {
-        release(s);
-        return rc;
-    }
     dv.nodes = nodes;
     dv.isect_a = a;
     dv.isect_bary = bary;
@@ -233,8 +222,9 @@ int rt_deviation_stats(RtDeviations *out, int reset)
     if (!d) { rt_set_error("rt_deviation_stats: no device block"); return RT_E_HIP; }
     unsigned long long w[RT_DEV_WORDS];
     // (chained renders joined first, so their statistics are complete; stranded
-    // pixels are not an error here: stranded_pixels reports them)
-    const int jr = join_status(nullptr, "rt_deviation_stats");
+    // pixels are not an error here — stranded_pixels reports them — and stay the
+    // next reporting join's RT_E_INCOMPLETE: rt_join, rt_download, rt_synchronize ...)
+    const int jr = join_status(nullptr, "rt_deviation_stats", 0);
     if (jr != RT_OK && jr != RT_E_INCOMPLETE) return jr;
     HIPCHK(hipDeviceSynchronize());
     HIPCHK(hipMemcpy(w, d, sizeof w, hipMemcpyDeviceToHost));
@@ -259,6 +249,7 @@ int rt_deviation_stats(RtDeviations *out, int reset)
     out->stranded_pixels = w[RT_DEV_STRANDED];
     out->check_dropped = w[RT_DEV_CHK_DROP];
     out->linger_expiries = w[RT_DEV_LINGER_EXP];
+    out->long_closed = w[RT_DEV_LONG_CLOSED];
     if (reset) HIPCHK(hipMemset(d, 0, RT_DEV_WORDS * 8));
     return RT_OK;
 }
@@ -394,7 +385,7 @@ int rt_gbuffer_create(int w, int h, uint64_t skip, G_Buffer *g)
 int rt_gbuffer_destroy(G_Buffer *g)
 {
     if (!g) return RT_E_INVALID;
-    (void)rt_wavefront_join(nullptr); // (a chained render's tail may still write it)
+    (void)rt_wavefront_join(nullptr, 0); // (a chained render's tail may still write it)
     (void)hipFree(g->frame_buffer);
     (void)hipFree(g->squared_luminance);
     (void)hipFree(g->sample_count);
@@ -479,8 +470,8 @@ int rt_gbuffer_load(const char *path, G_Buffer g, int width, int height, int *sa
     }
     // no render may still be writing this G_Buffer (a chained render's tail drained and
     // joined first; the chain is closed, so the next call does not continue it)
-    const int jr = join_status(nullptr, "rt_gbuffer_load");
-    if (jr != RT_OK && jr != RT_E_INCOMPLETE) return jr; // (the frame is overwritten anyway)
+    const int jr = join_status(nullptr, "rt_gbuffer_load", 0); // (a stranded result stays the next join's)
+    if (jr != RT_OK && jr != RT_E_INCOMPLETE) return jr;
     HIPCHK(hipDeviceSynchronize());
     HIPCHK(hipMemcpy(g.frame_buffer, buf.data(), n * 12, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(g.squared_luminance, buf.data() + n * 12, n * 4, hipMemcpyHostToDevice));
@@ -726,7 +717,7 @@ int rt_scene_prepare_counts(const Scene *ds, int node_count, int index_count, rt
 
 int rt_scene_release(rt_scene_t s)
 {
-    (void)rt_wavefront_join(nullptr); // (a chained render's tail may still read it)
+    (void)rt_wavefront_join(nullptr, 0); // (a chained render's tail may still read it)
     release(s);
     return RT_OK;
 }

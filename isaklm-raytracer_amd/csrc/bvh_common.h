@@ -14,22 +14,6 @@ RT_HD float rt_ray_margin(float ox, float oy, float oz, float scale)
     return 0x1p-16f * (fabsf(ox) + fabsf(oy) + fabsf(oz) + 2.0f * scale);
 }
 
-// The split values of an axis as an open-addressing hash set (host builds
-// it in scene_prepare.cpp, bvh_trace.h kd_bounded looks an origin up): the
-// bits of the value (-0 as +0), linear probing, RT_SPLIT_HASH_EMPTY (a NaN
-// pattern, never a split value there) marks a free slot
-#define RT_SPLIT_HASH_EMPTY 0xFFFFFFFFu
-RT_HD uint32_t rt_split_bits(float v)
-{
-    union {
-        float f;
-        uint32_t u;
-    } c;
-    c.f = v == 0.0f ? 0.0f : v;
-    return c.u;
-}
-RT_HD uint32_t rt_split_hash(uint32_t bits) { return (bits * 0x9E3779B1u) ^ (bits >> 15); }
-
 // whether v is one of the sorted values vals[lo, hi) (float ==: -0 == +0)
 RT_HD bool rt_sorted_contains(const float *vals, int lo, int hi, float v)
 {

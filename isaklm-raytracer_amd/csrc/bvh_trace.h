@@ -26,22 +26,6 @@
 
 namespace rtk {
 
-#ifdef RT_PHASE_PROF
-// phase profile (a -DRT_PHASE_PROF build, tools/phase_profile.py): per wave,
-// the s_memtime at which trace_bvh's BVH query ends (the KD phase starts)
-__device__ unsigned long long g_phase_mid[16384];
-__device__ unsigned long long g_phase_acc[8]; // wf_finish_bvh's per-phase sums (wavefront.hip)
-#define RT_PHASE_MID()                                                                                              \
-    g_phase_mid[((blockIdx.x * blockDim.x + threadIdx.x) >> 6) & 16383] = __builtin_amdgcn_s_memtime()
-#else
-#define RT_PHASE_MID()
-#endif
-#if defined(RT_LOCKSTEP_PROF) && !defined(RT_PHASE_PROF)
-// lockstep profile (a -DRT_LOCKSTEP_PROF build, tools/lockstep_profile.py): the counting
-// finisher's per-query lane steps against the wave's (wavefront.hip wf_finish_bvh)
-__device__ unsigned long long g_phase_acc[8];
-#endif
-
 // Scene data is read-only for a kernel's lifetime: loaded through the
 // constant address space (a wave-uniform address becomes a scalar load
 // through the scalar cache; a divergent one stays a vector load).
@@ -297,109 +281,6 @@ __device__ __forceinline__ float bvh4_bound(const RtDevScene &sc, Vec3D o, Vec3D
     return pk.best;
 }
 
-// Step 3's descent, given s_min, is stateless: at every split it goes to the
-// origin's side iff t < 0 or t > s_min (with entry <= s_min < exit, which
-// holds all the way down when s_min >= the scene-box entry), i.e. it walks to
-// the leaf whose interval holds s_min, with exit = min(root exit, every
-// split's t > s_min on the way) — no pop happens before that first leaf.  So
-// it may start below the root.  Per cell of a grid over the scene box the
-// host stores (build_kd_starts) the deepest KD node N whose cell holds the
-// grid cell, and N's own cell [lo, hi] (its ancestors' splits; +-inf where
-// none bounds it).  For P = o + d s_min's grid cell:
-//  * the side the rule takes at a split value v on axis a is monotone in v
-//    (t = (v - o_a) / d_a is, and the near child flips only at v = o_a),
-//    except at v == o_a with d_a > 0 (t = +0: the far, left child although
-//    the ray moves right).  So if the rule takes N's side at N's faces lo_a and
-//    hi_a, it takes it at every ancestor of N — unless o_a (d_a > 0, o_a <
-//    lo_a) is an ancestor's split value, which the axis's split hash set rules
-//    out.  The exit down to N is then min(root exit, face t > s_min) (the
-//    tightest ancestor per side is the face, by the same monotonicity);
-//  * below N the rule runs exactly as the descent would (exit tracked), to the
-//    leaf, whose test (closest = its exit) is the descent's first leaf test;
-//  * if a face check or a lookup fails, or that leaf holds no hit (the descent
-//    would pop), the descent runs from the root as before.
-// So the result is the descent's own, bit for bit; the entry saves the
-// dependent node fetches and the push / interval bookkeeping above N and
-// below it.  COUNT: the cell record counts as four node fetches (32 B), a
-// hash probe as one.
-#ifndef RT_KD_ENTER
-#define RT_KD_ENTER 0 // (measured slower on room2m: the wave still waits for its deepest lane; A/B only)
-#endif
-__device__ __forceinline__ bool split_hash_has(const RtDevScene &sc, int a, float v)
-{
-    const uint32_t bits = rt_split_bits(v), mask = sc.split_hash_mask[a];
-    const uint32_t *tbl = sc.split_hash + sc.split_hash_off[a];
-    uint32_t i = rt_split_hash(bits) & mask;
-    while (true) { // (a free slot always exists: the table is at least twice the set)
-        const uint32_t w = *(const RT_CONST uint32_t *)(tbl + i);
-        if (w == bits) return true;
-        if (w == RT_SPLIT_HASH_EMPTY) return false;
-        i = (i + 1) & mask;
-    }
-}
-
-// the rule's child at split value v on axis a: true = child1 (above the split)
-__device__ __forceinline__ bool kd_rule_above(float v, float oa, float da, float ya, float s_min, float &ex)
-{
-    const float t = rt_div_by(v - oa, da, ya); // intersect_plane (rt/trace_ray.cuh:190-210)
-    const bool near_above = oa >= v;           // ray_behind_plane (:174-188)
-    const bool go_near = t < 0 || t > s_min;
-    if (t > s_min) ex = fminf(ex, t);
-    return go_near ? near_above : !near_above;
-}
-
-// the leaf the descent reaches first and its exit, if certified (false: run the descent from the root)
-template <bool COUNT>
-__device__ __forceinline__ bool kd_entry_leaf(const RtDevScene &sc, const Vec3D o, const Vec3D d, const float yx,
-                                              const float yy, const float yz, const float s_min,
-                                              const float root_exit, uint2 &leaf, float &ex, Cnt &c)
-{
-    const int G = sc.kd_grid;
-    const float px = o.x + d.x * s_min, py = o.y + d.y * s_min, pz = o.z + d.z * s_min;
-    const float f0 = (px - sc.bmin[0]) * sc.kd_gscale[0], f1 = (py - sc.bmin[1]) * sc.kd_gscale[1],
-                f2 = (pz - sc.bmin[2]) * sc.kd_gscale[2];
-    const int c0 = f0 >= 0.0f ? (f0 < (float)(G - 1) ? (int)f0 : G - 1) : 0; // (NaN: 0)
-    const int c1 = f1 >= 0.0f ? (f1 < (float)(G - 1) ? (int)f1 : G - 1) : 0;
-    const int c2 = f2 >= 0.0f ? (f2 < (float)(G - 1) ? (int)f2 : G - 1) : 0;
-    const size_t k = ((size_t)c2 * (size_t)G + (size_t)c1) * (size_t)G + (size_t)c0;
-    const RtF4 r0 = ldc4(sc.kd_entry + 2 * k), r1 = ldc4(sc.kd_entry + 2 * k + 1);
-    if (COUNT) c.v[RT_CNT_NODE] += 4;
-    uint32_t node = __float_as_uint(r0.x);
-    if (node == 0xFFFFFFFFu) return false;
-    ex = root_exit;
-    bool ok = true;
-    // N's faces (-inf / +inf: no split bounds that side) and the origin lookups
-    const float lo[3] = {r0.y, r0.z, r0.w}, hi[3] = {r1.x, r1.y, r1.z};
-    const float oa[3] = {o.x, o.y, o.z}, da[3] = {d.x, d.y, d.z}, ya[3] = {yx, yy, yz};
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        if (lo[a] > -INFINITY) ok = ok && kd_rule_above(lo[a], oa[a], da[a], ya[a], s_min, ex);
-        if (hi[a] < INFINITY) ok = ok && !kd_rule_above(hi[a], oa[a], da[a], ya[a], s_min, ex);
-    }
-    if (!ok) return false;
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        if (da[a] > 0.0f && lo[a] > -INFINITY && oa[a] < lo[a]) {
-            if (COUNT) c.v[RT_CNT_NODE]++;
-            if (split_hash_has(sc, a, oa[a])) return false;
-        }
-    }
-    // below N: the rule itself
-    uint2 nd = ldc_u2(sc.nodes + 2 * (size_t)node);
-    if (COUNT) c.v[RT_CNT_NODE]++;
-    while ((nd.y & 3u) != RT_LEAF_TAG) {
-        const uint32_t axis = nd.y & 3u;
-        const float oax = axis == 0 ? o.x : (axis == 1 ? o.y : o.z);
-        const float dax = axis == 0 ? d.x : (axis == 1 ? d.y : d.z);
-        const float yax = axis == 0 ? yx : (axis == 1 ? yy : yz);
-        node = kd_rule_above(as_float(nd.x), oax, dax, yax, s_min, ex) ? nd.y >> 2 : node + 1;
-        nd = ldc_u2(sc.nodes + 2 * (size_t)node);
-        if (COUNT) c.v[RT_CNT_NODE]++;
-    }
-    leaf = nd;
-    return true;
-}
-
 // step 3: the reference's KD traversal with the skip bound s_min (-inf: the
 // plain traversal), from the scene box's [entry, root_exit]
 template <bool COUNT, typename STACK>
@@ -411,27 +292,6 @@ __device__ __forceinline__ int kd_bounded(const RtDevScene &sc, const Vec3D o, c
     const float yx = rt_recip_guard(d.x), yy = rt_recip_guard(d.y), yz = rt_recip_guard(d.z);
     int sp = 0;
     uint32_t node = 0;
-    if (RT_KD_ENTER && sc.kd_entry && s_min > -INFINITY && s_min >= entry) {
-        uint2 lf;
-        float ex;
-        if (kd_entry_leaf<COUNT>(sc, o, d, yx, yy, yz, s_min, root_exit, lf, ex, c)) {
-            const uint32_t count = lf.y >> 2;
-            if (count > 0 && ex > s_min) { // the descent's first leaf test (trace_leaf_node, :115-172)
-                float smallest = ex;
-                float bx = 0.0f, by = 0.0f, bz = 0.0f;
-                if (COUNT) c.v[RT_CNT_TRI] += count;
-                const int be = leaf_scan<COUNT>(sc.isect_a, sc.isect_bary, lf.x, lf.x + count, o, d, smallest, bx, by,
-                                                bz, c);
-                if (be >= 0) {
-                    if (COUNT) c.v[RT_CNT_HIT]++;
-                    hbx = bx;
-                    hby = by;
-                    hbz = bz;
-                    return (int)ldc_u2(&sc.isect_bary[be].rd).y;
-                }
-            }
-        }
-    }
     while (true) {
         uint2 nd = ldc_u2(sc.nodes + 2 * (size_t)node);
         if (COUNT) c.v[RT_CNT_NODE]++;
@@ -504,7 +364,6 @@ __device__ __forceinline__ int trace_bvh(const RtDevScene &sc, const Vec3D o, co
     float s_min = -INFINITY; // (the plain KD traversal)
     if (rt_bounded_ray(o, d, sc.split_vals, sc.split_off)) {
         s_min = RT_BVH4 ? bvh4_bound<COUNT>(sc, o, d, exit_, stk, c) : bvh_bound<COUNT>(sc, o, d, exit_, stk, c);
-        RT_PHASE_MID();
         if (!(s_min < root_exit)) return -1;
     }
     return kd_bounded<COUNT>(sc, o, d, entry, root_exit, s_min, hbx, hby, hbz, stk, c);
@@ -527,7 +386,6 @@ __device__ __forceinline__ bool trace_bvh_park(const RtDevScene &sc, const Vec3D
     if (rt_bounded_ray(o, d, sc.split_vals, sc.split_off)) {
         if (!bvh4_query<COUNT, true>(sc, o, d, exit_, stk, c, cap, resume, pk)) return false;
         s_min = pk.best;
-        RT_PHASE_MID();
         if (!(s_min < root_exit)) return true;
     }
     hit = kd_bounded<COUNT>(sc, o, d, entry, root_exit, s_min, hbx, hby, hbz, stk, c);

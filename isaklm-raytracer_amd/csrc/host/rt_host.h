@@ -77,9 +77,6 @@ struct PreparedHost {
     // the bounded KD phase's entry (bvh_trace.h kd_bounded): per grid cell
     // {start node bits, its cell's lo.xyz}, {hi.xyz, 0} (+-inf where no split
     // bounds it); and the split values per axis as open-addressing hash sets
-    std::vector<RtF4> kd_entry;
-    std::vector<uint32_t> split_hash;
-    uint32_t split_hash_off[3] = {0, 0, 0}, split_hash_mask[3] = {0, 0, 0};
     int kd_grid = 0;
     float kd_grid_scale[3] = {0, 0, 0};
 };

@@ -51,7 +51,6 @@ void build_kd_starts(PreparedHost &out, const Bounding_Box &bounds)
 {
     out.kd_rows.clear();
     out.kd_cell.clear();
-    out.kd_entry.clear();
     out.kd_grid = 0;
     if (out.nodes.empty()) return;
     std::unordered_map<uint32_t, uint32_t> row_of; // start node -> row offset
@@ -112,7 +111,6 @@ void build_kd_starts(PreparedHost &out, const Bounding_Box &bounds)
     G = G < 4 ? 4 : (G > 128 ? 128 : G);
     const float bmin[3] = {bounds.min.x, bounds.min.y, bounds.min.z};
     out.kd_cell.assign(2 * (size_t)G * G * G, 0xFFFFFFFFu);
-    out.kd_entry.assign(2 * (size_t)G * G * G, RtF4{0, 0, 0, 0});
     for (int z = 0; z < G; ++z)
         for (int y = 0; y < G; ++y)
             for (int x = 0; x < G; ++x) {
@@ -124,12 +122,8 @@ void build_kd_starts(PreparedHost &out, const Bounding_Box &bounds)
                 }
                 const size_t k = ((size_t)z * G + y) * G + x;
                 float cb[6];
-                if (!start_for(lo, hi, out.kd_cell[2 * k], out.kd_cell[2 * k + 1], cb)) {
+                if (!start_for(lo, hi, out.kd_cell[2 * k], out.kd_cell[2 * k + 1], cb))
                     out.kd_cell[2 * k] = out.kd_cell[2 * k + 1] = 0xFFFFFFFFu;
-                    for (int a = 0; a < 6; ++a) cb[a] = 0.0f;
-                }
-                out.kd_entry[2 * k] = RtF4{bitsf(out.kd_cell[2 * k]), cb[0], cb[1], cb[2]};
-                out.kd_entry[2 * k + 1] = RtF4{cb[3], cb[4], cb[5], 0.0f};
             }
     out.kd_grid = G;
     for (int a = 0; a < 3; ++a) out.kd_grid_scale[a] = (float)G / ext[a];
@@ -334,21 +328,6 @@ int prepare_host(const Triangle *tris, int ntris, const KD_Tree_Node *nodes, int
         }
         out.split_off[3] = (int)out.split_vals.size();
         if (nan_split) out.bvh_depth = -1;
-        // ... and per axis as a hash set (bvh_trace.h kd_entry_split: is an origin coordinate a split value)
-        out.split_hash.clear();
-        for (int a = 0; a < 3; ++a) {
-            uint32_t size = 16;
-            while (size < 2 * (uint32_t)ax[a].size() + 16) size *= 2;
-            out.split_hash_off[a] = (uint32_t)out.split_hash.size();
-            out.split_hash_mask[a] = size - 1;
-            out.split_hash.resize(out.split_hash.size() + size, RT_SPLIT_HASH_EMPTY);
-            uint32_t *tbl = out.split_hash.data() + out.split_hash_off[a];
-            for (float v : ax[a]) {
-                uint32_t i = rt_split_hash(rt_split_bits(v)) & (size - 1);
-                while (tbl[i] != RT_SPLIT_HASH_EMPTY) i = (i + 1) & (size - 1);
-                tbl[i] = rt_split_bits(v);
-            }
-        }
     }
 
     // --- lights: one padding entry for the xi == 1.0 draw -----

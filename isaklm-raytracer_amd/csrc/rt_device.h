@@ -59,11 +59,13 @@
 #define RT_DEV_LINGER_EXP 30  // finisher waves whose linger expired with pixels still out in wf_long
 #define RT_DEV_CHK_DROP 31    // guard records dropped past WF_CHECK_CAP (rays not re-traced)
 #define RT_DEV_STRANDED 32    // pixels found still OUT after a join's drain (wf_verify): an incomplete frame
+#define RT_DEV_LONG_CLOSED 33 // wf_long closed the hand-off ring: its call's finisher had not started (serialised
+                              // dispatch); the finisher's lanes ran their deep paths themselves
 #define RT_DEV_WORDS 48
 // rt_wavefront_join's return when its hand-off check found stranded pixels (-1: a HIP failure)
 #define RT_WAVEFRONT_INCOMPLETE (-2)
 static_assert(RT_DEV_HIST + RT_DEV_HIST_BINS <= RT_DEV_CHECKED && RT_DEV_MISRAY + 4 <= RT_DEV_OWED_PIXELS &&
-                  RT_DEV_STRANDED < RT_DEV_WORDS,
+                  RT_DEV_LONG_CLOSED < RT_DEV_WORDS,
               "deviation block");
 
 struct RtDevMaterial {          // 64 B
@@ -117,10 +119,6 @@ struct RtDevScene {
     const uint32_t *kd_cell;    // per cell of a kd_grid^3 grid over the scene box: {start node, row offset << 5 | depth}
     int kd_grid;                // cell of p: ((p - bmin) * kd_gscale), clamped to [0, kd_grid - 1]
     float kd_gscale[3];
-    // the bounded KD phase's entry (bvh_trace.h kd_bounded); nullptr: none
-    const RtF4 *kd_entry;       // per cell: {start node bits, its cell's lo.xyz}, {hi.xyz, 0}
-    const uint32_t *split_hash; // per axis a hash set of the split values (bvh_common.h rt_split_hash)
-    uint32_t split_hash_off[3], split_hash_mask[3];
 };
 
 // BVH child reference: an inner node's index, or RT_BVH_LEAF | first << 3 |

@@ -86,6 +86,8 @@ static_assert(WF_BLOCK % WF_TBLOCK == 0 && WF_TBLOCK % 64 == 0, "WF_TBLOCK must 
 #ifndef WF_FIN_QUIET_TRIPS
 #define WF_FIN_QUIET_TRIPS 4096u // ... while wf_long ran a path within this many of their idle loop trips
 #endif
+#define WF_FIN_LINGER_TRIPS 1000000u // ... and for at most this many idle loop trips in all (a bound that holds
+                                     // where s_memrealtime stands still: rocprofv3 counter collection)
 #ifndef WF_FIN_OCC
 #define WF_FIN_OCC 1 // wf_finish_coop occupancy floor (1: the compiler's choice, 2 waves/SIMD; 3: no change)
 #endif
@@ -117,25 +119,10 @@ static_assert(WF_BLOCK % WF_TBLOCK == 0 && WF_TBLOCK % 64 == 0, "WF_TBLOCK must 
                            // a 16-pass counter pass finishes in 8 s, but the bench's 256-pass WRITE_SIZE pass
                            // still runs past 240 s and the bench then reads 446: kept at 5)
 #endif
-#define WF_CALL_RING 16      // chained calls' descriptor slots (call id % WF_CALL_RING)
-#define WF_CALL_CURSORS (1u << 20) // their pixel-list cursors (call id % WF_CALL_CURSORS, epoch-tagged): a
-                                   // wave would have to lag 2^20 calls behind to meet a reused one
-#define WF_CALLS_IN_FLIGHT 8 // a call is issued once the call this many before it has run its list out
-#ifndef WF_FIN_CONTINUE
-// chained calls: 0 = their finishers run one after the other on pipeline 0 (a kernel boundary
-// between calls: a pixel's state crosses it for free); 1 = a finisher goes on with the chain's
-// next issued calls (no tail between calls, but every pixel let go needs an agent-scope release,
-// and a claimer on another XCD may share the pixel's cache lines with a third: measured slower
-// and, with write-through publication, not exact — profiles/r05/overlap_ab.md)
-#define WF_FIN_CONTINUE 0
-#endif
-#ifndef WF_FIN_PUBLISH
-#define WF_FIN_PUBLISH 0 // (WF_FIN_CONTINUE) a pixel let go: 0 = release fence; 1 = state re-stored write-through
-#endif
-#ifndef WF_FIN_ALT
-#define WF_FIN_ALT 0 // chained finishers alternate between pipelines 0 and 2 (0: all on pipeline 0 — the
-                     // running one takes the later calls' pixels; a second one beside it competes for them)
-#endif
+// (chained calls' finishers run one after the other on pipeline 0: a kernel boundary between calls,
+// which a pixel's state crosses for free.  The round-5 variants — a finisher going on with the next
+// issued call, finishers alternating between two streams — measured slower, one of them inexact,
+// and are gone: DESIGN.md §6 keeps their A/B records)
 #ifndef WF_FIN_SMALL_WAVES
 #define WF_FIN_SMALL_WAVES 3 // frames of at most this many finisher waves per SIMD take the unspilled build (151 VGPRs: 3 waves)
 #endif
@@ -157,25 +144,52 @@ static_assert(WF_BLOCK % WF_TBLOCK == 0 && WF_TBLOCK % 64 == 0, "WF_TBLOCK must 
 #ifndef WF_LONG_BLOCKS
 #define WF_LONG_BLOCKS 64 // wf_long grid (4 waves each, one path per wave at a time)
 #endif
-// safety nets of wf_long's claim loop (s_memrealtime ticks, 100 MHz), never
-// reached by a working protocol.  Every other wait there is bounded by the
-// protocol itself: while its producers (the finisher waves of its call) live,
-// while another wave runs a path (bounded by that path's watchdog), or while
-// hand-off entries keep coming, the idle clock does not run; once none of
-// these holds, a persistent wave leaves within the chain window (50 ms) and a
-// slice wave at once.  What is left for the nets: an entry reserved but never
-// published (WF_LONG_PUBLISH_WAIT) and a broken chain flag (WF_LONG_IDLE).
-// A net exit with entries unclaimed strands pixels instead of hanging the GPU
-// — counted (RT_DEV_LONG_QUIT), found by the join's wf_verify and reported.
+// Cross-kernel waits (finisher <-> wf_long).  No kernel may wait for work of
+// a kernel that is not resident: under rocprofv3 counter collection the
+// dispatches are serialised (either kernel may run first, alone), and a shared
+// chip may delay either one.  So every such wait is bounded by a count of the
+// waiting loop's trips — s_memrealtime stands still under counter collection
+// (ae07d5e), so the clock bounds below are a second, faster exit, never the
+// only one — and a bound that expires leaves the protocol in a state the
+// other side completes on its own:
+//  * wf_long waits for its call's finisher only once a finisher wave has
+//    started (WF_FIN_STARTED).  Before that it waits at most
+//    WF_LONG_START_TRIPS idle trips, then CLOSES the hand-off ring
+//    (WF_LONG_CLOSED in the reserved counter, set only while every reserved
+//    entry is claimed) and leaves: the finisher's hand-offs then fail and its
+//    lanes run their deep paths to the end themselves (the same shade_step
+//    sequence: bit-identical).  The ring stays closed until the next call
+//    that does not continue a chain resets it (RT_DEV_LONG_CLOSED counts it);
+//  * a finisher lingers for pixels out in wf_long at most WF_FIN_QUIET_TRIPS
+//    trips while no wf_long wave runs a path, and at most st.linger ticks;
+//  * a finisher claims a return wf_long reserved only while wf_long is
+//    resident (it reserves while running); its wait for the entry's
+//    publication is bounded by WF_SPIN_TRIPS (expired: the pixel is left out,
+//    found by wf_verify, RT_E_INCOMPLETE);
+//  * the safety nets of wf_long's claim loop, never reached by a working
+//    protocol: an entry reserved but never published (WF_LONG_PUBLISH_TRIPS /
+//    _WAIT) and nothing left that could bring work (WF_LONG_IDLE_TRIPS /
+//    WF_LONG_IDLE).  A net exit with entries unclaimed strands pixels instead
+//    of hanging the GPU — counted (RT_DEV_LONG_QUIT), found by the join's
+//    wf_verify and reported.
+// (A trip of these loops is an s_sleep plus 2-4 L2 atomics: ~1-2 us.)
+#define WF_FIN_STARTED 0x80000000u        // fin_live: a finisher wave of the call has started
+#define WF_LONG_CLOSED 0x80000000u        // long_ctr[0]: the ring takes no more hand-offs
+#define WF_LONG_START_TRIPS 20000u        // idle trips before wf_long closes the ring on an unstarted finisher
 #define WF_LONG_IDLE 200000000ull         // 2 s idle with nothing that could still bring work
+#define WF_LONG_IDLE_TRIPS 2000000u       // ... or this many trips
 #define WF_LONG_PUBLISH_WAIT 100000000ull // 1 s on one reserved, unpublished entry (publication is ~1 us)
+#define WF_LONG_PUBLISH_TRIPS 1000000u    // ... or this many trips
+#define WF_SPIN_TRIPS (1u << 24)          // a finisher lane's wait for a reserved return's publication
 // an idle persistent wf_long wave of an open chain stays until no entry has
-// been reserved (for any wave) for this long (50 ms) AND no wave runs a path:
-// the next calls' deep paths (WfState.chain_flag).  The grid leaves as a whole
-// — one whose idle waves left while a few ran 10^4-bounce samples on (a call's
-// tail can go 50 ms without a hand-off) served the next calls with those few
-// waves, its stream-queued successor blocked behind them.
+// been reserved (for any wave) for this long (50 ms, or WF_LONG_CHAIN_TRIPS
+// trips) AND no wave runs a path: the next calls' deep paths
+// (WfState.chain_flag).  The grid leaves as a whole — one whose idle waves
+// left while a few ran 10^4-bounce samples on (a call's tail can go 50 ms
+// without a hand-off) served the next calls with those few waves, its
+// stream-queued successor blocked behind them.
 #define WF_LONG_CHAIN_IDLE 5000000ull
+#define WF_LONG_CHAIN_TRIPS 50000u
 // RtOptions.check_interval: 1 ray in this many re-traced by the KD traversal
 // (a KD re-trace costs ~50 bounded queries: 1024 took 4 % of a 256-pass
 // room2m call, 4096 ~1 %, and still checks ~2M rays in the 20-step bench)
@@ -213,7 +227,7 @@ struct WfState {
     // pipeline for the concurrently running wf_long kernel through a ring of
     // long_cap entries: entry e (counted from the last reset) lives at e %
     // long_cap, published as long_ent = (e + 1) << 32 | slot after its ray
-    uint32_t *long_ctr;   // [0] entries reserved, [1] entries claimed, [3] paths running in wf_long
+    uint32_t *long_ctr;   // [0] entries reserved (| WF_LONG_CLOSED), [1] entries claimed, [3] paths running in wf_long
     unsigned long long *long_ent;
     RtF4 *long_ray;       // 2 per ring slot
     int long_depth;       // 0 = off
@@ -226,8 +240,10 @@ struct WfState {
     unsigned long long *long_log; // debug (RT_DEBUG_LONG_LOG): [0] call start, then per claim {claim, end, bounces, slot}
     // ret_ctr: u64 [0] = finisher waves alive << 32 | returns reserved (wf_long
     // reserves only while a finisher wave is alive; a wave leaves only when
-    // every reserved return is claimed: no pixel is stranded, and neither
-    // kernel ever waits for the other — they may share a hardware queue);
+    // every reserved return is claimed: no pixel is stranded.  The finisher
+    // never waits for a wf_long that is not resident: returns are reserved by
+    // a running wf_long wave, and lingering is bounded — see the cross-kernel
+    // waits above);
     // u32 [2] = returns claimed, u32 [3] = pixels out (handed to wf_long, not
     // yet returned or done): an idle finisher wave lingers (s_sleep) while
     // pixels are out — for at most `linger` ticks (0 for chained calls, whose
@@ -243,25 +259,16 @@ struct WfState {
     // no list (the tiles only)
     uint8_t *heavy;
     uint32_t *listed, *heavy_list, *heavy_n;
-    // the whole-call finisher takes this call's pixels itself (no wf_start, no path list):
-    // fresh = 1; concurrent = 1 when the next chained call's finisher may run beside this
-    // one (a pixel is released with a release fence and marked RT_PX_REL)
-    int fresh, concurrent;
+    // the whole-call finisher takes this call's pixels itself (no wf_start, no path list): fresh = 1
+    int fresh;
     uint32_t fresh_n; // (fresh) entries: 256 per 16x16-pixel tile (fresh_pixel); 0 for a chain's drain
     unsigned long long *span; // RtOptions.profile: {first wave start, last wave end} (s_memrealtime)
-    // chained calls (RtOptions.overlap): a finisher whose call's pixel list has run out goes on
-    // with the next call of the chain, if the host has issued it — so a chain runs without a
-    // kernel boundary between its calls, and the finisher launched by a later call only adds
-    // lanes.  call_id: this launch's call; call_ring (pinned host memory): issued calls,
-    // slot id % WF_CALL_RING = id << 32 | passes; call_ctr: per call (id % WF_CALL_CURSORS),
-    // id << 32 | entries taken of its pixel list (epoch-tagged: the call's first lane claims it);
-    // call_exh (pinned host memory): a call's id once its list ran out (the host's bound on
-    // calls in flight).  nullptr: an unchained call (its list is counts[4] of fresh_n).
-    uint32_t call_id;
-    unsigned long long *call_ring, *call_ctr;
-    uint32_t *call_exh;
-    // the persistent wf_long's producers: finisher waves of its call not yet
-    // past their last hand-off (nullptr: wf_long runs in host-kicked slices)
+    uint32_t call_id; // this launch's call (heavy-pixel list tags)
+    // the persistent wf_long's producers: the host sets the word to the finisher's wave count;
+    // each finisher wave sets WF_FIN_STARTED when it starts and subtracts 1 once past its last
+    // hand-off (nullptr: wf_long runs in host-kicked slices).  wf_long waits for producers only
+    // once one has started: a finisher not yet dispatched (counter collection serialises
+    // dispatches) is never waited for
     uint32_t *fin_live;
     // 1 while a chain of calls is open (set by chained calls, cleared by its
     // drain): an idle persistent wf_long wave then stays up to WF_LONG_CHAIN_IDLE
@@ -277,6 +284,7 @@ struct WfState {
     RtF4 *chk;
     uint32_t *chk_ctr;
     uint32_t chk_mask;
+    uint32_t chk_cap; // records per parity (more are dropped: RT_DEV_CHK_DROP)
     int chk_fault; // (RT_DEBUG_CHECK_FAULT, tests: record a wrong result for every checked ray)
     int debug_quit; // (RT_DEBUG_LONG_QUIT, tests: wf_long leaves at once, as by its safety net)
 };
@@ -351,8 +359,8 @@ __device__ __forceinline__ void publish_long(const WfState &st, bool to_long, ui
 // with one compare-and-swap that never laps an unclaimed entry (a pixel can be
 // handed over several times per call when wf_long returns it after each deep
 // sample, and chained calls keep the ring running).  Returns false
-// (wave-uniform) when the entries would not fit: the lanes then keep their
-// paths.  The path state is stored by the caller first; the pixel is OUT
+// (wave-uniform) when the entries would not fit or the ring is closed: the
+// lanes then keep their paths.  The path state is stored by the caller first; the pixel is OUT
 // (pxo) from here until a finisher takes it back or wf_long finishes it.
 __device__ __forceinline__ bool publish_long_capped(const WfState &st, bool to_long, uint32_t slot, Vec3D o, Vec3D d)
 {
@@ -365,7 +373,9 @@ __device__ __forceinline__ bool publish_long_capped(const WfState &st, bool to_l
         uint32_t r = __hip_atomic_load(st.long_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         while (true) {
             const uint32_t c = __hip_atomic_load(st.long_ctr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (r + k - c > st.long_cap) break; // (c may be stale-low: conservative)
+            // closed (wf_long left: see WF_LONG_CLOSED), the count's 31 bits used up, or a lap of an
+            // unclaimed entry (c may be stale-low: conservative): the lanes keep their paths
+            if ((r & WF_LONG_CLOSED) || r + k >= WF_LONG_CLOSED || r + k - c > st.long_cap) break;
             if (__hip_atomic_compare_exchange_strong(st.long_ctr, &r, r + k, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                      __HIP_MEMORY_SCOPE_AGENT)) {
                 base = r;
@@ -1372,27 +1382,23 @@ __global__ void __launch_bounds__(WF_BLOCK, WAVES) wf_finish_bvh(RtDevScene sc, 
     const int lane = __lane_id();
     unsigned long long *const ret_word = reinterpret_cast<unsigned long long *>(st.ret_ctr);
     uint32_t *const ret_claimed = st.ret_ctr + 2;
-    if (st.long_return && lane == 0) // this wave is alive: wf_long may return pixels to it
-        __hip_atomic_fetch_add(ret_word, 1ull << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (lane == 0) {
+        // the call's finisher has started: from here wf_long waits for its producers (WF_FIN_STARTED)
+        if (st.fin_live && !(__hip_atomic_load(st.fin_live, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & WF_FIN_STARTED))
+            __hip_atomic_fetch_or(st.fin_live, WF_FIN_STARTED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (st.long_return) // this wave is alive: wf_long may return pixels to it
+            __hip_atomic_fetch_add(ret_word, 1ull << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (st.span) atomicMin(st.span, __builtin_amdgcn_s_memrealtime());
         if (st.long_log && blockIdx.x == 0 && threadIdx.x == 0) st.long_log[0] = __builtin_amdgcn_s_memrealtime();
     }
-#ifdef RT_PHASE_PROF
-    // wave-time per phase (s_memtime, scalar): loop overhead, BVH query, KD phase, shading + guard + hand-off;
-    // iterations and active lanes at the ray query
-    unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    const int wid = ((blockIdx.x * blockDim.x + threadIdx.x) >> 6) & 16383;
-#endif
     PathRegs p;
     p.slot = 0;
     p.ro = p.rd = rt_v3(0, 0, 0);
     bool active = false, exhausted = false; // exhausted: this lane found the path list empty
     bool rel = false;                       // (fresh) the lane's pixel has no passes left: let it go
-    // (fresh) the wave's call: this launch's, then the chain's later issued calls
-    uint32_t cur = st.call_id, cur_passes = (uint32_t)fr.passes;
     unsigned long long idle_since = 0;      // (lane 0) when the wave first had nothing to do
     uint32_t quiet_trips = 0;               // (lane 0) idle loop trips in a row with no wf_long path running
+    uint32_t idle_trips = 0;                // (lane 0) idle loop trips in a row
     bool seated = false;                    // (lane 0) holds a linger seat
 #if WF_BVH_PARK
     // a lane whose s_min query ran WF_BVH_PARK node steps parks it (its state in LDS, the stack in
@@ -1403,38 +1409,14 @@ __global__ void __launch_bounds__(WF_BLOCK, WAVES) wf_finish_bvh(RtDevScene sc, 
     bool parked = false;
 #endif
     while (true) {
-#ifdef RT_PHASE_PROF
-        const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-#endif
         // (fresh) pixels whose passes are done are let go — unless a later chained call queued
-        // passes for them meanwhile: those run next, in the pixel's order (its state is this lane's)
+        // passes for them meanwhile: those run next, in the pixel's order (its state is this lane's).
+        // (The next claimer is a later launch — chained finishers run one after the other — whose
+        // kernel boundary orders this lane's stores before its loads.)
         while (st.fresh && __any(rel)) {
-            if (!WF_FIN_PUBLISH && st.concurrent) { // (A/B: every dirty line of the XCD's L2 written back)
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
             if (rel) {
-                if (WF_FIN_PUBLISH && st.concurrent) {
-                    // the pixel's state — its 24 bytes, all a later claimer reads (with sc1 loads) —
-                    // re-stored write-through (sc1) and drained before the word says it is free: a
-                    // claimer on another XCD reads them from memory, without a write-back of the
-                    // whole L2 (MI355X_MICROARCH.md, visibility: sc1 payload, drained, atomic flag)
-                    uint32_t *f3 = reinterpret_cast<uint32_t *>(fr.fb + p.slot);
-                    const uint32_t a0 = f3[0], a1 = f3[1], a2 = f3[2];
-                    const uint32_t sqb = *reinterpret_cast<const uint32_t *>(fr.sq + p.slot);
-                    const uint32_t cnb = *reinterpret_cast<const uint32_t *>(fr.count + p.slot);
-                    st_sc1(f3, a0);
-                    st_sc1(f3 + 1, a1);
-                    st_sc1(f3 + 2, a2);
-                    st_sc1(reinterpret_cast<uint32_t *>(fr.sq + p.slot), sqb);
-                    st_sc1(reinterpret_cast<uint32_t *>(fr.count + p.slot), cnb);
-                    st_sc1(fr.rng + p.slot, p.rng);
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                }
                 uint32_t x = RT_PX_BUSY;
-                if (__hip_atomic_compare_exchange_strong(st.pxo + p.slot, &x, st.concurrent ? RT_PX_REL : 0u,
-                                                         __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                if (__hip_atomic_compare_exchange_strong(st.pxo + p.slot, &x, 0u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                          __HIP_MEMORY_SCOPE_AGENT)) {
                     rel = false;
                 } else {
@@ -1488,25 +1470,37 @@ __global__ void __launch_bounds__(WF_BLOCK, WAVES) wf_finish_bvh(RtDevScene sc, 
                 got = (uint32_t)__shfl((int)got, leader);
                 const uint32_t rank = (uint32_t)__popcll(im & ((1ull << lane) - 1ull));
                 if (idle && rank < got) {
+                    // reserved by a running wf_long wave, which publishes it right after (store
+                    // in flight): a bounded wait — expired, the pixel stays out (wf_verify
+                    // reports it stranded) rather than the wave spinning on
                     const uint32_t e = base + rank;
-                    unsigned long long v;
-                    do { // reserved by wf_long, its store may still be in flight
+                    unsigned long long v = 0;
+                    bool pub = false;
+                    for (uint32_t spin = 0; spin < WF_SPIN_TRIPS; ++spin) {
                         v = __hip_atomic_load(st.ret_ring + e % st.long_cap, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    } while ((uint32_t)(v >> 32) != e + 1u);
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                    __hip_atomic_fetch_sub(st.ret_ctr + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    active = true;
-                    first_ray(st, fr, (uint32_t)v, p);
-                    // back from wf_long: no longer OUT but BUSY (this lane's); plus the passes chained
-                    // calls queued meanwhile
-                    const uint32_t owed = __hip_atomic_exchange(st.pxo + (uint32_t)v, RT_PX_BUSY, __ATOMIC_RELAXED,
-                                                                __HIP_MEMORY_SCOPE_AGENT);
-                    p.passes_left += (int)(owed & RT_PX_PASSES);
-                    if (owed & RT_PX_PASSES) { // (RT_DEBUG_CALL_LOG: most passes owed, pixels owed; RtDeviations)
-                        __hip_atomic_fetch_max(st.ret_ctr + 5, owed & RT_PX_PASSES, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        __hip_atomic_fetch_add(st.ret_ctr + 6, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        atomicAdd(fr.dev_stats + RT_DEV_OWED_PIXELS, 1ull);
-                        atomicAdd(fr.dev_stats + RT_DEV_OWED_PASSES, (unsigned long long)(owed & RT_PX_PASSES));
+                        pub = (uint32_t)(v >> 32) == e + 1u;
+                        if (pub) break;
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+                    if (!pub) {
+                        atomicAdd(fr.dev_stats + RT_DEV_LONG_QUIT, 1ull);
+                    } else {
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                        __hip_atomic_fetch_sub(st.ret_ctr + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        active = true;
+                        first_ray(st, fr, (uint32_t)v, p);
+                        // back from wf_long: no longer OUT but BUSY (this lane's); plus the passes chained
+                        // calls queued meanwhile
+                        const uint32_t owed = __hip_atomic_exchange(st.pxo + (uint32_t)v, RT_PX_BUSY, __ATOMIC_RELAXED,
+                                                                    __HIP_MEMORY_SCOPE_AGENT);
+                        p.passes_left += (int)(owed & RT_PX_PASSES);
+                        if (owed & RT_PX_PASSES) { // (RT_DEBUG_CALL_LOG: most passes owed, pixels owed; RtDeviations)
+                            __hip_atomic_fetch_max(st.ret_ctr + 5, owed & RT_PX_PASSES, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+                            __hip_atomic_fetch_add(st.ret_ctr + 6, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            atomicAdd(fr.dev_stats + RT_DEV_OWED_PIXELS, 1ull);
+                            atomicAdd(fr.dev_stats + RT_DEV_OWED_PASSES, (unsigned long long)(owed & RT_PX_PASSES));
+                        }
                     }
                 }
             }
@@ -1517,54 +1511,27 @@ __global__ void __launch_bounds__(WF_BLOCK, WAVES) wf_finish_bvh(RtDevScene sc, 
             // lane or wf_long —, which then owes it this call's passes and runs them next
             // (a lane that found the list run out stays out: idle trips must not keep adding to
             // the cursor — a lingering wave's trips wrapped it past 2^32 and re-ran the call's
-            // pixels.  Continuation mode: a later issued call may still have pixels for it.)
-            if (WF_FIN_CONTINUE && st.call_ring) exhausted = false;
+            // pixels)
             bool claim = !active && !rel && !exhausted, started = false, acq = false;
-            uint32_t my_passes = 0, my_call = 0;
             while (__any(claim)) {
                 const unsigned long long m = __ballot(claim);
                 const int leader = __ffsll((long long)m) - 1;
                 uint32_t base = 0;
-                int ok = 1;
-                if (lane == leader) {
-                    if (WF_FIN_CONTINUE && st.call_ctr) { // the wave's call's cursor, claimed for it by its first user
-                        unsigned long long *ctr = st.call_ctr + cur % WF_CALL_CURSORS;
-                        unsigned long long v = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        while ((uint32_t)(v >> 32) < cur &&
-                               !__hip_atomic_compare_exchange_strong(ctr, &v, (unsigned long long)cur << 32,
-                                                                     __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                                     __HIP_MEMORY_SCOPE_AGENT)) {
-                        }
-                        if ((uint32_t)(v >> 32) > cur) {
-                            ok = 0; // (a later call holds the slot: a wave 2^20 calls behind)
-                        } else {
-                            const unsigned long long o = __hip_atomic_fetch_add(
-                                ctr, (unsigned long long)__popcll(m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                            base = (uint32_t)o;
-                            ok = (uint32_t)(o >> 32) == cur;
-                        }
-                    } else {
-                        base = atomicAdd(fetch, (uint32_t)__popcll(m));
-                    }
-                }
+                if (lane == leader) base = atomicAdd(fetch, (uint32_t)__popcll(m));
                 base = __shfl(base, leader);
-                ok = __shfl(ok, leader);
-                bool ran_out = false;
                 if (claim) {
                     const uint32_t e = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
                     int slot = 0;
-                    if (!ok || e >= n) {
-                        ran_out = true;
-                        if (WF_FIN_CONTINUE && st.call_exh && ok && e == n) // (the lane that ran the list out tells the host)
-                            __hip_atomic_store(st.call_exh + cur % WF_CALL_RING, cur, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_SYSTEM);
+                    if (e >= n) {
+                        claim = false;
+                        exhausted = true;
                     } else if (e < n_heavy ? (slot = (int)st.heavy_list[e], true)
                                            : fresh_pixel(fr, e - n_heavy, slot) &&
                                                  !(st.heavy_list && st.listed[slot] == st.call_id)) {
                         uint32_t x = __hip_atomic_load(st.pxo + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         while (true) {
                             if (x & (RT_PX_OUT | RT_PX_BUSY)) { // held: owed this call's passes
-                                if (__hip_atomic_compare_exchange_strong(st.pxo + slot, &x, x + cur_passes,
+                                if (__hip_atomic_compare_exchange_strong(st.pxo + slot, &x, x + (uint32_t)fr.passes,
                                                                          __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                                          __HIP_MEMORY_SCOPE_AGENT))
                                     break;
@@ -1573,39 +1540,20 @@ __global__ void __launch_bounds__(WF_BLOCK, WAVES) wf_finish_bvh(RtDevScene sc, 
                                                                             __HIP_MEMORY_SCOPE_AGENT)) {
                                 claim = false;
                                 started = true;
-                                acq = (x & RT_PX_REL) != 0u; // (released by a concurrent holder)
-                                my_passes = cur_passes;
-                                my_call = cur;
+                                acq = (x & RT_PX_REL) != 0u; // (released by wf_long, which runs beside this)
                                 p.slot = (uint32_t)slot;
                                 break;
                             }
                         }
                     }
                 }
-                if (__any(ran_out)) {
-                    // the wave's call has run its list out: on to the chain's next call if it is issued
-                    uint32_t nxt = 0;
-                    if (WF_FIN_CONTINUE && lane == 0 && st.call_ring) {
-                        const unsigned long long v = __hip_atomic_load(st.call_ring + (cur + 1u) % WF_CALL_RING,
-                                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                        if ((uint32_t)(v >> 32) == cur + 1u) nxt = (uint32_t)v | 0x80000000u;
-                    }
-                    nxt = (uint32_t)__builtin_amdgcn_readfirstlane((int)nxt);
-                    if (nxt) {
-                        ++cur;
-                        cur_passes = nxt & 0x7FFFFFFFu;
-                    } else if (ran_out) {
-                        claim = false;
-                        exhausted = true;
-                    }
-                }
             }
-            // (a pixel whose last holder ran concurrently with this finisher — wf_long, or a
-            // chained finisher — released its stores with plain stores + an agent release before
-            // the word said free (REL / LONGDONE): read them after an agent acquire.  sc1 loads
-            // alone are no acquire for plain-stored bytes (MI355X_MICROARCH.md, Valid forms): this
-            // XCD's L2 may hold the line from a neighbouring pixel read earlier.  A pixel last held
-            // by an earlier launch needs none: the launch boundary is the release / acquire.)
+            // (a pixel whose last holder was wf_long, running beside this finisher, was released with
+            // plain stores + an agent release before the word said free (LONGDONE): read it after an
+            // agent acquire.  sc1 loads alone are no acquire for plain-stored bytes
+            // (MI355X_MICROARCH.md, Valid forms): this XCD's L2 may hold the line from a neighbouring
+            // pixel read earlier.  A pixel last held by an earlier launch needs none: the launch
+            // boundary is the release / acquire.)
             if (__any(acq)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             if (started) { // the pixel's state and its first pass (wf_start's)
                 const uint32_t slot = p.slot;
@@ -1613,7 +1561,7 @@ __global__ void __launch_bounds__(WF_BLOCK, WAVES) wf_finish_bvh(RtDevScene sc, 
                 Vec3D fb = rt_v3(0.0f, 0.0f, 0.0f);
                 float sq = 0.0f;
                 int count = 0;
-                if (fr.reset && my_call == st.call_id) { // reset_frame (rt/render.cuh:18-34)
+                if (fr.reset) { // reset_frame (rt/render.cuh:18-34)
                     fr.fb[slot] = fb;
                     fr.sq[slot] = sq;
                     fr.count[slot] = count;
@@ -1623,7 +1571,7 @@ __global__ void __launch_bounds__(WF_BLOCK, WAVES) wf_finish_bvh(RtDevScene sc, 
                     sq = __uint_as_float(ld_sc1(reinterpret_cast<const uint32_t *>(fr.sq + slot)));
                     count = (int)ld_sc1(reinterpret_cast<const uint32_t *>(fr.count + slot));
                 }
-                p.passes_left = (int)my_passes;
+                p.passes_left = fr.passes;
                 if (start_sample<COUNT>(fr, cam, (int)slot, p.passes_left, p.rng, fb, sq, count, p.ro, p.rd, c)) {
                     begin_path(p);
                     active = true;
@@ -1657,18 +1605,19 @@ __global__ void __launch_bounds__(WF_BLOCK, WAVES) wf_finish_bvh(RtDevScene sc, 
                 break;
             }
             // leave only while every reserved return is claimed (else: claim them next round), and
-            // while pixels are out in wf_long linger for them (bounded: st.linger)
+            // while pixels are out in wf_long linger for them — bounded: st.linger ticks, and
+            // WF_FIN_QUIET_TRIPS trips with no wf_long path running (where wf_long cannot run
+            // beside the finisher — counter collection serialises the two launches — lingering
+            // would only hold the finisher's end, and the next launch, up), WF_FIN_LINGER_TRIPS in all
             int leave = 0;
             if (lane == 0) {
                 if (idle_since == 0) idle_since = __builtin_amdgcn_s_memrealtime();
-                // linger only while wf_long runs paths that may come back: where it cannot run beside
-                // the finisher (rocprofv3 counter collection serialises the two launches) lingering
-                // would only hold the finisher's end — and the next launch — up by st.linger per wave
                 if (__hip_atomic_load(st.long_ctr + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
                     ++quiet_trips;
                 else
                     quiet_trips = 0;
-                bool out = st.linger != 0 && quiet_trips < WF_FIN_QUIET_TRIPS &&
+                ++idle_trips;
+                bool out = quiet_trips < WF_FIN_QUIET_TRIPS && idle_trips < WF_FIN_LINGER_TRIPS &&
                            __hip_atomic_load(st.ret_ctr + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
                 // only WF_FIN_LINGER_WAVES waves linger (a seat each, kept until they leave): the
                 // others leave their slots to wf_long, which the deep paths are waiting for
@@ -1696,28 +1645,10 @@ __global__ void __launch_bounds__(WF_BLOCK, WAVES) wf_finish_bvh(RtDevScene sc, 
         }
         idle_since = 0;
         quiet_trips = 0;
+        idle_trips = 0;
         bool to_long = false;
-#ifdef RT_LOCKSTEP_PROF
-        uint32_t lk_db = 0, lk_dk = 0;
-        unsigned long long lk_t = 0;
-        const unsigned long long lk_act = (unsigned long long)__popcll(__ballot(active));
-#endif
-#ifdef RT_PHASE_PROF
-        const unsigned long long t1 = __builtin_amdgcn_s_memtime();
-        ph[0] += t1 - t0;
-        ph[4] += 1;
-        ph[5] += (unsigned long long)__popcll(__ballot(active));
-        g_phase_mid[wid] = 0;
-#endif
         if (active) {
             float bx = 0.0f, by = 0.0f, bz = 0.0f;
-#ifdef RT_LOCKSTEP_PROF
-            // the query's lane steps (BVH nodes + plane batches of 4, KD nodes + batches) against the
-            // wave's: the BVH phase and the KD phase each run until the wave's slowest lane is done
-            const unsigned long long lb0 = c.v[RT_CNT_B_BVH_NODE] * 4 + c.v[RT_CNT_B_BVH_TRI],
-                                     lk0 = c.v[RT_CNT_NODE] * 4 + c.v[RT_CNT_TRI];
-            const unsigned long long lt0 = __builtin_amdgcn_s_memtime();
-#endif
 #if WF_BVH_PARK
             int hit;
             BvhPark pk{0u, 0, 0.0f};
@@ -1733,22 +1664,6 @@ __global__ void __launch_bounds__(WF_BLOCK, WAVES) wf_finish_bvh(RtDevScene sc, 
             const int hit = trace_bvh<COUNT>(sc, p.ro, p.rd, bx, by, bz, stk, c);
             const bool done = true;
 #endif
-#ifdef RT_LOCKSTEP_PROF
-            lk_t = __builtin_amdgcn_s_memtime() - lt0;
-            lk_db = (uint32_t)((c.v[RT_CNT_B_BVH_NODE] * 4 + c.v[RT_CNT_B_BVH_TRI] - lb0 + 3) / 4);
-            lk_dk = (uint32_t)((c.v[RT_CNT_NODE] * 4 + c.v[RT_CNT_TRI] - lk0 + 3) / 4);
-#endif
-#ifdef RT_PHASE_PROF
-            {
-                const unsigned long long t2 = __builtin_amdgcn_s_memtime();
-                const unsigned long long tm = g_phase_mid[wid];
-                const unsigned long long mid = tm > t1 && tm < t2 ? tm : t1;
-                ph[1] += mid - t1;
-                ph[2] += t2 - mid;
-                ph[6] += (unsigned long long)__popcll(__ballot(true));
-            }
-            const unsigned long long t2s = __builtin_amdgcn_s_memtime();
-#endif
             // run-time exactness guard: a deterministic sample of the rays, with the
             // bounded result, is queued for wf_check's plain KD re-trace
             if (!COUNT && st.chk && done) {
@@ -1760,7 +1675,7 @@ __global__ void __launch_bounds__(WF_BLOCK, WAVES) wf_finish_bvh(RtDevScene sc, 
                 const bool rec = (h & st.chk_mask) == 0u;
                 if (__any(rec)) {
                     const uint32_t i = wave_append(st.chk_ctr, rec);
-                    if (rec && i < WF_CHECK_CAP) {
+                    if (rec && i < st.chk_cap) {
                         st.chk[3 * (size_t)i] =
                             RtF4{p.ro.x, p.ro.y, p.ro.z, __int_as_float(st.chk_fault ? (hit >= 0 ? hit ^ 1 : 0) : hit)};
                         st.chk[3 * (size_t)i + 1] = RtF4{p.rd.x, p.rd.y, p.rd.z, bx};
@@ -1778,33 +1693,7 @@ __global__ void __launch_bounds__(WF_BLOCK, WAVES) wf_finish_bvh(RtDevScene sc, 
                     rel = st.fresh != 0; // (the pixel's passes are done: let go at the top of the loop)
                 }
             }
-#ifdef RT_PHASE_PROF
-            ph[3] += __builtin_amdgcn_s_memtime() - t2s;
-#endif
         }
-#ifdef RT_LOCKSTEP_PROF
-        if (COUNT) { // (every lane converged here: inactive lanes add 0)
-            uint32_t mb = lk_db, mk = lk_dk, sb = lk_db, sk = lk_dk;
-            for (int off = 32; off > 0; off >>= 1) {
-                mb = max(mb, (uint32_t)__shfl_xor((int)mb, off));
-                mk = max(mk, (uint32_t)__shfl_xor((int)mk, off));
-                sb += (uint32_t)__shfl_xor((int)sb, off);
-                sk += (uint32_t)__shfl_xor((int)sk, off);
-            }
-            unsigned long long tt = lk_t;
-            for (int off = 32; off > 0; off >>= 1) tt = max(tt, (unsigned long long)__shfl_xor(tt, off));
-            if (lane == 0) {
-                atomicAdd(g_phase_acc + 0, 1ull); // (wave-level ray queries)
-                atomicAdd(g_phase_acc + 1, (unsigned long long)(sb + sk));
-                atomicAdd(g_phase_acc + 2, 64ull * mb);
-                atomicAdd(g_phase_acc + 3, (unsigned long long)sb);
-                atomicAdd(g_phase_acc + 4, 64ull * mk);
-                atomicAdd(g_phase_acc + 5, (unsigned long long)sk);
-                atomicAdd(g_phase_acc + 6, lk_act);
-                atomicAdd(g_phase_acc + 7, tt);
-            }
-        }
-#endif
         if (__any(to_long) && publish_long_capped(st, to_long, p.slot, p.ro, p.rd) && to_long) {
             active = false;
             if (st.heavy) { // (first in the next call's list: the more hand-offs, the earlier)
@@ -1813,10 +1702,6 @@ __global__ void __launch_bounds__(WF_BLOCK, WAVES) wf_finish_bvh(RtDevScene sc, 
             }
         }
     }
-#ifdef RT_PHASE_PROF
-    if (lane == 0)
-        for (int k = 0; k < 7; ++k) atomicAdd(g_phase_acc + k, ph[k]);
-#endif
     if (COUNT) flush_counters(c, fr.counters);
     if (st.span && lane == 0) atomicMax(st.span + 1, __builtin_amdgcn_s_memrealtime());
     if (st.fin_live) { // this wave's hand-offs are published: the persistent wf_long may stop once all are past here
@@ -1841,8 +1726,8 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_check(RtDevScene sc, WfState st, 
     Stack<WF_LDS_STACK> stk{s_node + tid, s_entry + tid, WF_BLOCK, st.spill + gtid, st.spill_threads};
     Cnt c;
     uint32_t n = *st.chk_ctr;
-    if (n > WF_CHECK_CAP && gtid == 0) atomicAdd(dev + RT_DEV_CHK_DROP, (unsigned long long)(n - WF_CHECK_CAP));
-    n = n < WF_CHECK_CAP ? n : WF_CHECK_CAP;
+    if (n > st.chk_cap && gtid == 0) atomicAdd(dev + RT_DEV_CHK_DROP, (unsigned long long)(n - st.chk_cap));
+    n = n < st.chk_cap ? n : st.chk_cap;
     unsigned long long checked = 0, bad = 0;
     for (uint32_t e = gtid; e < n; e += gridDim.x * WF_BLOCK) {
         const RtF4 a = st.chk[3 * (size_t)e], b = st.chk[3 * (size_t)e + 1], q = st.chk[3 * (size_t)e + 2];
@@ -1931,7 +1816,7 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_verify(WfState st, uint32_t n, ui
         const unsigned long long rw = *reinterpret_cast<const unsigned long long *>(st.ret_ctr);
         res[1] += st.ret_ctr[3];
         res[2] += (uint32_t)rw - st.ret_ctr[2];
-        res[3] += st.long_ctr[0] - st.long_ctr[1];
+        res[3] += (st.long_ctr[0] & ~WF_LONG_CLOSED) - st.long_ctr[1];
         res[4] += (uint32_t)(rw >> 32);
     }
 }
@@ -2074,8 +1959,11 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_FIN_OCC) wf_finish_coop(RtDevScen
 //    by the pipelines' host threads; a wave with nothing to claim waits only
 //    while another path is running, the final slice drains the rest; a path
 //    runs to the end of its pixel's passes.
-// Neither form ever waits on work another queue must do, so neither can
-// deadlock when the runtime maps two of these streams onto one hardware queue.
+// Neither form waits for a kernel that is not resident (see the cross-kernel
+// waits at WF_FIN_STARTED): a persistent wave waits for its finisher only once
+// a finisher wave has started, and closes the ring and leaves when none has
+// within WF_LONG_START_TRIPS — so neither can deadlock when the runtime maps
+// these streams onto one hardware queue or a profiler serialises dispatches.
 template <bool COUNT>
 __global__ void __launch_bounds__(WF_BLOCK, WF_LONG_WAVES) wf_long(RtDevScene sc, RtDevFrame fr, RtDevCamera cam, WfState st,
                                                     int final_slice)
@@ -2096,6 +1984,8 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_LONG_WAVES) wf_long(RtDevScene sc
     unsigned long long t_idle = __builtin_amdgcn_s_memrealtime(); // (chain window: since entries last flowed)
     unsigned long long t_net = t_idle; // safety net: since anything that could still bring work last held
     unsigned long long t_pub = 0;      // since entry e_pub was first seen reserved but unpublished
+    // (the same bounds in loop trips: s_memrealtime stands still under counter collection)
+    uint32_t n_idle = 0, n_net = 0, n_pub = 0, n_start = 0;
     uint32_t r_seen = 0, e_pub = 0xffffffffu;
     while (true) {
         // ---- claim the next published entry (lane 0): its tag and ray are read
@@ -2106,24 +1996,36 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_LONG_WAVES) wf_long(RtDevScene sc
         if (lane == 0) {
             while (true) {
                 const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+                ++n_idle;
+                ++n_net;
                 // (producers first: once they are all past their last hand-off,
-                // `reserved` read after this acquire holds every entry)
-                const bool producing =
-                    persist && __hip_atomic_load(st.fin_live, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+                // `reserved` read after this acquire holds every entry.)  A finisher
+                // that has not started is not waited for (WF_LONG_START_TRIPS below)
+                const uint32_t fl = persist ? __hip_atomic_load(st.fin_live, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+                const bool unstarted = persist && !(fl & WF_FIN_STARTED);
+                const bool producing = persist && !unstarted && (fl & ~WF_FIN_STARTED) != 0u;
                 const bool others = __hip_atomic_load(running, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
-                const bool done =
-                    persist && !producing &&
-                    (__hip_atomic_load(st.chain_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u ||
-                     (now - t_idle > WF_LONG_CHAIN_IDLE && !others));
-                if (done) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                const bool chain_open =
+                    persist && __hip_atomic_load(st.chain_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+                if (persist && !producing && !unstarted) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                 e = __hip_atomic_load(claimed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const uint32_t r = __hip_atomic_load(reserved, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t rw = __hip_atomic_load(reserved, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const bool closed = (rw & WF_LONG_CLOSED) != 0u;
+                const uint32_t r = rw & ~WF_LONG_CLOSED;
                 const bool flowing = r != r_seen;
                 if (flowing) { // entries still flowing (to any wave): not idle
                     r_seen = r;
                     t_idle = now;
+                    n_idle = 0;
                 }
-                if (flowing || producing || others) t_net = now; // work may still come: a bounded wait
+                if (flowing || producing || others) { // work may still come: a bounded wait
+                    t_net = now;
+                    n_net = 0;
+                }
+                // done once nothing can bring entries: the ring closed, or the call's finisher
+                // past its last hand-off and no chain open (or its window over)
+                const bool window_over = (now - t_idle > WF_LONG_CHAIN_IDLE || n_idle > WF_LONG_CHAIN_TRIPS) && !others;
+                const bool done = persist && (closed || (!producing && !unstarted && (!chain_open || window_over)));
                 if (st.debug_quit) { // (tests: as if the net fired at once)
                     quit = 2;
                     break;
@@ -2150,19 +2052,34 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_LONG_WAVES) wf_long(RtDevScene sc
                     if (e != e_pub) {
                         e_pub = e;
                         t_pub = now;
-                    } else if (now - t_pub > WF_LONG_PUBLISH_WAIT) {
+                        n_pub = 0;
+                    } else if (now - t_pub > WF_LONG_PUBLISH_WAIT || ++n_pub > WF_LONG_PUBLISH_TRIPS) {
                         quit = 2;
                         break;
                     }
                 } else {
-                    // nothing claimable.  Persistent: done once the producers are; slices: the
+                    // nothing claimable.  Persistent: done once nothing can bring entries; slices: the
                     // final one once every entry is claimed, the others unless a path still runs.
                     if (persist ? done : (final_slice || !others)) {
                         quit = 1;
                         break;
                     }
+                    // the call's finisher has not started: it may be dispatched only after this kernel
+                    // ends (serialised dispatch).  After WF_LONG_START_TRIPS such trips close the ring —
+                    // atomically with the reservations, so only while every entry is claimed — and
+                    // leave: the finisher then keeps its deep paths
+                    if (unstarted && !closed && ++n_start > WF_LONG_START_TRIPS) {
+                        uint32_t x = r;
+                        if (__hip_atomic_compare_exchange_strong(reserved, &x, r | WF_LONG_CLOSED, __ATOMIC_RELAXED,
+                                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                            atomicAdd(fr.dev_stats + RT_DEV_LONG_CLOSED, 1ull);
+                            quit = 1;
+                            break;
+                        }
+                        continue; // a reservation came in: serve it
+                    }
                 }
-                if (now - t_net > WF_LONG_IDLE) { // safety net (see WF_LONG_IDLE)
+                if (now - t_net > WF_LONG_IDLE || n_net > WF_LONG_IDLE_TRIPS) { // safety net (see WF_LONG_IDLE)
                     quit = e < r ? 2 : 1;
                     break;
                 }
@@ -2296,27 +2213,9 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_LONG_WAVES) wf_long(RtDevScene sc
             __hip_atomic_fetch_sub(running, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         t_idle = __builtin_amdgcn_s_memrealtime();
+        n_idle = 0;
     }
     if (COUNT) flush_counters(c, fr.counters);
-}
-
-// debug (tools/phase_profile.py): the -DRT_PHASE_PROF build's per-phase wave
-// time of wf_finish_bvh since the last reset (zeros in other builds)
-extern "C" int rt_debug_phase_profile(unsigned long long *out8, int reset)
-{
-#if defined(RT_PHASE_PROF) || defined(RT_LOCKSTEP_PROF)
-    if (hipDeviceSynchronize() != hipSuccess ||
-        hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_phase_acc), 8 * sizeof(unsigned long long)) != hipSuccess)
-        return RT_E_HIP;
-    if (reset) {
-        unsigned long long z[8] = {};
-        if (hipMemcpyToSymbol(HIP_SYMBOL(g_phase_acc), z, sizeof z) != hipSuccess) return RT_E_HIP;
-    }
-#else
-    (void)reset;
-    for (int k = 0; k < 8; ++k) out8[k] = 0;
-#endif
-    return RT_OK;
 }
 
 // ---------------------------------------------------------------- launcher
@@ -2367,8 +2266,9 @@ struct Workspace {
     bool recorded = false;   // long_ev recorded by a previous call
     uint32_t *fin_live = nullptr; // 8 producer words (whole-call mode, one per call in flight: call % 8)
     uint32_t *heavy_list = nullptr; // (WfState.heavy_list: every pixel at most once)
-    RtF4 *chk = nullptr;          // the exactness guard's records (2 x WF_CHECK_CAP x 3 RtF4; allocated on
-                                  // the first call with the guard on) and their counter
+    RtF4 *chk = nullptr;          // the exactness guard's records (2 x chk_cap x 3 RtF4; allocated on the
+                                  // first call with the guard on, regrown for a larger frame) and their counter
+    uint32_t chk_cap = 0;
     uint32_t *chk_ctr = nullptr;
     // the join's hand-off check (wf_verify): its result words (own allocation: they outlive a
     // blob reallocation), a whole call with the hand-off ran since the last check, a check's
@@ -2376,22 +2276,16 @@ struct Workspace {
     uint32_t *verify_res = nullptr;
     bool verify_pending = false;
     bool verify_unread = false;
+    // after the last wf_verify (on whatever stream joined): every later launch on the workspace,
+    // and the host's read of verify_res, wait for it — it rewrites every pixel's ownership word
+    hipEvent_t verify_ev = nullptr;
+    bool verify_rec = false;
     int cus = 0;                                // compute units of the device (the finisher's grid)
     unsigned long long *long_log_buf = nullptr; // RT_DEBUG_LONG_LOG records
-    int fin_flip = 0; // the next chained call's finisher runs on pipeline 2 (1) or 0 (0)
-    // the guard's wf_check per record parity on pipeline 2 (!WF_FIN_ALT): the event after it (the
-    // call two later, whose finisher writes the same records, waits for it)
+    // the guard's wf_check per record parity on pipeline 2: the event after it (the call two
+    // later, whose finisher writes the same records, waits for it)
     hipEvent_t chk_done[2] = {};
     bool chk_rec[2] = {false, false};
-    // chained calls (WfState.call_ring): the issued calls' descriptors and the lists that ran out
-    // (pinned host memory, WF_CALL_RING each), the epoch-tagged list cursors (device), the open
-    // chain's first call id, and per call slot the event after its launch
-    unsigned long long *call_ring = nullptr;
-    uint32_t *call_exh = nullptr;
-    unsigned long long *call_ctr = nullptr;
-    uint32_t chain_first = 0;
-    hipEvent_t call_ev[WF_CALL_RING] = {};
-    bool call_ev_rec[WF_CALL_RING] = {};
     // RtOptions.profile of whole calls: per profiled call its finisher's span on the device
     // ({first wave start, last wave end}, s_memrealtime) in a ring of WF_PROF_SLOTS, resolved
     // into RtProfile records by rt_last_profile / rt_profile_history (they join first)
@@ -2439,19 +2333,9 @@ int ensure_streams(Workspace &w, int npipes)
         if (hipEventCreateWithFlags(&w.fin_ready, hipEventDisableTiming) != hipSuccess) return -1;
         if (hipEventCreateWithFlags(&w.long_ev, hipEventDisableTiming) != hipSuccess) return -1;
         if (hipEventCreate(&w.ev0) != hipSuccess || hipEventCreate(&w.ev1) != hipSuccess) return -1;
+        if (hipEventCreateWithFlags(&w.verify_ev, hipEventDisableTiming) != hipSuccess) return -1;
         if (hipMalloc((void **)&w.verify_res, 64) != hipSuccess || hipMemset(w.verify_res, 0, 64) != hipSuccess)
             return -1;
-        // chained calls: descriptors and ran-out marks in pinned host memory (the host writes the
-        // one, the device the other, both while kernels run), the list cursors on the device
-        if (hipHostMalloc((void **)&w.call_ring, WF_CALL_RING * 8, hipHostMallocCoherent) != hipSuccess ||
-            hipHostMalloc((void **)&w.call_exh, WF_CALL_RING * 4, hipHostMallocCoherent) != hipSuccess ||
-            hipMalloc((void **)&w.call_ctr, (size_t)WF_CALL_CURSORS * 8) != hipSuccess ||
-            hipMemset(w.call_ctr, 0, (size_t)WF_CALL_CURSORS * 8) != hipSuccess)
-            return -1;
-        memset(w.call_ring, 0, WF_CALL_RING * 8);
-        memset(w.call_exh, 0, WF_CALL_RING * 4);
-        for (auto &e : w.call_ev)
-            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return -1;
         for (auto &e : w.chk_done)
             if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return -1;
         w.streams_ok = true;
@@ -2615,15 +2499,13 @@ int ensure(Workspace &w, size_t slots, int grid, int npipes)
         st.fin_live = nullptr;
         st.chain_flag = (uint32_t *)(b + o_ctl + 128);
         st.fresh = 0;
-        st.concurrent = 0;
         st.fresh_n = 0;
         st.span = nullptr;
         st.call_id = 0;
-        st.call_ring = st.call_ctr = nullptr;
-        st.call_exh = nullptr;
         st.chk = nullptr; // (whole-call mode only: launch_whole)
         st.chk_ctr = nullptr;
         st.chk_mask = 0;
+        st.chk_cap = 0;
         st.chk_fault = 0;
         st.debug_quit = 0;
     }
@@ -2648,16 +2530,21 @@ int launch_verify(Workspace &w, hipStream_t stream)
     hipLaunchKernelGGL(wf_verify, dim3(blocks), dim3(WF_BLOCK), 0, stream, w.pipe[0].st, (uint32_t)w.slots,
                        w.verify_res, w.last_fr.dev_stats);
     if (hipGetLastError() != hipSuccess) return -1;
+    // (every later launch on the workspace waits for it: join_all; and so does the host's read of its result)
+    if (hipEventRecord(w.verify_ev, stream) != hipSuccess) return -1;
+    w.verify_rec = true;
     w.verify_unread = true;
     return 0;
 }
 
 // `stream` waits for every call's device work on this workspace (the
-// pipelines' last launches and every wf_long), an open chain drained first;
-// then the hand-off check runs on it
+// pipelines' last launches and every wf_long), an open chain drained first,
+// and for the last hand-off check (which another stream may have run: it
+// rewrites every ownership word); then the hand-off check runs on it
 int join_all(Workspace &w, hipStream_t stream)
 {
     if (launch_drain(w) != 0) return -1;
+    if (w.verify_rec && hipStreamWaitEvent(stream, w.verify_ev, 0) != hipSuccess) return -1;
     for (int pi = 0; pi < WF_MAX_PIPES; ++pi) {
         Pipe &p = w.pipe[pi];
         if (p.joined && hipStreamWaitEvent(stream, p.join, 0) != hipSuccess) return -1;
@@ -2725,31 +2612,42 @@ int launch_whole(Workspace &w, int dev, const RtDevScene &sc, const RtDevFrame &
     // workspace first (before a larger frame's workspace replaces the old one)
     if (!chained && join_all(w, stream) != 0) return -1;
     if (ensure(w, slots, grid, 1) != 0) return -1;
-    if (!chained) w.fin_flip = 0;
-    // the finisher's stream: chained calls alternate between pipelines 0 and 2 (the
-    // previous finisher's tail and this one's bulk share the chip); its counters, its
-    // stack spill area and its guard records go with it
-    const int fpi = WF_FIN_ALT && w.fin_flip ? 2 : 0;
-    w.fin_flip ^= overlap ? 1 : 0;
-    Pipe &pp = w.pipe[fpi];
+    // the finisher's stream (chained calls' finishers one after the other on it); its counters,
+    // its stack spill area and its guard records go with it
+    Pipe &pp = w.pipe[0];
     WfState st = pp.st;
     const int long_return = long_depth > 0 ? 1 : 0;
     st.long_depth = long_depth;
     st.long_return = long_return;
     st.fresh = 1;
-    st.concurrent = overlap && WF_FIN_CONTINUE ? 1 : 0;
     st.fresh_n = (uint32_t)(((fr.width + 15) / 16) * ((fr.height + 15) / 16)) * 256u;
     st.linger = overlap ? 0ull : WF_FIN_LINGER;
     st.chk_mask = check_mask;
-    // the guard's records per call parity (WF_FIN_ALT: per finisher stream, its wf_check behind it)
-    const int par = WF_FIN_ALT ? fpi / 2 : (int)(w.call_seq & 1);
-    // (the guard's records: allocated by the first call that samples rays)
-    if (check_mask != 0xFFFFFFFFu && !w.chk &&
-        hipMalloc((void **)&w.chk, 2 * (size_t)WF_CHECK_CAP * 3 * sizeof(RtF4)) != hipSuccess) {
-        w.chk = nullptr;
-        return -1;
+    // the guard's records per call parity (the call two later reuses them after this call's wf_check),
+    // sized from the call's rays: <= 8 rays per sample (deep paths go to wf_long; owed passes are few)
+    // / the sampling interval, so a small frame does not hold the 2 x 4M-record maximum
+    const int par = (int)(w.call_seq & 1);
+    if (check_mask != 0xFFFFFFFFu) {
+        const unsigned long long want = (unsigned long long)slots * (unsigned long long)fr.passes * 8ull /
+                                        ((unsigned long long)check_mask + 1ull);
+        uint32_t cap = 1u << 16;
+        while (cap < want && cap < WF_CHECK_CAP) cap <<= 1;
+        if (cap > w.chk_cap) { // (grown: after every wf_check that reads the old records)
+            if (w.chk) {
+                if (hipDeviceSynchronize() != hipSuccess) return -1;
+                (void)hipFree(w.chk);
+                w.chk = nullptr;
+                w.chk_cap = 0;
+            }
+            if (hipMalloc((void **)&w.chk, 2 * (size_t)cap * 3 * sizeof(RtF4)) != hipSuccess) {
+                w.chk = nullptr;
+                return -1;
+            }
+            w.chk_cap = cap;
+        }
     }
-    st.chk = check_mask == 0xFFFFFFFFu ? nullptr : w.chk + 3 * (size_t)WF_CHECK_CAP * (size_t)par;
+    st.chk = check_mask == 0xFFFFFFFFu ? nullptr : w.chk + 3 * (size_t)w.chk_cap * (size_t)par;
+    st.chk_cap = w.chk_cap;
     st.chk_ctr = w.chk_ctr + par;
     st.chk_fault = (debug & RT_DEBUG_CHECK_FAULT) ? 1 : 0;
     st.debug_quit = (debug & RT_DEBUG_LONG_QUIT) ? 1 : 0;
@@ -2768,33 +2666,8 @@ int launch_whole(Workspace &w, int dev, const RtDevScene &sc, const RtDevFrame &
     const uint32_t k = (uint32_t)(w.call_seq % 8);
     st.fin_live = long_return ? w.fin_live + k : nullptr;
     st.call_id = (uint32_t)w.call_seq + 1u;
-    st.call_ring = st.call_ctr = nullptr;
-    st.call_exh = nullptr;
-    if (overlap && WF_FIN_CONTINUE) {
-        // issue the call: lanes of the chain's running finishers may take its pixels from now on.
-        // (Bound: the call WF_CALLS_IN_FLIGHT before it has run its list out, so no cursor slot
-        // is still in use by a call WF_CALL_RING before.)
-        if (!chained) w.chain_first = st.call_id;
-        const uint32_t old = st.call_id - WF_CALLS_IN_FLIGHT;
-        if (chained && st.call_id > WF_CALLS_IN_FLIGHT && old >= w.chain_first) {
-            const int oi = (int)(old % WF_CALL_RING);
-            while (__atomic_load_n(w.call_exh + oi, __ATOMIC_ACQUIRE) != old) {
-                if (w.call_ev_rec[oi]) {
-                    const hipError_t q = hipEventQuery(w.call_ev[oi]);
-                    if (q == hipSuccess) break; // (its launch ended: every list it could take ran out)
-                    if (q != hipErrorNotReady) return -1;
-                }
-                std::this_thread::sleep_for(std::chrono::microseconds(20));
-            }
-        }
-        st.call_ring = w.call_ring;
-        st.call_ctr = w.call_ctr;
-        st.call_exh = w.call_exh;
-        __atomic_store_n(w.call_ring + st.call_id % WF_CALL_RING,
-                         (unsigned long long)st.call_id << 32 | (uint32_t)fr.passes, __ATOMIC_RELEASE);
-    }
     if (!chained) {
-        // the hand-off state from zero (nothing of it is in flight now)
+        // the hand-off state from zero (nothing of it is in flight now; a ring a wf_long closed reopens)
         if (long_return) {
             // (the rings' whole capacity: the workspace may be sized for an earlier, larger frame, and a
             // stale tag beyond this frame's pixel count would look published to wf_long / the finishers)
@@ -2810,10 +2683,11 @@ int launch_whole(Workspace &w, int dev, const RtDevScene &sc, const RtDevFrame &
     const hipStream_t s = pp.stream;
     if (hipEventRecord(w.fork, stream) != hipSuccess || hipStreamWaitEvent(s, w.fork, 0) != hipSuccess) return -1;
     if (hipMemsetAsync(st.counts, 0, 256, s) != hipSuccess) return -1;
+    // (the producers' word: the finisher's wave count, no wave started yet)
     if (st.fin_live && hipMemsetD32Async((hipDeviceptr_t)st.fin_live, (int)(fgrid * (WF_BLOCK / 64)), 1, s) != hipSuccess)
         return -1;
     if (st.chk) { // (this parity's records: after the wf_check that last read them)
-        if (!WF_FIN_ALT && w.chk_rec[par] && hipStreamWaitEvent(s, w.chk_done[par], 0) != hipSuccess) return -1;
+        if (w.chk_rec[par] && hipStreamWaitEvent(s, w.chk_done[par], 0) != hipSuccess) return -1;
         if (hipMemsetAsync(st.chk_ctr, 0, 4, s) != hipSuccess) return -1;
     }
     if (long_return && hipMemsetD32Async((hipDeviceptr_t)st.chain_flag, overlap ? 1 : 0, 1, s) != hipSuccess) return -1;
@@ -2824,7 +2698,7 @@ int launch_whole(Workspace &w, int dev, const RtDevScene &sc, const RtDevFrame &
     }
     // heavy pixels first (wf_heavy_list): listed and tagged with this call before the finisher
     st.heavy_list = nullptr;
-    if (long_return && w.heavy_list && WF_HEAVY_FIRST && !WF_FIN_CONTINUE) {
+    if (long_return && w.heavy_list && WF_HEAVY_FIRST) {
         st.heavy_list = w.heavy_list;
         if (hipMemsetAsync(st.heavy_n, 0, 4, s) != hipSuccess) return -1;
         // two classes: pixels handed over WF_HEAVY_SPLIT+ times so far, then the others
@@ -2835,43 +2709,39 @@ int launch_whole(Workspace &w, int dev, const RtDevScene &sc, const RtDevFrame &
         if (hipGetLastError() != hipSuccess) return -1;
     }
     if (hipEventRecord(w.fin_ready, s) != hipSuccess) return -1;
-    // (the finisher is launched before its wf_long: on a shared hardware queue
-    // it then completes first, and wf_long finds its producers done.  Counting:
-    // the finisher's own work; wf_long's deep paths are not counted)
+    Pipe *lp = long_return ? &w.pipe[1] : nullptr;
+    // wf_long on pipeline 1's stream, after the finisher's set-up.  Normally it starts beside the
+    // finisher; nothing relies on that (serialised dispatch runs either alone, in either order:
+    // see the cross-kernel waits at WF_FIN_STARTED).  Debug: force one order —
+    // RT_DEBUG_SERIAL_LONG_FIRST runs wf_long to its end before the finisher starts,
+    // RT_DEBUG_SERIAL_FIN_FIRST the finisher to its end before wf_long starts
+    const bool long_first = lp && (debug & RT_DEBUG_SERIAL_LONG_FIRST);
+    const bool fin_first = lp && !long_first && (debug & RT_DEBUG_SERIAL_FIN_FIRST);
+    auto launch_long = [&]() -> int {
+        if (hipStreamWaitEvent(lp->stream, fin_first ? pp.fin_done : w.fin_ready, 0) != hipSuccess) return -1;
+        hipLaunchKernelGGL(wf_long<false>, dim3(WF_LONG_BLOCKS), dim3(WF_BLOCK), 0, lp->stream, sc, fr, cam, st, 1);
+        if (hipGetLastError() != hipSuccess) return -1;
+        if (hipEventRecord(lp->long_done, lp->stream) != hipSuccess) return -1;
+        lp->long_rec = true;
+        return 0;
+    };
+    if (long_first && (launch_long() != 0 || hipStreamWaitEvent(s, lp->long_done, 0) != hipSuccess)) return -1;
+    // Counting: the finisher's own work; wf_long's deep paths are not counted
     if (count) hipLaunchKernelGGL(wf_finish_bvh<true>, dim3(fgrid), dim3(WF_BLOCK), 0, s, sc, fr, cam, st, 0);
     else if (fgrid <= w.cus * WF_FIN_SMALL_WAVES)
         hipLaunchKernelGGL((wf_finish_bvh<false, 1>), dim3(fgrid), dim3(WF_BLOCK), 0, s, sc, fr, cam, st, 0);
     else hipLaunchKernelGGL(wf_finish_bvh<false>, dim3(fgrid), dim3(WF_BLOCK), 0, s, sc, fr, cam, st, 0);
     if (hipGetLastError() != hipSuccess) return -1;
-    if (overlap) {
-        const int ci = (int)(st.call_id % WF_CALL_RING);
-        if (hipEventRecord(w.call_ev[ci], s) != hipSuccess) return -1;
-        w.call_ev_rec[ci] = true;
-    }
-    Pipe *lp = nullptr;
-    if (long_return) {
-        lp = &w.pipe[1];
-        if (hipStreamWaitEvent(lp->stream, w.fin_ready, 0) != hipSuccess) return -1;
-        hipLaunchKernelGGL(wf_long<false>, dim3(WF_LONG_BLOCKS), dim3(WF_BLOCK), 0, lp->stream, sc, fr, cam, st, 1);
-        if (hipGetLastError() != hipSuccess) return -1;
-        if (hipEventRecord(lp->long_done, lp->stream) != hipSuccess) return -1;
-        lp->long_rec = true;
-    }
-    if (st.chk && WF_FIN_ALT) {
-        // the guard's re-traces after the finisher on its stream (its KD stacks in the finisher's
-        // spill area), beside the next chained call's finisher: latency-bound single-lane KD
-        // traversals, 256 blocks
-        hipLaunchKernelGGL(wf_check, dim3(WF_CHECK_BLOCKS), dim3(WF_BLOCK), 0, s, sc, st, fr.dev_stats);
-        if (hipGetLastError() != hipSuccess) return -1;
-    } else if (st.chk) {
-        // ... on pipeline 2's stream after the finisher, beside whatever follows it on pipeline 0
-        // (the next call's finisher, a chain's drain); its KD stacks in pipeline 2's spill area
+    if (hipEventRecord(pp.fin_done, s) != hipSuccess) return -1;
+    if (lp && !long_first && launch_long() != 0) return -1;
+    if (st.chk) {
+        // the guard's re-traces on pipeline 2's stream after the finisher, beside whatever follows it on
+        // pipeline 0 (the next call's finisher, a chain's drain); its KD stacks in pipeline 2's spill area
         Pipe &cp = w.pipe[2];
         WfState cs = st;
         cs.spill = cp.st.spill;
         if (!cs.spill) return -1;
-        if (hipEventRecord(pp.fin_done, s) != hipSuccess || hipStreamWaitEvent(cp.stream, pp.fin_done, 0) != hipSuccess)
-            return -1;
+        if (hipStreamWaitEvent(cp.stream, pp.fin_done, 0) != hipSuccess) return -1;
         hipLaunchKernelGGL(wf_check, dim3(WF_CHECK_BLOCKS), dim3(WF_BLOCK), 0, cp.stream, sc, cs, fr.dev_stats);
         if (hipGetLastError() != hipSuccess) return -1;
         if (hipEventRecord(w.chk_done[par], cp.stream) != hipSuccess || hipEventRecord(cp.join, cp.stream) != hipSuccess)
@@ -2882,7 +2752,8 @@ int launch_whole(Workspace &w, int dev, const RtDevScene &sc, const RtDevFrame &
     if (hipEventRecord(pp.join, s) != hipSuccess) return -1;
     pp.joined = true;
     // join: unless the call overlaps the next one, the caller's stream continues after the
-    // finisher (and the guard) and after its wf_long
+    // finisher and after its wf_long (the guard's wf_check touches no frame data: its statistics
+    // are read by rt_deviation_stats, which joins it)
     if (!overlap) {
         if (hipStreamWaitEvent(stream, pp.join, 0) != hipSuccess) return -1;
         if (lp && hipStreamWaitEvent(stream, lp->long_done, 0) != hipSuccess) return -1;
@@ -2933,7 +2804,6 @@ int launch_drain(Workspace &w)
     st.long_return = 1;
     st.fresh = 1;
     st.fresh_n = 0; // (no pixels of its own)
-    st.concurrent = 0;
     st.span = nullptr;
     st.linger = WF_FIN_LINGER; // (a pixel still out after it: wf_long runs it to the end)
     st.chk = nullptr;
@@ -2947,7 +2817,6 @@ int launch_drain(Workspace &w)
     st.fin_live = w.fin_live + (uint32_t)(w.call_seq % 8);
     ++w.call_seq;
     const hipStream_t s = pp.stream;
-    if (WF_FIN_ALT && w.pipe[2].joined && hipStreamWaitEvent(s, w.pipe[2].join, 0) != hipSuccess) return -1;
     // no pixels (counts[4] = 0 of fresh_n 0), no linger seat taken yet
     if (hipMemsetAsync(st.counts, 0, 256, s) != hipSuccess) return -1;
     if (hipMemsetAsync(st.ret_ctr + 4, 0, 4, s) != hipSuccess) return -1;
@@ -3050,8 +2919,10 @@ const char *rt_wavefront_incomplete_msg() { return g_incomplete; }
 // on the current device, chained calls' deep-path tails included, and for the
 // hand-off check after them.  A host join returns RT_WAVEFRONT_INCOMPLETE if
 // that check, or one enqueued by an earlier stream join, found pixels that
-// never came back from wf_long.
-int rt_wavefront_join(void *stream)
+// never came back from wf_long.  consume = 0 (the library's joins that do
+// not report: rt_deviation_stats, buffer and scene teardown) leaves such a
+// result for the next reporting join: the incomplete status is sticky.
+int rt_wavefront_join(void *stream, int consume)
 {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return -1;
@@ -3072,14 +2943,16 @@ int rt_wavefront_join(void *stream)
     if (w->recorded && hipEventSynchronize(w->long_ev) != hipSuccess) return -1;
     if (w->verify_pending) {
         const hipStream_t s = w->pipe[0].stream; // (idle: everything above is done)
-        if (launch_verify(*w, s) != 0 || hipStreamSynchronize(s) != hipSuccess) return -1;
+        if (launch_verify(*w, s) != 0) return -1;
     }
+    // (the last check may run on a caller's stream: its result is read after it)
+    if (w->verify_rec && hipEventSynchronize(w->verify_ev) != hipSuccess) return -1;
     if (!w->verify_unread) return 0;
-    w->verify_unread = false;
     uint32_t r[5] = {};
-    if (hipMemcpy(r, w->verify_res, sizeof r, hipMemcpyDeviceToHost) != hipSuccess ||
-        hipMemset(w->verify_res, 0, sizeof r) != hipSuccess)
-        return -1;
+    if (hipMemcpy(r, w->verify_res, sizeof r, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    if (!consume) return 0;
+    w->verify_unread = false;
+    if (hipMemset(w->verify_res, 0, sizeof r) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return -1;
     if (r[0] | r[1] | r[2] | r[3] | r[4]) {
         snprintf(g_incomplete, sizeof g_incomplete,
                  "%u pixels stranded in the deep-path hand-off (pixels out %u, returns unclaimed %u, hand-offs "
@@ -3104,13 +2977,8 @@ void rt_wavefront_shutdown()
         if (w->blob) (void)launch_drain(*w); // (an open chain's wf_longs leave only after its drain)
         (void)hipDeviceSynchronize();
         if (w->blob) (void)hipFree(w->blob);
-        for (void *p : {(void *)w->chk, (void *)w->verify_res, (void *)w->long_log_buf, (void *)w->spans,
-                        (void *)w->call_ctr})
+        for (void *p : {(void *)w->chk, (void *)w->verify_res, (void *)w->long_log_buf, (void *)w->spans})
             if (p) (void)hipFree(p);
-        for (void *p : {(void *)w->call_ring, (void *)w->call_exh})
-            if (p) (void)hipHostFree(p);
-        for (hipEvent_t e : w->call_ev)
-            if (e) (void)hipEventDestroy(e);
         for (int i = WF_MAX_PIPES - 1; i >= 0; --i) {
             Pipe &p = w->pipe[i];
             for (auto &e : p.ev)
@@ -3121,7 +2989,8 @@ void rt_wavefront_shutdown()
             if (p.host_count) (void)hipHostFree(p.host_count);
             if (p.stream) (void)hipStreamDestroy(p.stream);
         }
-        for (hipEvent_t e : {w->chk_done[1], w->chk_done[0], w->ev1, w->ev0, w->long_ev, w->fin_ready, w->fork})
+        for (hipEvent_t e : {w->verify_ev, w->chk_done[1], w->chk_done[0], w->ev1, w->ev0, w->long_ev, w->fin_ready,
+                             w->fork})
             if (e) (void)hipEventDestroy(e);
         delete w;
         kv.second = nullptr;

@@ -95,11 +95,12 @@ class RtDeviations(ctypes.Structure):
                 ("mismatch_ray", ctypes.c_float * 6),
                 ("owed_pixels", ctypes.c_ulonglong), ("owed_passes", ctypes.c_ulonglong),
                 ("long_safety_quits", ctypes.c_ulonglong), ("stranded_pixels", ctypes.c_ulonglong),
-                ("check_dropped", ctypes.c_ulonglong), ("linger_expiries", ctypes.c_ulonglong)]
+                ("check_dropped", ctypes.c_ulonglong), ("linger_expiries", ctypes.c_ulonglong),
+                ("long_closed", ctypes.c_ulonglong)]
 
 
 HANDOFF_FIELDS = ("owed_pixels", "owed_passes", "long_safety_quits", "stranded_pixels", "check_dropped",
-                  "linger_expiries")
+                  "linger_expiries", "long_closed")
 
 
 def deviation_stats(reset=False):
@@ -125,9 +126,10 @@ def join(stream=None):
     check(lib().rt_join(stream))
 
 
-ABI_VERSION = 7  # RT_ABI_VERSION of include/isaklm_rt.h
+ABI_VERSION = 8  # RT_ABI_VERSION of include/isaklm_rt.h
 E_INCOMPLETE = -7  # RT_E_INCOMPLETE: a join found stranded pixels
 DEBUG_CALL_LOG, DEBUG_LONG_LOG, DEBUG_CHECK_FAULT, DEBUG_LONG_QUIT = 1, 2, 4, 8  # RtOptions.debug bits
+DEBUG_SERIAL_LONG_FIRST, DEBUG_SERIAL_FIN_FIRST = 16, 32  # (tests: serialised dispatch in either order)
 TRIANGLE_BYTES = 152
 NODE_BYTES = 20
 COUNTER_NAMES = ["node", "tri", "hit", "texel", "nee", "sample", "skip", "ray", "watchdog", "maxdepth"]

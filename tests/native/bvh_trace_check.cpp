@@ -290,65 +290,6 @@ bool kd_resume(const rt_host::PreparedHost &h, uint32_t start, uint32_t packed, 
     return true;
 }
 
-// restatement of bvh_trace.h kd_entry_leaf: the descent's first leaf from the
-// start node of P = o + d s_min's grid cell, certified by the start node's
-// faces (the rule's monotonicity) and the origin lookups in the split hash
-// sets, then the rule below the start node (false: the descent from the root)
-long long g_entry_ok = 0, g_entry_fail = 0, g_entry_miss = 0;
-bool split_hash_has(const rt_host::PreparedHost &h, int a, float v)
-{
-    const uint32_t bits = rt_split_bits(v), mask = h.split_hash_mask[a];
-    const uint32_t *tbl = h.split_hash.data() + h.split_hash_off[a];
-    uint32_t i = rt_split_hash(bits) & mask;
-    while (true) {
-        if (tbl[i] == bits) return true;
-        if (tbl[i] == RT_SPLIT_HASH_EMPTY) return false;
-        i = (i + 1) & mask;
-    }
-}
-bool rule_above(float v, float oa, float da, float s_min, float &ex)
-{
-    const float t = (v - oa) / da;
-    const bool near_above = oa >= v;
-    if (t > s_min) ex = fminf(ex, t);
-    return (t < 0 || t > s_min) ? near_above : !near_above;
-}
-bool entry_leaf(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, float s_min, float root_exit, uint32_t &leaf,
-                float &ex)
-{
-    if (h.kd_entry.empty() || h.split_hash.empty()) return false;
-    const int G = h.kd_grid;
-    const float p[3] = {o.x + d.x * s_min, o.y + d.y * s_min, o.z + d.z * s_min};
-    const float bmin[3] = {h.bounds.min.x, h.bounds.min.y, h.bounds.min.z};
-    int c[3];
-    for (int a = 0; a < 3; ++a) {
-        const float f = (p[a] - bmin[a]) * h.kd_grid_scale[a];
-        c[a] = f >= 0.0f ? (f < (float)(G - 1) ? (int)f : G - 1) : 0;
-    }
-    const size_t k = ((size_t)c[2] * G + c[1]) * G + c[0];
-    const RtF4 r0 = h.kd_entry[2 * k], r1 = h.kd_entry[2 * k + 1];
-    uint32_t node;
-    memcpy(&node, &r0.x, 4);
-    if (node == 0xFFFFFFFFu) return false;
-    ex = root_exit;
-    const float lo[3] = {r0.y, r0.z, r0.w}, hi[3] = {r1.x, r1.y, r1.z};
-    const float oa[3] = {o.x, o.y, o.z}, da[3] = {d.x, d.y, d.z};
-    for (int a = 0; a < 3; ++a) {
-        if (lo[a] > -INFINITY && !rule_above(lo[a], oa[a], da[a], s_min, ex)) return false;
-        if (hi[a] < INFINITY && rule_above(hi[a], oa[a], da[a], s_min, ex)) return false;
-    }
-    for (int a = 0; a < 3; ++a)
-        if (da[a] > 0.0f && lo[a] > -INFINITY && oa[a] < lo[a] && split_hash_has(h, a, oa[a])) return false;
-    while (true) {
-        const uint32_t x = h.nodes[2 * node], y = h.nodes[2 * node + 1];
-        if ((y & 3u) == RT_LEAF_TAG) break;
-        const int a = (int)(y & 3u);
-        node = rule_above(bitsf(x), oa[a], da[a], s_min, ex) ? y >> 2 : node + 1;
-    }
-    leaf = node;
-    return true;
-}
-
 Hit bounded_trace(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, Work &w)
 {
     float t1, t2;
@@ -362,34 +303,6 @@ Hit bounded_trace(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, Work &w)
         ++g_bvh4_mism;
     }
     if (!(s_min < t2)) return Hit{};
-    uint32_t leaf;
-    float ex;
-    if (s_min >= t1 && entry_leaf(h, o, d, s_min, t2, leaf, ex)) {
-        const uint32_t nx = h.nodes[2 * leaf], count = h.nodes[2 * leaf + 1] >> 2;
-        Hit hit;
-        if (count > 0 && ex > s_min) {
-            float smallest = ex;
-            for (uint32_t e = nx; e < nx + count; ++e) {
-                float s, b[3];
-                ++w.tests;
-                if (test(h.isect_a.data(), h.isect_bary.data(), e, o, d, smallest, s, b)) {
-                    smallest = s;
-                    hit.tri = (int)h.isect_bary[e].tri;
-                    memcpy(hit.b, b, sizeof b);
-                }
-            }
-        }
-        if (hit.tri >= 0) {
-#pragma omp atomic
-            ++g_entry_ok;
-            return hit;
-        }
-#pragma omp atomic
-        ++g_entry_miss;
-    } else {
-#pragma omp atomic
-        ++g_entry_fail;
-    }
     return kd_trace(h, o, d, t1, t2, s_min, w);
 }
 
@@ -612,8 +525,6 @@ int main(int argc, char **argv)
     printf("bounded per ray: bvh nodes %.1f bvh tests %.1f kd nodes %.1f leaves %.2f tests %.1f\n", wb.bvh_nodes / R,
            wb.bvh_tests / R, wb.nodes / R, wb.leaves / R, wb.tests / R);
     printf("origin-cell entry: %lld resumed, mismatches vs the plain traversal %lld\n", g_origin_resumed, g_origin_mism);
-    printf("KD phase entry: %lld hit at the certified leaf, %lld leaf without a hit, %lld not certified\n", g_entry_ok,
-           g_entry_miss, g_entry_fail);
     printf("4-wide s_min query: %zu nodes, deepest stack %d, s_min differing from the binary query %lld\n",
            h.bvh4.size() / 8, h.bvh4_stack, g_bvh4_mism);
     return mism == 0 && g_origin_mism == 0 && g_bvh4_mism == 0 ? 0 : 1;

@@ -118,26 +118,3 @@ def test_bounded_equals_kd_adversarial_host(trace_check, tmp_path, variant):
     out = _run_trace_check(trace_check, path, 1_000_000, seed=3)
     assert "rays 1000000" in out and " mismatches 0\n" in out, out
     assert "shipped below the proven bound 0, unproven 0" in out, out
-
-
-@pytest.mark.parametrize("name", ["cornell_blob", "room_small", "trap", "aligned"])
-def test_kd_phase_entry_host(trace_check, tmp_path, name):
-    """The bounded KD phase's entry (bvh_trace.h kd_entry_leaf): the descent's
-    first leaf found from the start node of P = o + d s_min's grid cell,
-    certified by that node's faces and the origin's split lookups — and the
-    descent from the root whenever it is not certified or that leaf holds no
-    hit — equals the plain KD traversal on every ray (bounded_trace uses it),
-    including the wall-on-split-plane and trap scenes; and it is taken for most
-    rays."""
-    if name == "trap":
-        path = helpers.make_trap_scene(str(tmp_path / "t"))
-    elif name == "aligned":
-        path = hazards.cornell_variant(str(tmp_path / "a"), "aligned", yaw_room=0.0)
-    else:
-        path = helpers.scene_path(name)
-    out = _run_trace_check(trace_check, path, 400_000, seed=5)
-    assert "rays 400000" in out and " mismatches 0\n" in out, out
-    line = out.split("KD phase entry: ")[1].split("\n")[0]
-    ok, miss, fail = (int(line.split(" hit at")[0]), int(line.split(", ")[1].split(" leaf")[0]),
-                      int(line.split(", ")[2].split(" not")[0]))
-    assert ok > 0 and ok > 4 * (miss + fail), out

@@ -271,3 +271,110 @@ def test_unchained_long_calls_run_each_pass_once():
     W, H = 1920, 1080
     gpu = _render_calls(run, W, H, [256, 256], overlap=False)
     assert int(gpu[2].min()) == 512 and int(gpu[2].max()) == 512
+
+
+def _stream_nonblocking():
+    """a raw non-blocking hipStream_t (hipStreamNonBlocking: not ordered against the null stream)"""
+    global _HIP
+    if _HIP is None:
+        _HIP = ctypes.CDLL("libamdhip64.so")
+    s = ctypes.c_void_p()
+    assert _HIP.hipStreamCreateWithFlags(ctypes.byref(s), ctypes.c_uint(1)) == 0
+    _STREAMS.append(s)
+    return s
+
+
+@pytest.mark.parametrize("overlap", [False, True])
+@pytest.mark.parametrize("order", ["long_first", "fin_first"])
+def test_serialised_dispatch_is_exact(tmp_path, order, overlap):
+    """under rocprofv3 counter collection the path kernel
+    (the finisher) and the long-path kernel (wf_long) dispatch one at a time,
+    in either order — the bench's counter pass hung when wf_long went first
+    and waited for a finisher that could not start.  The debug bits force each
+    order: wf_long first must close its hand-off ring after its bounded wait
+    and leave (the finisher then runs its deep paths itself); the finisher
+    first must stop lingering for wf_long (bounded by loop trips, not by the
+    clock).  Both must be bit-exact, strand nothing, and finish in seconds."""
+    import time
+
+    trap = helpers.make_trap_scene(str(tmp_path / "t"))
+    run = helpers.GpuRun(trap)
+    W, H = 96, 64
+    bit = rt.DEBUG_SERIAL_LONG_FIRST if order == "long_first" else rt.DEBUG_SERIAL_FIN_FIRST
+    rt.join()
+    rt.deviation_stats(reset=True)
+    t = time.perf_counter()
+    gpu = _render_calls(run, W, H, [2, 3, 1], overlap=overlap, wf_long_depth=8, debug=bit)
+    dt = time.perf_counter() - t
+    ref, _ = helpers.oracle_render(trap, W, H, [2, 3, 1])
+    helpers.assert_bitwise(gpu, ref, what=f"serialised dispatch ({order}, overlap {overlap})")
+    dev = rt.deviation_stats(reset=True)
+    assert dev["stranded_pixels"] == 0 and dev["long_safety_quits"] == 0, dev
+    if order == "long_first":
+        assert dev["long_closed"] > 0, dev  # every call's wf_long found its finisher not started
+    else:
+        assert dev["long_closed"] == 0, dev
+    assert dt < 30.0, dt
+    # the workspace recovers: the next (unserialised) render hands deep paths off again, exactly
+    rt.deviation_stats(reset=True)
+    gpu = _render_calls(run, W, H, [2, 2], overlap=overlap, wf_long_depth=8)
+    ref, _ = helpers.oracle_render(trap, W, H, [2, 2])
+    helpers.assert_bitwise(gpu, ref, what="render after serialised dispatch")
+    assert rt.deviation_stats(reset=True)["long_closed"] == 0
+
+
+def test_serialised_dispatch_room2m_bench_shape():
+    """The bench's counter pass, as it hung: an unchained 1080p room2m call
+    with wf_long dispatched before the finisher.  Bit-identical to the
+    unserialised call of the same passes."""
+    run = helpers.GpuRun("room2m")
+    W, H = 1920, 1080
+    plain = _render_calls(run, W, H, [2, 6], overlap=False)
+    rt.deviation_stats(reset=True)
+    serial = _render_calls(run, W, H, [2, 6], overlap=False, debug=rt.DEBUG_SERIAL_LONG_FIRST)
+    helpers.assert_bitwise(serial, plain, what="room2m 1080p, wf_long dispatched first")
+    dev = rt.deviation_stats(reset=True)
+    assert dev["long_closed"] > 0 and dev["stranded_pixels"] == 0, dev
+
+
+def test_incomplete_status_is_sticky(tmp_path):
+    """a library join that does not report (rt_deviation_stats)
+    must not swallow a stranded frame: the next reporting join still returns
+    RT_E_INCOMPLETE, once."""
+    trap = helpers.make_trap_scene(str(tmp_path / "t"))
+    run = helpers.GpuRun(trap)
+    W, H = 96, 64
+    rt.join()
+    rt.deviation_stats(reset=True)
+    g = rt.GBuffer(W, H)
+    rt.render(run.dev, g, run.camera, 0, rt.options(W, H, 2, adaptive=False, kernel=WF, wf_long_depth=8,
+                                                    debug=rt.DEBUG_LONG_QUIT))
+    dev = rt.deviation_stats(reset=False)  # joins, does not report
+    assert dev["stranded_pixels"] > 0, dev
+    with pytest.raises(rt.RtError) as ei:
+        rt.join()
+    assert f"rt error {rt.E_INCOMPLETE}" in str(ei.value), str(ei.value)
+    rt.join()  # reported once
+    rt.deviation_stats(reset=True)
+
+
+def test_stream_join_then_render_on_another_stream(tmp_path):
+    """a stream join enqueues the hand-off check
+    (wf_verify, which rewrites every pixel's ownership word) on that stream;
+    a render on another, non-blocking stream right after must run after it —
+    else the check can free a pixel a new finisher lane holds."""
+    trap = helpers.make_trap_scene(str(tmp_path / "t"))
+    run = helpers.GpuRun(trap)
+    W, H = 96, 64
+    a, b = _stream_nonblocking(), _stream_nonblocking()
+    g = rt.GBuffer(W, H)
+    split = [2, 1, 2, 3]
+    for c, p in enumerate(split):
+        s = a if c < 2 else b
+        rt.render(run.dev, g, run.camera, 0 if c == 0 else 1,
+                  rt.options(W, H, p, adaptive=False, kernel=WF, overlap=c < 2, wf_long_depth=8, stream=s))
+        if c == 1:
+            rt.join(a)  # drain + wf_verify on a; the host does not wait
+    rt.join()
+    ref, _ = helpers.oracle_render(trap, W, H, split)
+    helpers.assert_bitwise(g.download(), ref, what="render on stream b after a join on stream a")
