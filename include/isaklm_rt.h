@@ -58,7 +58,8 @@ extern "C" {
  * rt_join, rt_shutdown; 7 = RtDeviations' hand-off fields (owed passes,
  * safety-net exits, stranded pixels, dropped guard records, linger
  * expiries), RT_E_INCOMPLETE from the joins, rt_profile_history; 8 =
- * RtDeviations.long_closed (the struct grew).  An integrator checks
+ * RtDeviations.long_closed, RtOptions.coalesce_passes (both structs grew).
+ * An integrator checks
  * rt_abi_version() == RT_ABI_VERSION at start-up: a binary built against an
  * older header would otherwise link (C linkage) and mis-pass arguments. */
 #define RT_ABI_VERSION 8
@@ -448,7 +449,9 @@ typedef struct RtOptions {
     /* wavefront: a path deeper than this many bounces (total internal
      * reflection loops in glass reach 10^4 and more) is handed to a kernel
      * running beside the pipelines, which finishes it one ray per wave with
-     * all 64 lanes (0 = default 64, < 0 = off) */
+     * all 64 lanes (0 = default 64, < 0 = off; values below 16 are raised to
+     * 16: the long-path kernel is sized for rare deep paths, and at 8 it took
+     * a third of all paths and ran 7x slower) */
     int wf_long_depth;
     /* ray queries (identical results either way): RT_TRAVERSAL_BOUNDED
      * (default) first finds a lower bound of the ray's first hit distance in
@@ -489,6 +492,16 @@ typedef struct RtOptions {
      * RtDeviations.bounded_mismatches.  < 0: off. */
     int check_interval;
     int debug;           /* RT_DEBUG_* bits: stderr diagnostics of the wavefront calls */
+    /* chained calls (overlap 1) of fewer passes than this are coalesced on
+     * the host (ABI 8): such a call is recorded and returns; the pending
+     * calls of the same frame, options and stream are launched as ONE chained
+     * call once they hold this many passes, or before anything that must see
+     * them — another call, rt_join and the library's readers of the frame,
+     * rt_last_profile / rt_profile_history (one record per launched batch),
+     * rt_shutdown.  k calls of p passes run each pixel's passes in the same
+     * order as one call of k*p: bit-identical.  0 = default 256; < 0 = off
+     * (every call launches). */
+    int coalesce_passes;
 } RtOptions;
 
 #define RT_TRAVERSAL_BOUNDED 0
@@ -502,6 +515,7 @@ typedef struct RtOptions {
 #define RT_DEBUG_SERIAL_LONG_FIRST 16 /* tests of serialised dispatch (a profiler's counter collection): the
                                        * long-path kernel runs to its end before the path kernel starts */
 #define RT_DEBUG_SERIAL_FIN_FIRST 32  /* ... the path kernel runs to its end before the long-path kernel starts */
+/* (calls with RT_DEBUG_CALL_LOG, _LONG_LOG or _SERIAL_* are never coalesced) */
 
 /* Per-call kernel timing of the last rt_render on this device with
  * RtOptions.profile = 1 (wavefront kernels: HIP events on the pipelines'

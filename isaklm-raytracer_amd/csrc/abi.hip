@@ -23,7 +23,8 @@ int rt_launch_path(const RtDevScene &sc, const RtDevFrame &fr, const RtDevCamera
 int rt_launch_tonemap(const Vec3D *fb, const int *count, RtUChar4 *out, int n, hipStream_t stream);
 int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevCamera &cam, hipStream_t stream,
                         int variant, int tail, int finish_waves, int profile, int cap, int postpone, int wide,
-                        int pipes, int long_depth, int traversal, int overlap, int check_interval, int debug);
+                        int pipes, int long_depth, int traversal, int overlap, int check_interval, int debug,
+                        int coalesce);
 
 int rt_wavefront_device_init();
 int rt_wavefront_join(void *stream, int consume);
@@ -806,7 +807,7 @@ int rt_render(rt_scene_t scene, G_Buffer g, Camera cam, int sample_count, const 
         if (scene->max_depth > RT_STACK_DEPTH ||
             rt_launch_wavefront(scene->dev, fr, dc, stream, o.kernel, o.wf_tail, o.wf_finish_waves, o.profile,
                                 o.wf_descent_cap, o.wf_postpone, o.wf_wide, o.wf_pipelines, o.wf_long_depth,
-                                o.traversal, o.overlap, o.check_interval, o.debug) != 0) {
+                                o.traversal, o.overlap, o.check_interval, o.debug, o.coalesce_passes) != 0) {
             rt_set_error("rt_render: wavefront launch failed: %s", hipGetErrorString(hipGetLastError()));
             return RT_E_HIP;
         }

@@ -141,6 +141,8 @@ static_assert(WF_BLOCK % WF_TBLOCK == 0 && WF_TBLOCK % 64 == 0, "WF_TBLOCK must 
 #define WF_MAX_PIPES 6                // concurrent pipelines (RtOptions.wf_pipelines); more than 3 need GPU_MAX_HW_QUEUES > 4
 #define WF_PIPES_DEFAULT 3
 #define WF_LONG_DEPTH_DEFAULT 64      // RtOptions.wf_long_depth: paths deeper than this go to wf_long
+#define WF_LONG_DEPTH_MIN 16          // ... smaller values are raised to this (profiles/r05/small_calls/long_depth_sweep)
+#define WF_COALESCE_DEFAULT 256       // RtOptions.coalesce_passes: chained calls are coalesced up to this many passes
 #ifndef WF_LONG_BLOCKS
 #define WF_LONG_BLOCKS 64 // wf_long grid (4 waves each, one path per wave at a time)
 #endif
@@ -2254,7 +2256,51 @@ struct ChainKey {
     RtDevCamera cam;
 };
 
+ChainKey chain_key(const RtDevScene &sc, const RtDevFrame &fr, const RtDevCamera &cam, int long_depth)
+{
+    ChainKey key;
+    memset(&key, 0, sizeof key);
+    key.nodes = sc.nodes;
+    key.bvh = sc.bvh_nodes;
+    key.fb = fr.fb;
+    key.sq = fr.sq;
+    key.count = fr.count;
+    key.rng = fr.rng;
+    key.width = fr.width;
+    key.height = fr.height;
+    key.adaptive = fr.adaptive;
+    key.min_samples = fr.min_samples;
+    key.max_depth = fr.max_depth;
+    key.shard_id = fr.shard_id;
+    key.num_shards = fr.num_shards;
+    key.long_depth = long_depth;
+    key.tolerance = fr.tolerance;
+    key.cam = cam;
+    return key;
+}
+
+// Chained calls of fewer passes than RtOptions.coalesce_passes are coalesced
+// on the host: such a call is recorded (its passes added to the pending batch
+// of the same frame, options and stream) and the batch is launched as ONE
+// chained call once it holds that many passes, or before anything that must
+// see it (any other call, a join — rt_join and the library's readers —, the
+// profile readers, rt_shutdown).  k chained calls of p passes are the same
+// per-pixel pass sequence as one call of k*p passes: bit-identical.
+struct Pending {
+    bool on = false;
+    int dev = 0;
+    RtDevScene sc{};
+    RtDevFrame fr{};
+    RtDevCamera cam{};
+    hipStream_t stream = nullptr;
+    int long_depth = 0, debug = 0, calls = 0;
+    bool prof = false;
+    uint32_t check_mask = 0;
+    ChainKey key{};
+};
+
 struct Workspace {
+    Pending pend; // coalesced chained calls not yet launched
     size_t slots = 0;
     int grid = 0;
     int spill_pipes = 0;
@@ -2357,6 +2403,7 @@ int ensure_streams(Workspace &w, int npipes)
 }
 
 int launch_drain(Workspace &w);
+int flush_pending(Workspace &w);
 
 #define WF_PROF_SLOTS 256 // profiled whole calls in flight before their spans are read back
 
@@ -2572,9 +2619,9 @@ int debug_long_log(Workspace &w, unsigned long long *buf);
 // does not wait for the call either: rt_join and the library's readers of the
 // frame do.  Results are bit-identical to unchained calls: a pixel's passes run
 // in order whoever runs them.
-int launch_whole(Workspace &w, int dev, const RtDevScene &sc, const RtDevFrame &fr, const RtDevCamera &cam,
-                 hipStream_t stream, int long_depth, bool prof, bool overlap, uint32_t check_mask, int debug,
-                 bool count)
+int launch_whole_now(Workspace &w, int dev, const RtDevScene &sc, const RtDevFrame &fr, const RtDevCamera &cam,
+                     hipStream_t stream, int long_depth, bool prof, bool overlap, uint32_t check_mask, int debug,
+                     bool count)
 {
     const size_t slots = (size_t)fr.width * fr.height;
     // a resetting call (sample_count 0) neither continues nor opens a chain: its reset of a pixel
@@ -2589,24 +2636,7 @@ int launch_whole(Workspace &w, int dev, const RtDevScene &sc, const RtDevFrame &
                     : 256;
     }
     const int grid = w.cus * 4 * WF_FIN_BVH_WAVES / (WF_BLOCK / 64);
-    ChainKey key;
-    memset(&key, 0, sizeof key);
-    key.nodes = sc.nodes;
-    key.bvh = sc.bvh_nodes;
-    key.fb = fr.fb;
-    key.sq = fr.sq;
-    key.count = fr.count;
-    key.rng = fr.rng;
-    key.width = fr.width;
-    key.height = fr.height;
-    key.adaptive = fr.adaptive;
-    key.min_samples = fr.min_samples;
-    key.max_depth = fr.max_depth;
-    key.shard_id = fr.shard_id;
-    key.num_shards = fr.num_shards;
-    key.long_depth = long_depth;
-    key.tolerance = fr.tolerance;
-    key.cam = cam;
+    const ChainKey key = chain_key(sc, fr, cam, long_depth);
     const bool chained = overlap && w.chain_open && !fr.reset && memcmp(&key, &w.key, sizeof key) == 0;
     // a fresh call: an open chain drained and every earlier call's work on the
     // workspace first (before a larger frame's workspace replaces the old one)
@@ -2784,6 +2814,56 @@ int launch_whole(Workspace &w, int dev, const RtDevScene &sc, const RtDevFrame &
     return 0;
 }
 
+// the pending batch of coalesced chained calls, launched as one chained call
+int flush_pending(Workspace &w)
+{
+    if (!w.pend.on) return 0;
+    Pending b = w.pend;
+    w.pend.on = false;
+    return launch_whole_now(w, b.dev, b.sc, b.fr, b.cam, b.stream, b.long_depth, b.prof, true, b.check_mask, b.debug,
+                            false);
+}
+
+// rt_render's whole call (see launch_whole_now), with small chained calls
+// coalesced (Pending; coalesce <= 0: off)
+int launch_whole(Workspace &w, int dev, const RtDevScene &sc, const RtDevFrame &fr, const RtDevCamera &cam,
+                 hipStream_t stream, int long_depth, bool prof, bool overlap, uint32_t check_mask, int debug,
+                 bool count, int coalesce)
+{
+    // (debug diagnostics per call and forced dispatch orders are per launch: never coalesced)
+    const bool can = overlap && !fr.reset && !count && coalesce > 0 && !fr.wave_times &&
+                     !(debug & (RT_DEBUG_CALL_LOG | RT_DEBUG_LONG_LOG | RT_DEBUG_SERIAL_LONG_FIRST |
+                                RT_DEBUG_SERIAL_FIN_FIRST));
+    if (w.pend.on) {
+        const ChainKey key = chain_key(sc, fr, cam, long_depth);
+        if (can && w.pend.dev == dev && w.pend.stream == stream && w.pend.prof == prof &&
+            w.pend.check_mask == check_mask && w.pend.debug == debug && w.pend.sc.nodes == sc.nodes &&
+            memcmp(&key, &w.pend.key, sizeof key) == 0 && (long long)w.pend.fr.passes + fr.passes < (1LL << 28)) {
+            w.pend.fr.passes += fr.passes;
+            ++w.pend.calls;
+            return w.pend.fr.passes < coalesce ? 0 : flush_pending(w);
+        }
+        if (flush_pending(w) != 0) return -1;
+    }
+    if (can && fr.passes < coalesce) {
+        Pending &b = w.pend;
+        b.on = true;
+        b.dev = dev;
+        b.sc = sc;
+        b.fr = fr;
+        b.cam = cam;
+        b.stream = stream;
+        b.long_depth = long_depth;
+        b.debug = debug;
+        b.calls = 1;
+        b.prof = prof;
+        b.check_mask = check_mask;
+        b.key = chain_key(sc, fr, cam, long_depth);
+        return 0;
+    }
+    return launch_whole_now(w, dev, sc, fr, cam, stream, long_depth, prof, overlap, check_mask, debug, count);
+}
+
 // The drain of an open chain (join_all, i.e. rt_join and every reader of the
 // frame, or the next call that does not continue it): a chained call's
 // finisher leaves pixels wf_long hands back after its pixel list ran out to
@@ -2794,6 +2874,7 @@ int launch_whole(Workspace &w, int dev, const RtDevScene &sc, const RtDevFrame &
 // and every wf_long.
 int launch_drain(Workspace &w)
 {
+    if (flush_pending(w) != 0) return -1; // (coalesced chained calls: launched, then drained)
     if (!w.chain_open) return 0;
     w.chain_open = false;
     const RtDevFrame &fr = w.last_fr;
@@ -3010,7 +3091,7 @@ extern "C" int rt_last_profile(RtProfile *out)
         *out = RtProfile{};
         return RT_OK;
     }
-    if (resolve_profiles(*it->second) != 0) return RT_E_HIP;
+    if (flush_pending(*it->second) != 0 || resolve_profiles(*it->second) != 0) return RT_E_HIP;
     *out = it->second->prof;
     return RT_OK;
 }
@@ -3025,7 +3106,7 @@ extern "C" int rt_profile_history(RtProfile *out, int cap, int *count, int reset
     *count = 0;
     if (it == g_ws.end() || !it->second) return RT_OK;
     Workspace &w = *it->second;
-    if (resolve_profiles(w) != 0) return RT_E_HIP;
+    if (flush_pending(w) != 0 || resolve_profiles(w) != 0) return RT_E_HIP;
     *count = (int)w.prof_hist.size();
     for (int i = 0; i < cap && i < *count; ++i) out[i] = w.prof_hist[i];
     if (reset) w.prof_hist.clear();
@@ -3035,7 +3116,7 @@ extern "C" int rt_profile_history(RtProfile *out, int cap, int *count, int reset
 int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevCamera &cam, hipStream_t stream,
                         int variant, int tail_opt, int finish_waves_opt, int profile, int cap_opt, int postpone_opt,
                         int wide_opt, int pipes_opt, int long_opt, int traversal, int overlap, int check_interval,
-                        int debug)
+                        int debug, int coalesce_opt)
 {
     // 1: wave-cooperative leaves (entries packed as k << 6 | lane: needs < 2^26 entries), 2: static, 3: per-lane fetch
     int trace_kind = variant;
@@ -3050,7 +3131,12 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
     const bool bounded = sc.bvh_nodes != nullptr && ((traversal == RT_TRAVERSAL_BOUNDED && !count) ||
                                                      traversal == RT_TRAVERSAL_BOUNDED_COUNTED);
     // paths deeper than this leave their pipeline for wf_long (cooperative trace only)
-    const int long_depth = trace_kind == 1 && long_opt >= 0 ? (long_opt > 0 ? long_opt : WF_LONG_DEPTH_DEFAULT) : 0;
+    // (at least WF_LONG_DEPTH_MIN: wf_long is sized for the rare deep paths — one path per wave on its 64
+    // blocks —, and at depth 8 the hand-off took a third of all paths and ran 7x slower)
+    const int long_depth = trace_kind == 1 && long_opt >= 0
+                               ? (long_opt > 0 ? (long_opt > WF_LONG_DEPTH_MIN ? long_opt : WF_LONG_DEPTH_MIN)
+                                               : WF_LONG_DEPTH_DEFAULT)
+                               : 0;
     // bounded traversal, not counting: the whole call in the finisher by default
     // — one path per lane to the end of its passes beats queue iterations once
     // a ray query is ~30 dependent loads: 1.22 vs 1.61 s per 256-pass room2m
@@ -3071,7 +3157,7 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
             mask = p2 - 1;
         }
         return launch_whole(w, dev, sc, fr, cam, stream, long_depth, profile != 0, overlap != 0 && !count, mask,
-                            debug, count);
+                            debug, count, coalesce_opt < 0 ? 0 : (coalesce_opt > 0 ? coalesce_opt : WF_COALESCE_DEFAULT));
     }
     // persistent-ish grid for trace/shade (grid-stride over the queue).  512
     // blocks = 2,048 waves = a third of the chip's 6,144 wave slots at the

@@ -57,7 +57,7 @@ class RtOptions(ctypes.Structure):
                 ("wf_descent_cap", ctypes.c_int), ("wf_postpone", ctypes.c_int), ("wf_wide", ctypes.c_int),
                 ("shard_id", ctypes.c_int), ("num_shards", ctypes.c_int), ("wf_pipelines", ctypes.c_int),
                 ("wf_long_depth", ctypes.c_int), ("traversal", ctypes.c_int), ("overlap", ctypes.c_int),
-                ("check_interval", ctypes.c_int), ("debug", ctypes.c_int)]
+                ("check_interval", ctypes.c_int), ("debug", ctypes.c_int), ("coalesce_passes", ctypes.c_int)]
 
 
 class RtProfile(ctypes.Structure):
@@ -395,12 +395,13 @@ TRAVERSAL_BOUNDED_COUNTED = 2  # measurement: the bounded queue trace kernel cou
 def options(width, height, passes=1, adaptive=True, min_samples=100, tolerance=0.05, max_depth=0, stream=None,
             counters=None, kernel=KERNEL_MEGA, wf_tail=0, wf_finish_waves=0, profile=False, wf_descent_cap=0,
             wf_postpone=0, wf_wide=0, shard_id=0, num_shards=1, wave_times=None, wf_pipelines=0, wf_long_depth=0,
-            traversal=None, overlap=False, check_interval=0, debug=0):
+            traversal=None, overlap=False, check_interval=0, debug=0, coalesce_passes=0):
     """RtOptions; traversal: TRAVERSAL_BOUNDED / TRAVERSAL_KD (None: the
     library default, or RT_TRAVERSAL from the environment); overlap: chained
     calls (RtOptions.overlap: join before reading the frame); check_interval:
     the bounded traversal's run-time guard (0: the library default, 1 ray in
-    4096; < 0: off)."""
+    4096; < 0: off); coalesce_passes: chained calls of fewer passes are
+    coalesced up to this many (0: the library default 256; < 0: off)."""
     o = RtOptions()
     lib().rt_default_options(ctypes.byref(o))
     o.width, o.height, o.passes = width, height, passes
@@ -415,6 +416,7 @@ def options(width, height, passes=1, adaptive=True, min_samples=100, tolerance=0
     o.wf_pipelines = wf_pipelines
     o.wf_long_depth = wf_long_depth
     o.overlap, o.check_interval, o.debug = int(overlap), check_interval, debug
+    o.coalesce_passes = coalesce_passes
     if traversal is None and os.environ.get("RT_TRAVERSAL"):
         traversal = {"bounded": TRAVERSAL_BOUNDED, "kd": TRAVERSAL_KD,
                      "bounded_counted": TRAVERSAL_BOUNDED_COUNTED}[os.environ["RT_TRAVERSAL"]]

@@ -39,7 +39,7 @@ class GpuRun:
     def render(self, W, H, passes, calls=1, adaptive=False, min_samples=100, tolerance=0.05, max_depth=0,
                seed_skip=0, count=False, kernel=0, wf_tail=0, wf_finish_waves=0, wf_wide=0, shard_id=0,
                num_shards=1, wf_pipelines=0, wf_long_depth=0, traversal=None, overlap=False, check_interval=0,
-               debug=0, stream=None):
+               debug=0, stream=None, coalesce_passes=0):
         g = rt.GBuffer(W, H, seed_skip)
         cnt = rt.DeviceCounters() if count else None
         per_call = list(passes) if isinstance(passes, (list, tuple)) else [passes] * calls  # passes of each call
@@ -49,7 +49,7 @@ class GpuRun:
                              wf_finish_waves=wf_finish_waves, wf_wide=wf_wide, shard_id=shard_id,
                              num_shards=num_shards, wf_pipelines=wf_pipelines, wf_long_depth=wf_long_depth,
                              traversal=traversal, overlap=overlap, check_interval=check_interval, debug=debug,
-                             stream=stream)
+                             stream=stream, coalesce_passes=coalesce_passes)
             rt.render(self.dev, g, self.camera, 0 if c == 0 else 1, opt)
         rt.join()  # (chained calls: their deep-path tails) — download() uses the null stream
         out = g.download()

@@ -40,17 +40,25 @@ def _stream():
     return s
 
 
+# the chained-call protocol tests launch every call (coalesce_passes < 0): coalescing
+# (the default, RtOptions.coalesce_passes) would merge their small calls into one launch;
+# tests of coalescing pass coalesce_passes explicitly
+NOCO = -1
+
+
 def _render_calls(run, W, H, passes, stream=None, overlap=True, **kw):
+    kw.setdefault("coalesce_passes", NOCO)
     return run.render(W, H, passes, kernel=WF, overlap=overlap, stream=stream, **kw)[0]
 
 
+@pytest.mark.parametrize("coalesce", [NOCO, 0])
 @pytest.mark.parametrize("name,W,H,split", [("room2m", 1920, 1080, [16, 16, 16, 16]),
                                             ("cornell_blob", 640, 360, [1, 2, 5, 8])])
-def test_chained_calls_equal_one_call(name, W, H, split):
+def test_chained_calls_equal_one_call(name, W, H, split, coalesce):
     run = helpers.GpuRun(name)
     one = _render_calls(run, W, H, [sum(split)], overlap=False)
     s = _stream()
-    chained = _render_calls(run, W, H, split, stream=s)
+    chained = _render_calls(run, W, H, split, stream=s, coalesce_passes=coalesce)
     helpers.assert_bitwise(chained, one, what=f"{name} {len(split)} chained calls vs one call")
     assert int(chained[2].sum()) == W * H * sum(split)
 
@@ -89,7 +97,8 @@ def test_checkpoint_mid_chain(tmp_path):
     ck = tmp_path / "mid.gbuf"
     for c in range(4):
         rt.render(run.dev, g, run.camera, 0 if c == 0 else 1,
-                  rt.options(W, H, 1, adaptive=False, kernel=WF, overlap=True, wf_long_depth=8))
+                  rt.options(W, H, 1, adaptive=False, kernel=WF, overlap=True, wf_long_depth=8,
+                             coalesce_passes=NOCO))
     g.save(ck, 4)  # mid-chain: joins (drains) first
     dev = rt.deviation_stats(reset=False)
     assert dev["owed_pixels"] > 0, dev  # the chain was open with owed passes at the save
@@ -99,7 +108,7 @@ def test_checkpoint_mid_chain(tmp_path):
     helpers.assert_bitwise(g2.download(), mid_ref, what="checkpoint taken mid-chain")
     for c in range(3):  # resume: chained calls again, on the loaded G_Buffer
         rt.render(run.dev, g2, run.camera, 1, rt.options(W, H, 1, adaptive=False, kernel=WF, overlap=True,
-                                                         wf_long_depth=8))
+                                                         wf_long_depth=8, coalesce_passes=NOCO))
     ref, _ = helpers.oracle_render(trap, W, H, [1] * 7)
     helpers.assert_bitwise(g2.download(), ref, what="resumed from a mid-chain checkpoint")
 
@@ -119,7 +128,7 @@ def test_long_kernel_quit_is_reported(tmp_path, overlap):
     for c in range(2):
         rt.render(run.dev, g, run.camera, 0 if c == 0 else 1,
                   rt.options(W, H, 2, adaptive=False, kernel=WF, overlap=overlap, wf_long_depth=8,
-                             debug=rt.DEBUG_LONG_QUIT))
+                             debug=rt.DEBUG_LONG_QUIT, coalesce_passes=NOCO))
     with pytest.raises(rt.RtError) as ei:
         rt.join()
     assert f"rt error {rt.E_INCOMPLETE}" in str(ei.value) and "stranded" in str(ei.value), str(ei.value)
@@ -214,7 +223,8 @@ def test_small_frame_after_a_large_one(tmp_path):
     helpers.assert_bitwise(gpu, ref, what="light guide after a 1080p frame")
 
 
-def test_chain_interrupted_by_another_frame(tmp_path):
+@pytest.mark.parametrize("coalesce", [NOCO, 0])
+def test_chain_interrupted_by_another_frame(tmp_path, coalesce):
     """A chain left open on one G_Buffer is drained when a call for another
     frame comes (join_all in the fresh call): both frames equal their
     unchained renders.  The light guide keeps pixels out in wf_long across
@@ -225,10 +235,12 @@ def test_chain_interrupted_by_another_frame(tmp_path):
     ga, gb = rt.GBuffer(W, H), rt.GBuffer(W, H, W * H)
     for c in range(3):
         rt.render(run.dev, ga, run.camera, 0 if c == 0 else 1,
-                  rt.options(W, H, 1, adaptive=False, kernel=WF, overlap=True, wf_long_depth=8))
-    for c in range(3):  # another frame: not a continuation, the open chain drains first
+                  rt.options(W, H, 1, adaptive=False, kernel=WF, overlap=True, wf_long_depth=8,
+                             coalesce_passes=coalesce))
+    for c in range(3):  # another frame: not a continuation, the open chain (or batch) drains first
         rt.render(run.dev, gb, run.camera, 0 if c == 0 else 1,
-                  rt.options(W, H, 2, adaptive=False, kernel=WF, overlap=True, wf_long_depth=8))
+                  rt.options(W, H, 2, adaptive=False, kernel=WF, overlap=True, wf_long_depth=8,
+                             coalesce_passes=coalesce))
     rt.join()
     ra, _ = helpers.oracle_render(trap, W, H, [1, 1, 1])
     rb, _ = helpers.oracle_render(trap, W, H, [2, 2, 2], seed_skip=W * H)
@@ -372,9 +384,47 @@ def test_stream_join_then_render_on_another_stream(tmp_path):
     for c, p in enumerate(split):
         s = a if c < 2 else b
         rt.render(run.dev, g, run.camera, 0 if c == 0 else 1,
-                  rt.options(W, H, p, adaptive=False, kernel=WF, overlap=c < 2, wf_long_depth=8, stream=s))
+                  rt.options(W, H, p, adaptive=False, kernel=WF, overlap=c < 2, wf_long_depth=8, stream=s,
+                             coalesce_passes=NOCO))
         if c == 1:
             rt.join(a)  # drain + wf_verify on a; the host does not wait
     rt.join()
     ref, _ = helpers.oracle_render(trap, W, H, split)
     helpers.assert_bitwise(g.download(), ref, what="render on stream b after a join on stream a")
+
+
+def test_coalesced_chained_calls():
+    """RtOptions.coalesce_passes: chained calls of fewer passes are recorded
+    and launched as one chained call once the batch holds that many passes, or
+    before anything that must see them.  16 chained 1-pass calls with the
+    default threshold (256) run as ONE launch (one profile record); with a
+    threshold of 4, as launches of 4, 4, 4 and 4 passes; a read of the frame in
+    between (rt_tonemap: joins) launches the batch first; a call of another
+    frame launches the batch first.  Every frame equals the oracle's."""
+    run = helpers.GpuRun("cornell_blob")
+    W, H = 320, 180
+    ref, _ = helpers.oracle_render(run.path, W, H, [1] * 16)
+    for thr, launches in ((0, 1), (4, 4)):
+        rt.join()
+        rt.profile_history(reset=True)
+        g = rt.GBuffer(W, H)
+        rt.render(run.dev, g, run.camera, 0, rt.options(W, H, 1, adaptive=False, kernel=WF))  # (resets: not chained)
+        for _ in range(15):
+            rt.render(run.dev, g, run.camera, 1, rt.options(W, H, 1, adaptive=False, kernel=WF, overlap=True,
+                                                            profile=True, coalesce_passes=thr))
+        rt.join()
+        hist = rt.profile_history(reset=True)
+        helpers.assert_bitwise(g.download(), ref, what=f"16 1-pass calls, coalesce_passes {thr}")
+        # the resetting call (not profiled) + 15 chained passes: 1 batch of 15 (thr 256) or 4+4+4+3 (thr 4)
+        assert len(hist) == launches, (thr, len(hist))
+    # a read between chained calls launches (and joins) the pending batch
+    g = rt.GBuffer(W, H)
+    ref8, _ = helpers.oracle_render(run.path, W, H, [1] * 8)
+    for c in range(8):
+        rt.render(run.dev, g, run.camera, 0 if c == 0 else 1, rt.options(W, H, 1, adaptive=False, kernel=WF,
+                                                                         overlap=True))
+        if c == 4:
+            rt.tonemap(g)
+            assert int(g.download()[2].min()) == 5  # the 4 pending chained passes ran before the read
+    rt.join()
+    helpers.assert_bitwise(g.download(), ref8, what="coalesced calls with a read between")

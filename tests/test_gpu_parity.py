@@ -360,14 +360,15 @@ def test_room2m_bench_chained_shape_sparse_pixels():
 
 
 @pytest.mark.timeout(240)
-def test_room2m_single_pass_chained_calls():
+@pytest.mark.parametrize("coalesce", [-1, 0])
+def test_room2m_single_pass_chained_calls(coalesce):
     """The reference's call granularity (one render() per pass,
     rt/main.cu:114-122) through chained calls: room2m at 480x270, 16 chained
     calls of 1 pass, then the join; every pixel against the oracle."""
     run = helpers.GpuRun("room2m")
     W, H = 480, 270
     rt.deviation_stats(reset=True)
-    gpu, _, _ = run.render(W, H, [1] * 16, kernel=rt.KERNEL_WAVEFRONT, overlap=True)
+    gpu, _, _ = run.render(W, H, [1] * 16, kernel=rt.KERNEL_WAVEFRONT, overlap=True, coalesce_passes=coalesce)
     dev = rt.deviation_stats(reset=True)
     ref, _ = helpers.oracle_render(run.path, W, H, [1] * 16)
     helpers.assert_bitwise(gpu, ref, what="room2m, 16 chained 1-pass calls")
