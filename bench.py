@@ -591,6 +591,7 @@ def main(argv=None, binding=None):
     value = total_samples / elapsed / 1e6
     acc = gb.download()[2]
     got = int(acc.sum(dtype=np.int64)) if rank == 0 else None
+    timed_samples = (int(acc.sum(dtype=np.int64)) - cnt_before) if world == 1 else n * P * args.steps
     # rank 0 after the reduce holds every rank's counts
     actual_samples = got - cnt_before if rank == 0 else None
     expect = world * P * (args.warmup + args.steps)
@@ -632,10 +633,9 @@ def main(argv=None, binding=None):
                     busy += b - hi
                     hi = b
             avg_launch_ms = busy / max(launches, 1)
-            counted_launches = cprof["finish_launches"]
-            # per launch: the counted bytes per sample x the samples one timed call runs
-            # (every pixel's passes of its call: W x H x passes-per-call, adaptive off)
-            samples_per_launch = n * sum(p["passes"] for p in profiles) / max(launches, 1)
+            # per launch: the counted bytes per sample x the samples one timed call ran (the timed
+            # region's accumulated samples / its launches: adaptive sampling skips some)
+            samples_per_launch = timed_samples / max(launches, 1)
             trace_bytes = bounded_kernel_bytes(bc) / max(bc["sample"], 1) * samples_per_launch
             counted_launches = 1
             work = {"rays": bc["ray"], "bvh_nodes_per_ray": round(bc["b_bvh_node"] / max(bc["ray"], 1), 2),

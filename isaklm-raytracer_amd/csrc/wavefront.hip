@@ -1731,7 +1731,13 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_check(RtDevScene sc, WfState st, 
     if (n > st.chk_cap && gtid == 0) atomicAdd(dev + RT_DEV_CHK_DROP, (unsigned long long)(n - st.chk_cap));
     n = n < st.chk_cap ? n : st.chk_cap;
     unsigned long long checked = 0, bad = 0;
-    for (uint32_t e = gtid; e < n; e += gridDim.x * WF_BLOCK) {
+    // records over the waves first (record e on wave e % waves, lane e / waves): a small call's
+    // few records run one or two per wave, each re-trace's node fetches alone in its wave, not
+    // 64 in lockstep in the first waves (the slowest re-trace bounds the kernel, and the chained
+    // call two later waits for it: its records reuse this parity)
+    const uint32_t waves = gridDim.x * (WF_BLOCK / 64);
+    const uint32_t first = (uint32_t)(tid & 63) * waves + blockIdx.x * (WF_BLOCK / 64) + (uint32_t)(tid >> 6);
+    for (uint32_t e = first; e < n; e += gridDim.x * WF_BLOCK) {
         const RtF4 a = st.chk[3 * (size_t)e], b = st.chk[3 * (size_t)e + 1], q = st.chk[3 * (size_t)e + 2];
         const Vec3D o = rt_v3(a.x, a.y, a.z), d = rt_v3(b.x, b.y, b.z);
         float bx = 0.0f, by = 0.0f, bz = 0.0f;
@@ -2342,7 +2348,8 @@ struct Workspace {
         int passes;
     };
     std::vector<PendingProf> prof_pending;
-    std::vector<RtProfile> prof_hist; // resolved, since the last rt_profile_history reset
+    std::vector<RtProfile> prof_hist; // resolved, since the last rt_profile_history reset (the newest
+                                      // WF_PROF_HISTORY: a profiling caller that never reads it stays bounded)
     unsigned long long call_seq = 0;
     bool chain_open = false; // the last call was a whole-call call with RtOptions.overlap
     ChainKey key{};
@@ -2427,6 +2434,14 @@ int prof_slot(Workspace &w, hipStream_t s, unsigned long long **span, int passes
     return 0;
 }
 
+#define WF_PROF_HISTORY 65536
+void push_history(Workspace &w, const RtProfile &P)
+{
+    if (w.prof_hist.size() >= WF_PROF_HISTORY) // (drop the oldest half: amortised O(1))
+        w.prof_hist.erase(w.prof_hist.begin(), w.prof_hist.begin() + WF_PROF_HISTORY / 2);
+    w.prof_hist.push_back(P);
+}
+
 // the pending profiled whole calls' spans -> RtProfile records (waits for their finishers)
 int resolve_profiles(Workspace &w)
 {
@@ -2446,7 +2461,7 @@ int resolve_profiles(Workspace &w)
         P.pipelines = 1;
         P.finish_ms = b > a ? (float)((double)(b - a) * 1e-5) : 0.0f; // (s_memrealtime: 100 MHz)
         P.call_ms = P.finish_ms;
-        w.prof_hist.push_back(P);
+        push_history(w, P);
         w.prof = P;
     }
     w.prof_pending.clear();
@@ -3460,7 +3475,7 @@ int rt_launch_wavefront(const RtDevScene &sc, const RtDevFrame &fr, const RtDevC
         if (hi > lo) P.trace_union_ms += hi - lo;
         P.pipelines = npipes;
         w.prof = P;
-        w.prof_hist.push_back(P);
+        push_history(w, P);
     }
     return 0;
 }

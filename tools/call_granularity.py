@@ -17,6 +17,7 @@ total = int(sys.argv[1]) if len(sys.argv) > 1 else 256
 per_calls = [int(x) for a in sys.argv[2:] for x in a.split(",")] or [1, 16, 64, 256]
 scene = os.environ.get("RT_SCENE", "room2m")
 long_depth = int(os.environ.get("RT_LONG_DEPTH", "0"))  # RtOptions.wf_long_depth (0 = default)
+coalesce = int(os.environ.get("RT_COALESCE", "0"))  # RtOptions.coalesce_passes (0 = default 256, -1 = off)
 overlaps = (1,) if os.environ.get("RT_CHAINED_ONLY") else (1, 0)
 W, H = 1920, 1080
 rt.check(rt.lib().rt_set_device(0))
@@ -33,9 +34,11 @@ for pc in per_calls:
         t = time.perf_counter()
         for _ in range(n_calls):
             rt.render(run.dev, g, run.camera, 1, rt.options(W, H, pc, adaptive=False, kernel=rt.KERNEL_WAVEFRONT,
-                                                             overlap=bool(overlap), wf_long_depth=long_depth))
+                                                             overlap=bool(overlap), wf_long_depth=long_depth,
+                                                             coalesce_passes=coalesce))
         rt.join()
         dt = time.perf_counter() - t
         print(json.dumps({"scene": scene, "passes_per_call": pc, "calls": n_calls, "overlap": overlap, "long_depth": long_depth,
+                          "coalesce_passes": coalesce,
                           "seconds": round(dt, 3), "Msamples_per_s": round(W * H * pc * n_calls / dt / 1e6, 1)}),
               flush=True)
