@@ -101,7 +101,9 @@ static_assert(WF_BLOCK % WF_TBLOCK == 0 && WF_TBLOCK % 64 == 0, "WF_TBLOCK must 
 #define WF_TRACE_WAVES 6 // wf_trace_coop occupancy target (blocks of 4 waves per CU = waves per SIMD)
 #endif
 #ifndef WF_BVH_LDS
-#define WF_BVH_LDS 12   // wf_trace_bvh: stack entries in LDS (BVH query and KD descent share the stack)
+#define WF_BVH_LDS 8    // wf_finish_bvh / wf_trace_bvh: stack entries in LDS (BVH query and KD descent share the
+                        // stack; deeper entries go to the HBM spill area).  8, not 12: with the NEE state in LDS
+                        // (WF_NEE_LDS) 12 entries left no room for a wf_long block beside 4 finisher blocks (-9 %)
 #endif
 #ifndef WF_BVH_WAVES
 #define WF_BVH_WAVES 6  // wf_trace_bvh occupancy target
@@ -113,16 +115,21 @@ static_assert(WF_BLOCK % WF_TBLOCK == 0 && WF_TBLOCK % 64 == 0, "WF_TBLOCK must 
 #define WF_BVH_PARK 8 // wf_finish_bvh: BVH node steps per loop trip before a lane's query parks (0: never)
 #endif
 #ifndef WF_FIN_BVH_WAVES
-#define WF_FIN_BVH_WAVES 5 // wf_finish_bvh occupancy target (round 5, with parked queries: 6 -9 %; 4 equal on the bench
-                           // with 65 % less write traffic (128 VGPRs, 29 spilled vs 96 / 117), but its rocprofv3 counter
-                           // passes ran past 240 s where 5 takes 5 s — not understood; re-run on the final tree:
-                           // a 16-pass counter pass finishes in 8 s, but the bench's 256-pass WRITE_SIZE pass
-                           // still runs past 240 s and the bench then reads 446: kept at 5)
+#define WF_FIN_BVH_WAVES 4 // wf_finish_bvh occupancy target: 4 waves/SIMD (128 VGPRs, 29 spilled) run the bench at
+                           // 5's rate (566.8-572.2 vs 562.8-573.1 Msamples/s, round 6) with a third of its HBM traffic
+                           // for spills: 107 vs 324 GB written and 908 vs 1,350 GB fetched per 256-pass call
+                           // (profiles/r06/bench_w4_pmc.json); 6: -9 %.  (Round 5 kept 5 because 4's counter passes
+                           // hung: that was wf_long's start race, fixed in round 6, not the occupancy)
 #endif
 // (chained calls' finishers run one after the other on pipeline 0: a kernel boundary between calls,
 // which a pixel's state crosses for free.  The round-5 variants — a finisher going on with the next
 // issued call, finishers alternating between two streams — measured slower, one of them inexact,
 // and are gone: DESIGN.md §6 keeps their A/B records)
+#ifndef WF_NEE_LDS
+#define WF_NEE_LDS 1 // wf_finish_bvh keeps a NEE set-up's state in LDS (PathRegsL), not in registers: at 4 waves/SIMD
+                     // 8 VGPRs spilled instead of 30, 64 instead of 107 GB written per 256-pass call, the bench
+                     // unchanged (569.5 vs 569.3; profiles/r06/bench_nee_lds_pmc.json)
+#endif
 #ifndef WF_FIN_SMALL_WAVES
 #define WF_FIN_SMALL_WAVES 3 // frames of at most this many finisher waves per SIMD take the unspilled build (151 VGPRs: 3 waves)
 #endif
@@ -1043,7 +1050,51 @@ struct PathRegs {
     Vec3D T, L, rp, cont, snorm, ro, rd;
 };
 
-__device__ __forceinline__ void load_regs(const WfState &st, const RtDevFrame &fr, uint32_t slot, PathRegs &p)
+// (wf_finish_bvh) a NEE set-up's state — light point, continuation, shading normal, light — in LDS
+// between the set-up and its shadow ray's shading: written once and read once per diffuse bounce, it
+// holds no registers through the traversal.  Addressed from a wave-uniform base plus the lane id
+// recomputed at use (lane_id_here), so no per-lane address stays live either.
+struct LdsV3 {
+    float *w; // wave-uniform: this wave's column 0 of three WF_BLOCK-strided rows
+    __device__ __forceinline__ operator Vec3D() const
+    {
+        const int l = lane_id_here();
+        return rt_v3(w[l], w[WF_BLOCK + l], w[2 * WF_BLOCK + l]);
+    }
+    __device__ __forceinline__ LdsV3 &operator=(Vec3D v)
+    {
+        const int l = lane_id_here();
+        w[l] = v.x;
+        w[WF_BLOCK + l] = v.y;
+        w[2 * WF_BLOCK + l] = v.z;
+        return *this;
+    }
+    __device__ __forceinline__ LdsV3 &operator=(const LdsV3 &o) { return *this = (Vec3D)o; }
+};
+struct LdsInt {
+    int *w;
+    __device__ __forceinline__ operator int() const { return w[lane_id_here()]; }
+    __device__ __forceinline__ LdsInt &operator=(int v)
+    {
+        w[lane_id_here()] = v;
+        return *this;
+    }
+    __device__ __forceinline__ LdsInt &operator=(const LdsInt &o) { return *this = (int)o; }
+};
+// PathRegs with the NEE state in LDS (the same fields: shade_step and the load / store helpers take either)
+struct PathRegsL {
+    uint32_t slot;
+    bool shadow, inside, dual, ext_live;
+    int prev_type, depth, passes_left;
+    LdsInt light;
+    uint32_t rng;
+    Vec3D T, L;
+    LdsV3 rp, cont, snorm;
+    Vec3D ro, rd;
+};
+
+template <typename P>
+__device__ __forceinline__ void load_regs(const WfState &st, const RtDevFrame &fr, uint32_t slot, P &p)
 {
     p.slot = slot;
     const uint32_t flags = st.flags[slot];
@@ -1065,7 +1116,8 @@ __device__ __forceinline__ void load_regs(const WfState &st, const RtDevFrame &f
     }
 }
 
-__device__ __forceinline__ void store_regs(const WfState &st, const RtDevFrame &fr, const PathRegs &p)
+template <typename P>
+__device__ __forceinline__ void store_regs(const WfState &st, const RtDevFrame &fr, const P &p)
 {
     const uint32_t slot = p.slot;
     fr.rng[slot] = p.rng;
@@ -1084,7 +1136,8 @@ __device__ __forceinline__ void store_regs(const WfState &st, const RtDevFrame &
 
 // a path of a path list with its first pending ray in p.ro / p.rd (the
 // shadow ray if one is pending: its direction recomputed as it was set up)
-__device__ __forceinline__ void first_ray(const WfState &st, const RtDevFrame &fr, uint32_t slot, PathRegs &p)
+template <typename P>
+__device__ __forceinline__ void first_ray(const WfState &st, const RtDevFrame &fr, uint32_t slot, P &p)
 {
     load_regs(st, fr, slot, p);
     p.ro = st.ro[slot];
@@ -1102,9 +1155,9 @@ __device__ __forceinline__ void first_ray(const WfState &st, const RtDevFrame &f
 // queue iteration as the shadow ray (p.dual, p.ext_live).  The shadow result
 // is still applied first (L += direct * T, then T /= p), in the reference's
 // order.  Any shade_step (DUAL or not) resumes such a path correctly.
-template <bool COUNT, bool DUAL = false>
+template <bool COUNT, bool DUAL = false, typename P>
 __device__ __forceinline__ bool shade_step(const RtDevScene &sc, const RtDevFrame &fr, const RtDevCamera &cam,
-                                           PathRegs &p, int hit, float bx, float by, float bz, int limit, Cnt &c)
+                                           P &p, int hit, float bx, float by, float bz, int limit, Cnt &c)
 {
     bool finish = false, roulette = true, want = false;
     if (!p.shadow) {
@@ -1338,7 +1391,8 @@ __device__ __forceinline__ bool fresh_pixel(const RtDevFrame &fr, uint32_t e, in
 }
 
 // a sample's path state at its camera ray (trace_path's start, rt/path_tracing.cuh:270-277)
-__device__ __forceinline__ void begin_path(PathRegs &p)
+template <typename P>
+__device__ __forceinline__ void begin_path(P &p)
 {
     p.T = rt_v3(1.0f, 1.0f, 1.0f);
     p.L = rt_v3(0.0f, 0.0f, 0.0f);
@@ -1393,7 +1447,16 @@ __global__ void __launch_bounds__(WF_BLOCK, WAVES) wf_finish_bvh(RtDevScene sc, 
         if (st.span) atomicMin(st.span, __builtin_amdgcn_s_memrealtime());
         if (st.long_log && blockIdx.x == 0 && threadIdx.x == 0) st.long_log[0] = __builtin_amdgcn_s_memrealtime();
     }
+#if WF_NEE_LDS
+    __shared__ float s_nee[10 * WF_BLOCK];
+    PathRegsL p;
+    p.rp.w = s_nee + wbase;
+    p.cont.w = s_nee + 3 * WF_BLOCK + wbase;
+    p.snorm.w = s_nee + 6 * WF_BLOCK + wbase;
+    p.light.w = reinterpret_cast<int *>(s_nee + 9 * WF_BLOCK) + wbase;
+#else
     PathRegs p;
+#endif
     p.slot = 0;
     p.ro = p.rd = rt_v3(0, 0, 0);
     bool active = false, exhausted = false; // exhausted: this lane found the path list empty
@@ -2642,8 +2705,8 @@ int launch_whole_now(Workspace &w, int dev, const RtDevScene &sc, const RtDevFra
     // a resetting call (sample_count 0) neither continues nor opens a chain: its reset of a pixel
     // must come before any later pass, and a chained lane may reach a pixel before it does
     overlap = overlap && !fr.reset;
-    // every wave slot at the finisher's occupancy (MI355X: 256 CUs x 4 SIMDs x 5 waves / 4 waves per
-    // block = 1,280 blocks), the last WF_LONG_BLOCKS of them left to wf_long
+    // every wave slot at the finisher's occupancy (MI355X: 256 CUs x 4 SIMDs x 4 waves / 4 waves per
+    // block = 1,024 blocks), the last WF_LONG_BLOCKS of them left to wf_long
     if (!w.cus) {
         hipDeviceProp_t prop;
         w.cus = hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0
