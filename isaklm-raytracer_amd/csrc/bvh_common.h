@@ -38,28 +38,53 @@ RT_HD bool rt_sorted_contains(const float *vals, int lo, int hi, float v)
 // axis (`splits`: per axis sorted, `off[a]..off[a+1]`); one lying in a split
 // plane (and any non-finite ray) takes the plain KD traversal.  About 0.2 % of
 // room2m's rays have a zero component; lying in a split plane is rarer still.
+// (Also an origin beyond 2^64 in |o|_1 takes the plain traversal: the slab
+// test's per-ray products, rt_slab, stay finite below it.)
 RT_HD bool rt_bounded_ray(Vec3D o, Vec3D d, const float *splits, const int *off)
 {
     if (!(o.x - o.x == 0.0f && o.y - o.y == 0.0f && o.z - o.z == 0.0f && d.x - d.x == 0.0f && d.y - d.y == 0.0f &&
           d.z - d.z == 0.0f))
         return false;
+    if (!(fabsf(o.x) + fabsf(o.y) + fabsf(o.z) < 0x1p64f)) return false;
     if (d.x == 0.0f && rt_sorted_contains(splits, off[0], off[1], o.x)) return false;
     if (d.y == 0.0f && rt_sorted_contains(splits, off[1], off[2], o.y)) return false;
     if (d.z == 0.0f && rt_sorted_contains(splits, off[2], off[3], o.z)) return false;
     return true;
 }
 
-// Slab test of a box grown by the ray's margin: om = o + margin, op = o -
-// margin, inv = 1 / d.  True when the ray's [0, best] may meet the box.  An
-// axis-parallel ray (inv = inf) whose origin lies exactly on a grown face
-// makes a NaN there; culling or not is then both correct (no hit point can
-// lie on a grown face: the margins are generous).
-RT_HD bool rt_bvh_box(float lx, float ly, float lz, float hx, float hy, float hz, Vec3D om, Vec3D op, Vec3D inv,
-                      float best, float &tn)
+// The slab test's per-ray constants: inv = 1 / d clamped to [-2^60, 2^60],
+// lo = -(om * inv) and hi = -(op * inv) for om = o + margin, op = o - margin,
+// so that a face costs one fma (rt_bvh_box).  Finite: |inv| <= 2^60, and
+// |om|, |op| < 2^65 (rt_bounded_ray: |o|_1 < 2^64; scene_prepare: scale <
+// 2^64).  Its rounding, u|om inv| + u|lx inv - om inv| in t, is the slab
+// term 3u(|box|_1 + |o|_1) of the margin's derivation as
+// the form (lx - om) * inv's was.  The clamp changes only axes with |d| <
+// 2^-60: over the query (t <= the scene box's exit, <= 6 scale) such a ray
+// moves < 2^-57 scale along the axis, so a hit point in the box leaves its
+// origin inside the grown slab by more than margin / 2, and the clamped
+// interval there still spans beyond +-2^42 scale (no cull); an origin
+// closer to a grown face has no hit point in that box to lose.
+struct RtSlab {
+    Vec3D inv, lo, hi;
+};
+RT_HD RtSlab rt_slab(Vec3D o, Vec3D d, float m)
 {
-    const float ax = (lx - om.x) * inv.x, bx = (hx - op.x) * inv.x;
-    const float ay = (ly - om.y) * inv.y, by = (hy - op.y) * inv.y;
-    const float az = (lz - om.z) * inv.z, bz = (hz - op.z) * inv.z;
+    const float H = 0x1p60f;
+    RtSlab r;
+    r.inv = rt_v3(fminf(fmaxf(1.0f / d.x, -H), H), fminf(fmaxf(1.0f / d.y, -H), H), fminf(fmaxf(1.0f / d.z, -H), H));
+    r.lo = rt_v3(-((o.x + m) * r.inv.x), -((o.y + m) * r.inv.y), -((o.z + m) * r.inv.z));
+    r.hi = rt_v3(-((o.x - m) * r.inv.x), -((o.y - m) * r.inv.y), -((o.z - m) * r.inv.z));
+    return r;
+}
+
+// Slab test of a box grown by the ray's margin (rt_slab).  True when the
+// ray's [0, best] may meet the box, with tn its entry distance.
+RT_HD bool rt_bvh_box(float lx, float ly, float lz, float hx, float hy, float hz, const RtSlab &r, float best,
+                      float &tn)
+{
+    const float ax = fmaf(lx, r.inv.x, r.lo.x), bx = fmaf(hx, r.inv.x, r.hi.x);
+    const float ay = fmaf(ly, r.inv.y, r.lo.y), by = fmaf(hy, r.inv.y, r.hi.y);
+    const float az = fmaf(lz, r.inv.z, r.lo.z), bz = fmaf(hz, r.inv.z, r.hi.z);
     tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
     const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
     return tn <= tf && tf >= 0.0f && tn <= best;

@@ -99,9 +99,7 @@ __device__ __forceinline__ int leaf_scan(const RtF4 *plane, const RtIsectBary *b
 template <bool COUNT, typename STACK>
 __device__ __forceinline__ float bvh_bound(const RtDevScene &sc, Vec3D o, Vec3D d, float best, STACK &stk, Cnt &cn)
 {
-    const float m = rt_ray_margin(o.x, o.y, o.z, sc.bvh_scale);
-    const Vec3D om = rt_v3(o.x + m, o.y + m, o.z + m), op = rt_v3(o.x - m, o.y - m, o.z - m);
-    const Vec3D inv = rt_v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const RtSlab sl = rt_slab(o, d, rt_ray_margin(o.x, o.y, o.z, sc.bvh_scale));
     int sp = 0;
     uint32_t cur = 0; // the root (always an inner node)
     // pop the next subtree that may still hold a smaller s (RT_BVH_EMPTY: none)
@@ -126,8 +124,8 @@ __device__ __forceinline__ float bvh_bound(const RtDevScene &sc, Vec3D o, Vec3D 
             const RtF4 a = ldc4(nd), b = ldc4(nd + 1), c = ldc4(nd + 2);
             const uint2 ch = ldc_u2(nd + 3);
             float tn0, tn1;
-            const bool h0 = rt_bvh_box(a.x, a.y, a.z, a.w, b.x, b.y, om, op, inv, best, tn0) && ch.x != RT_BVH_EMPTY;
-            const bool h1 = rt_bvh_box(b.z, b.w, c.x, c.y, c.z, c.w, om, op, inv, best, tn1) && ch.y != RT_BVH_EMPTY;
+            const bool h0 = rt_bvh_box(a.x, a.y, a.z, a.w, b.x, b.y, sl, best, tn0) && ch.x != RT_BVH_EMPTY;
+            const bool h1 = rt_bvh_box(b.z, b.w, c.x, c.y, c.z, c.w, sl, best, tn1) && ch.y != RT_BVH_EMPTY;
             if (h0 && h1) {
                 const bool second_first = tn1 < tn0;
                 stk.put(sp, second_first ? ch.x : ch.y, second_first ? tn0 : tn1);
@@ -172,13 +170,59 @@ struct BvhPark {
     float best;
 };
 
+// One node step of the 4-wide query: node `cur`'s children whose grown box
+// the ray may meet within [0, best], nearest first — the nearest returned,
+// the others pushed farthest-first with their entry distance (RT_BVH_EMPTY:
+// none hit).  A missed child sorts last by its entry alone (INFINITY; a hit's
+// entry is <= best, finite): a 5-comparator network on (entry, reference).
+template <typename STACK>
+__device__ __forceinline__ uint32_t bvh4_children(const RtDevScene &sc, uint32_t cur, const RtSlab &sl, float best,
+                                                  STACK &stk, int &sp)
+{
+    const RtF4 *nd = sc.bvh4 + 8 * (size_t)cur;
+    const RtF4 lx = ldc4(nd), ly = ldc4(nd + 1), lz = ldc4(nd + 2), hx = ldc4(nd + 3), hy = ldc4(nd + 4),
+               hz = ldc4(nd + 5);
+    const uint4 rf = ldc_u4(reinterpret_cast<const uint32_t *>(nd + 6));
+    float t0, t1, t2, t3;
+    uint32_t r0 = rf.x, r1 = rf.y, r2 = rf.z, r3 = rf.w;
+    if (!(rt_bvh_box(lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, sl, best, t0) && r0 != RT_BVH_EMPTY)) t0 = INFINITY;
+    if (!(rt_bvh_box(lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, sl, best, t1) && r1 != RT_BVH_EMPTY)) t1 = INFINITY;
+    if (!(rt_bvh_box(lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, sl, best, t2) && r2 != RT_BVH_EMPTY)) t2 = INFINITY;
+    if (!(rt_bvh_box(lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, sl, best, t3) && r3 != RT_BVH_EMPTY)) t3 = INFINITY;
+    auto cswap = [](float &ta, uint32_t &ra, float &tb, uint32_t &rb) {
+        const bool sw = tb < ta;
+        const float t = sw ? tb : ta, u = sw ? ta : tb;
+        const uint32_t r = sw ? rb : ra, q = sw ? ra : rb;
+        ta = t;
+        tb = u;
+        ra = r;
+        rb = q;
+    };
+    cswap(t0, r0, t1, r1);
+    cswap(t2, r2, t3, r3);
+    cswap(t0, r0, t2, r2);
+    cswap(t1, r1, t3, r3);
+    cswap(t1, r1, t2, r2);
+    if (t3 != INFINITY) {
+        stk.put(sp, r3, t3);
+        ++sp;
+    }
+    if (t2 != INFINITY) {
+        stk.put(sp, r2, t2);
+        ++sp;
+    }
+    if (t1 != INFINITY) {
+        stk.put(sp, r1, t1);
+        ++sp;
+    }
+    return t0 != INFINITY ? r0 : RT_BVH_EMPTY;
+}
+
 template <bool COUNT, bool PARK, typename STACK>
 __device__ __forceinline__ bool bvh4_query(const RtDevScene &sc, Vec3D o, Vec3D d, float best0, STACK &stk, Cnt &cn,
                                            int cap, bool resume, BvhPark &pk)
 {
-    const float m = rt_ray_margin(o.x, o.y, o.z, sc.bvh_scale);
-    const Vec3D om = rt_v3(o.x + m, o.y + m, o.z + m), op = rt_v3(o.x - m, o.y - m, o.z - m);
-    const Vec3D inv = rt_v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const RtSlab sl = rt_slab(o, d, rt_ray_margin(o.x, o.y, o.z, sc.bvh_scale));
     int sp = 0;
     uint32_t cur = 0; // the root (always an inner node)
     float best = best0;
@@ -210,56 +254,8 @@ __device__ __forceinline__ bool bvh4_query(const RtDevScene &sc, Vec3D o, Vec3D 
                 ++steps;
             }
             if (COUNT) cn.v[RT_CNT_B_BVH_NODE]++;
-            const RtF4 *nd = sc.bvh4 + 8 * (size_t)cur;
-            const RtF4 lx = ldc4(nd), ly = ldc4(nd + 1), lz = ldc4(nd + 2), hx = ldc4(nd + 3), hy = ldc4(nd + 4),
-                       hz = ldc4(nd + 5);
-            const uint4 rf = ldc_u4(reinterpret_cast<const uint32_t *>(nd + 6));
-            float t0, t1, t2, t3;
-            uint32_t r0 = rf.x, r1 = rf.y, r2 = rf.z, r3 = rf.w;
-            if (!(rt_bvh_box(lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, om, op, inv, best, t0) && r0 != RT_BVH_EMPTY)) {
-                t0 = INFINITY;
-                r0 = RT_BVH_EMPTY;
-            }
-            if (!(rt_bvh_box(lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, om, op, inv, best, t1) && r1 != RT_BVH_EMPTY)) {
-                t1 = INFINITY;
-                r1 = RT_BVH_EMPTY;
-            }
-            if (!(rt_bvh_box(lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, om, op, inv, best, t2) && r2 != RT_BVH_EMPTY)) {
-                t2 = INFINITY;
-                r2 = RT_BVH_EMPTY;
-            }
-            if (!(rt_bvh_box(lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, om, op, inv, best, t3) && r3 != RT_BVH_EMPTY)) {
-                t3 = INFINITY;
-                r3 = RT_BVH_EMPTY;
-            }
-            // sort the 4 (entry, ref) pairs by entry (misses last): a 5-comparator network
-            auto cswap = [](float &ta, uint32_t &ra, float &tb, uint32_t &rb) {
-                const bool sw = tb < ta || (ra == RT_BVH_EMPTY && rb != RT_BVH_EMPTY);
-                const float t = sw ? tb : ta, u = sw ? ta : tb;
-                const uint32_t r = sw ? rb : ra, q = sw ? ra : rb;
-                ta = t;
-                tb = u;
-                ra = r;
-                rb = q;
-            };
-            cswap(t0, r0, t1, r1);
-            cswap(t2, r2, t3, r3);
-            cswap(t0, r0, t2, r2);
-            cswap(t1, r1, t3, r3);
-            cswap(t1, r1, t2, r2);
-            if (r3 != RT_BVH_EMPTY) {
-                stk.put(sp, r3, t3);
-                ++sp;
-            }
-            if (r2 != RT_BVH_EMPTY) {
-                stk.put(sp, r2, t2);
-                ++sp;
-            }
-            if (r1 != RT_BVH_EMPTY) {
-                stk.put(sp, r1, t1);
-                ++sp;
-            }
-            cur = r0 != RT_BVH_EMPTY ? r0 : pop();
+            const uint32_t next = bvh4_children(sc, cur, sl, best, stk, sp);
+            cur = next != RT_BVH_EMPTY ? next : pop();
         }
         if (cur == RT_BVH_EMPTY) break;
         const uint32_t first = (cur & ~RT_BVH_LEAF) >> 3, end = first + (cur & 7u) + 1u;

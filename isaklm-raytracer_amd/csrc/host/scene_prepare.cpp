@@ -299,7 +299,9 @@ int prepare_host(const Triangle *tris, int ntris, const KD_Tree_Node *nodes, int
             out.bvh_bary[k] = tbary[bvh.order[k]];
         }
         out.bvh_scale = bvh.scale;
-        out.bvh_depth = out.bvh4_stack < RT_BVH_STACK ? bvh.depth : -1; // (too deep: the KD traversal alone)
+        // (too deep, or a scene beyond 2^64 in |vertex|_1 — the slab test's per-ray products, bvh_common.h
+        // rt_slab, need it below —: the KD traversal alone)
+        out.bvh_depth = out.bvh4_stack < RT_BVH_STACK && bvh.scale < 0x1p64f ? bvh.depth : -1;
         // the grid cells' start nodes: wf_long enters each deep bounce's KD traversal at the cell
         // of the ray's origin (coop_trace.h kd_origin_frontier)
         build_kd_starts(out, bounds);

@@ -571,8 +571,9 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_DYN_WAVES) wf_trace_bvh_dyn(RtDev
     uint2 nd = make_uint2(0u, 0u);
     bool nd_ok = false; // nd holds node's words
     int sp = 0;
-    Vec3D o = rt_v3(0, 0, 0), d = rt_v3(0, 0, 0), inv = rt_v3(0, 0, 0);
-    float m = 0.0f, best = 0.0f, entry = 0.0f, exit_ = 0.0f, root_exit = 0.0f, s_min = 0.0f;
+    Vec3D o = rt_v3(0, 0, 0), d = rt_v3(0, 0, 0);
+    RtSlab sl{rt_v3(0, 0, 0), rt_v3(0, 0, 0), rt_v3(0, 0, 0)};
+    float best = 0.0f, entry = 0.0f, exit_ = 0.0f, root_exit = 0.0f, s_min = 0.0f;
     while (true) {
         // ---- refill: lanes without a ray take the next queued one
         const bool need = phase == 0 && !exhausted;
@@ -597,8 +598,7 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_DYN_WAVES) wf_trace_bvh_dyn(RtDev
                         sp = 0;
                         if (rt_bounded_ray(o, d, sc.split_vals, sc.split_off)) {
                             phase = 1;
-                            m = rt_ray_margin(o.x, o.y, o.z, sc.bvh_scale);
-                            inv = rt_v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+                            sl = rt_slab(o, d, rt_ray_margin(o.x, o.y, o.z, sc.bvh_scale));
                             best = exit_;
                             cur = 0;
                         } else {
@@ -621,48 +621,9 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_DYN_WAVES) wf_trace_bvh_dyn(RtDev
             if (!__any(step)) break;
             if (step) {
                 if (COUNT) c.v[RT_CNT_B_BVH_NODE]++;
-                const Vec3D om = rt_v3(o.x + m, o.y + m, o.z + m), op = rt_v3(o.x - m, o.y - m, o.z - m);
-                const RtF4 *p4 = sc.bvh4 + 8 * (size_t)cur;
-                const RtF4 lx = ldc4(p4), ly = ldc4(p4 + 1), lz = ldc4(p4 + 2), hx = ldc4(p4 + 3),
-                           hy = ldc4(p4 + 4), hz = ldc4(p4 + 5);
-                const uint4 rf = ldc_u4(reinterpret_cast<const uint32_t *>(p4 + 6));
-                float t0, t1, t2, t3;
-                uint32_t r0 = rf.x, r1 = rf.y, r2 = rf.z, r3 = rf.w;
-                if (!(rt_bvh_box(lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, om, op, inv, best, t0) && r0 != RT_BVH_EMPTY)) {
-                    t0 = INFINITY;
-                    r0 = RT_BVH_EMPTY;
-                }
-                if (!(rt_bvh_box(lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, om, op, inv, best, t1) && r1 != RT_BVH_EMPTY)) {
-                    t1 = INFINITY;
-                    r1 = RT_BVH_EMPTY;
-                }
-                if (!(rt_bvh_box(lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, om, op, inv, best, t2) && r2 != RT_BVH_EMPTY)) {
-                    t2 = INFINITY;
-                    r2 = RT_BVH_EMPTY;
-                }
-                if (!(rt_bvh_box(lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, om, op, inv, best, t3) && r3 != RT_BVH_EMPTY)) {
-                    t3 = INFINITY;
-                    r3 = RT_BVH_EMPTY;
-                }
-                auto cswap = [](float &ta, uint32_t &ra, float &tb, uint32_t &rb) {
-                    const bool sw = tb < ta || (ra == RT_BVH_EMPTY && rb != RT_BVH_EMPTY);
-                    const float t = sw ? tb : ta, u = sw ? ta : tb;
-                    const uint32_t r = sw ? rb : ra, qq = sw ? ra : rb;
-                    ta = t;
-                    tb = u;
-                    ra = r;
-                    rb = qq;
-                };
-                cswap(t0, r0, t1, r1);
-                cswap(t2, r2, t3, r3);
-                cswap(t0, r0, t2, r2);
-                cswap(t1, r1, t3, r3);
-                cswap(t1, r1, t2, r2);
-                if (r3 != RT_BVH_EMPTY) stk.put(sp++, r3, t3);
-                if (r2 != RT_BVH_EMPTY) stk.put(sp++, r2, t2);
-                if (r1 != RT_BVH_EMPTY) stk.put(sp++, r1, t1);
-                if (r0 != RT_BVH_EMPTY) {
-                    cur = r0;
+                const uint32_t next = bvh4_children(sc, cur, sl, best, stk, sp);
+                if (next != RT_BVH_EMPTY) {
+                    cur = next;
                 } else { // pop the next subtree that may still hold a smaller s
                     cur = RT_BVH_EMPTY;
                     while (sp > 0) {

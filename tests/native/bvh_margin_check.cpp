@@ -154,10 +154,9 @@ void check_triangle(Vec3D p1, Vec3D p2, Vec3D p3, int rays, Stats &st)
             continue;
         }
         const float mr = rt_ray_margin(o.x, o.y, o.z, fscale);
-        const Vec3D om = rt_v3(o.x + mr, o.y + mr, o.z + mr), op = rt_v3(o.x - mr, o.y - mr, o.z - mr);
-        const Vec3D inv = rt_v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+        const RtSlab sl = rt_slab(o, d, mr);
         float tn;
-        const bool kept = rt_bvh_box(glo[0], glo[1], glo[2], ghi[0], ghi[1], ghi[2], om, op, inv, s, tn);
+        const bool kept = rt_bvh_box(glo[0], glo[1], glo[2], ghi[0], ghi[1], ghi[2], sl, s, tn);
         // the slack: how far outside the vertex box the exact hit point lies
         const double P[3] = {(double)o.x + (double)d.x * s, (double)o.y + (double)d.y * s, (double)o.z + (double)d.z * s};
         double out = 0.0;

@@ -144,8 +144,7 @@ Hit kd_trace(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, float entry, floa
 float bvh_bound(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, float best, Work &w)
 {
     const float m = rt_ray_margin(o.x, o.y, o.z, h.bvh_scale);
-    const Vec3D om = rt_v3(o.x + m, o.y + m, o.z + m), op = rt_v3(o.x - m, o.y - m, o.z - m);
-    const Vec3D inv = rt_v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const RtSlab sl = rt_slab(o, d, m);
     struct E { uint32_t ref; float tn; };
     E stk[RT_BVH_STACK];
     int sp = 0;
@@ -158,9 +157,9 @@ float bvh_bound(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, float best, Wo
             memcpy(&c0, &nd[3].x, 4);
             memcpy(&c1, &nd[3].y, 4);
             float tn0, tn1;
-            const bool h0 = rt_bvh_box(nd[0].x, nd[0].y, nd[0].z, nd[0].w, nd[1].x, nd[1].y, om, op, inv, best, tn0) &&
+            const bool h0 = rt_bvh_box(nd[0].x, nd[0].y, nd[0].z, nd[0].w, nd[1].x, nd[1].y, sl, best, tn0) &&
                             c0 != RT_BVH_EMPTY;
-            const bool h1 = rt_bvh_box(nd[1].z, nd[1].w, nd[2].x, nd[2].y, nd[2].z, nd[2].w, om, op, inv, best, tn1) &&
+            const bool h1 = rt_bvh_box(nd[1].z, nd[1].w, nd[2].x, nd[2].y, nd[2].z, nd[2].w, sl, best, tn1) &&
                             c1 != RT_BVH_EMPTY;
             if (h0 && h1) {
                 const bool sf = tn1 < tn0;
@@ -203,8 +202,7 @@ long long g_bvh4_mism = 0;
 float bvh4_bound(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, float best, Work &w)
 {
     const float m = rt_ray_margin(o.x, o.y, o.z, h.bvh_scale);
-    const Vec3D om = rt_v3(o.x + m, o.y + m, o.z + m), op = rt_v3(o.x - m, o.y - m, o.z - m);
-    const Vec3D inv = rt_v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const RtSlab sl = rt_slab(o, d, m);
     struct E { uint32_t ref; float tn; };
     std::vector<E> stk;
     uint32_t cur = 0;
@@ -224,7 +222,7 @@ float bvh4_bound(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, float best, W
             E c[4];
             for (int k = 0; k < 4; ++k) {
                 float tn;
-                const bool hit = rt_bvh_box(f[k], f[4 + k], f[8 + k], f[12 + k], f[16 + k], f[20 + k], om, op, inv,
+                const bool hit = rt_bvh_box(f[k], f[4 + k], f[8 + k], f[12 + k], f[16 + k], f[20 + k], sl,
                                             best, tn) && rf[k] != RT_BVH_EMPTY;
                 c[k] = hit ? E{rf[k], tn} : E{RT_BVH_EMPTY, INFINITY};
             }

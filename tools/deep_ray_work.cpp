@@ -99,8 +99,7 @@ int kd(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, float entry, float exit
 float bvh2(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, float best, double &nodes, double &leaves)
 {
     const float m = rt_ray_margin(o.x, o.y, o.z, h.bvh_scale);
-    const Vec3D om = rt_v3(o.x + m, o.y + m, o.z + m), op = rt_v3(o.x - m, o.y - m, o.z - m);
-    const Vec3D inv = rt_v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const RtSlab sl = rt_slab(o, d, m);
     struct E { uint32_t r; float tn; } stk[RT_BVH_STACK];
     int sp = 0;
     uint32_t cur = 0;
@@ -112,8 +111,8 @@ float bvh2(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, float best, double 
             memcpy(&c0, &nd[3].x, 4);
             memcpy(&c1, &nd[3].y, 4);
             float t0, t1;
-            const bool h0 = rt_bvh_box(nd[0].x, nd[0].y, nd[0].z, nd[0].w, nd[1].x, nd[1].y, om, op, inv, best, t0) && c0 != RT_BVH_EMPTY;
-            const bool h1 = rt_bvh_box(nd[1].z, nd[1].w, nd[2].x, nd[2].y, nd[2].z, nd[2].w, om, op, inv, best, t1) && c1 != RT_BVH_EMPTY;
+            const bool h0 = rt_bvh_box(nd[0].x, nd[0].y, nd[0].z, nd[0].w, nd[1].x, nd[1].y, sl, best, t0) && c0 != RT_BVH_EMPTY;
+            const bool h1 = rt_bvh_box(nd[1].z, nd[1].w, nd[2].x, nd[2].y, nd[2].z, nd[2].w, sl, best, t1) && c1 != RT_BVH_EMPTY;
             if (h0 && h1) {
                 const bool sf = t1 < t0;
                 stk[sp++] = E{sf ? c0 : c1, sf ? t0 : t1};
@@ -202,8 +201,7 @@ float bvh8(const rt_host::PreparedHost &h, const std::vector<Node8> &N, const st
            float best, double &visits, double &leafvis, double &tests)
 {
     const float m = rt_ray_margin(o.x, o.y, o.z, h.bvh_scale);
-    const Vec3D om = rt_v3(o.x + m, o.y + m, o.z + m), op = rt_v3(o.x - m, o.y - m, o.z - m);
-    const Vec3D inv = rt_v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const RtSlab sl = rt_slab(o, d, m);
     struct E { uint32_t r; float tn; } stk[512];
     int sp = 0;
     uint32_t cur = 0;
@@ -213,7 +211,7 @@ float bvh8(const rt_host::PreparedHost &h, const std::vector<Node8> &N, const st
         float tn[8];
         bool hit[8];
         for (int k = 0; k < nd.n; ++k)
-            hit[k] = rt_bvh_box(nd.lo[k][0], nd.lo[k][1], nd.lo[k][2], nd.hi[k][0], nd.hi[k][1], nd.hi[k][2], om, op, inv,
+            hit[k] = rt_bvh_box(nd.lo[k][0], nd.lo[k][1], nd.lo[k][2], nd.hi[k][0], nd.hi[k][1], nd.hi[k][2], sl,
                                 best, tn[k]);
         bool any_leaf = false;
         for (int k = 0; k < nd.n; ++k) {

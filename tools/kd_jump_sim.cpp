@@ -138,8 +138,7 @@ float g_margin_scale = 1.0f; // (experiment: the per-ray margin scaled; results 
 float bvh4_bound(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, float best, Work &w)
 {
     const float m = g_margin_scale * rt_ray_margin(o.x, o.y, o.z, h.bvh_scale);
-    const Vec3D om = rt_v3(o.x + m, o.y + m, o.z + m), op = rt_v3(o.x - m, o.y - m, o.z - m);
-    const Vec3D inv = rt_v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const RtSlab sl = rt_slab(o, d, m);
     struct SE { uint32_t ref; float tn; };
     std::vector<SE> stk;
     uint32_t cur = 0;
@@ -159,7 +158,7 @@ float bvh4_bound(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, float best, W
             SE c[4];
             for (int k = 0; k < 4; ++k) {
                 float tn;
-                const bool hit = rt_bvh_box(f[k], f[4 + k], f[8 + k], f[12 + k], f[16 + k], f[20 + k], om, op, inv,
+                const bool hit = rt_bvh_box(f[k], f[4 + k], f[8 + k], f[12 + k], f[16 + k], f[20 + k], sl,
                                             best, tn) && rf[k] != RT_BVH_EMPTY;
                 c[k] = hit ? SE{rf[k], tn} : SE{RT_BVH_EMPTY, INFINITY};
             }
@@ -305,8 +304,7 @@ float bvh8(const rt_host::PreparedHost &h, const std::vector<Node8> &N, const st
            float best, double &visits, double &leafvis, double &tests)
 {
     const float m = g_margin_scale * rt_ray_margin(o.x, o.y, o.z, h.bvh_scale);
-    const Vec3D om = rt_v3(o.x + m, o.y + m, o.z + m), op = rt_v3(o.x - m, o.y - m, o.z - m);
-    const Vec3D inv = rt_v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const RtSlab sl = rt_slab(o, d, m);
     struct E { uint32_t r; float tn; } stk[512];
     int sp = 0;
     uint32_t cur = 0;
@@ -316,7 +314,7 @@ float bvh8(const rt_host::PreparedHost &h, const std::vector<Node8> &N, const st
         float tn[8];
         bool hit[8];
         for (int k = 0; k < nd.n; ++k)
-            hit[k] = rt_bvh_box(nd.lo[k][0], nd.lo[k][1], nd.lo[k][2], nd.hi[k][0], nd.hi[k][1], nd.hi[k][2], om, op, inv,
+            hit[k] = rt_bvh_box(nd.lo[k][0], nd.lo[k][1], nd.lo[k][2], nd.hi[k][0], nd.hi[k][1], nd.hi[k][2], sl,
                                 best, tn[k]);
         bool any_leaf = false;
         for (int k = 0; k < nd.n; ++k) {
