@@ -111,5 +111,5 @@ RT_HD bool rt_tri_bary(RtF4 B, RtF4 C, RtF4 D, float rd, Vec3D o, Vec3D d, float
     cy = (D.w * d20 - C.w * d21) * rd;
     cz = (B.w * d21 - C.w * d20) * rd;
     cx = 1.0f - cy - cz;
-    return cx >= 0.0f && cx <= 1.0f && cy >= 0.0f && cy <= 1.0f && cz >= 0.0f && cz <= 1.0f;
+    return rt_bary_inside(cx, cy, cz);
 }

@@ -44,7 +44,7 @@ __device__ __forceinline__ bool coop_bary(const RtDevScene &sc, uint32_t k, Vec3
     cz = (B.w * d21 - C.w * d20) * rd;
     cx = 1.0f - cy - cz;
     tri = (int)R.y;
-    return cx >= 0.0f && cx <= 1.0f && cy >= 0.0f && cy <= 1.0f && cz >= 0.0f && cz <= 1.0f;
+    return rt_bary_inside(cx, cy, cz);
 }
 
 // A plane-test candidate in the per-wave LDS list: (entry << 6 | owner lane),
@@ -569,7 +569,7 @@ __device__ __forceinline__ void wide_trace_from(const RtDevScene &sc, Vec3D o, V
                         cz = (B.w * d21 - C.w * d20) * rd;
                         cx = 1.0f - cy - cz;
                         t = (int)R.y;
-                        if (cx >= 0.0f && cx <= 1.0f && cy >= 0.0f && cy <= 1.0f && cz >= 0.0f && cz <= 1.0f) {
+                        if (rt_bary_inside(cx, cy, cz)) {
                             mine = ((unsigned long long)j << 58) | ((unsigned long long)__float_as_uint(s) << 26) |
                                    (unsigned long long)e;
                             atomicMin(wkey, mine);

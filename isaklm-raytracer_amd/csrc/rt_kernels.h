@@ -301,7 +301,7 @@ __device__ __forceinline__ int trace(const RtDevScene &sc, const Vec3D o, const 
                     const float cy = (D.w * d20 - C.w * d21) * rd;
                     const float cz = (B.w * d21 - C.w * d20) * rd;
                     const float cx = 1.0f - cy - cz;
-                    if (cx >= 0.0f && cx <= 1.0f && cy >= 0.0f && cy <= 1.0f && cz >= 0.0f && cz <= 1.0f) {
+                    if (rt_bary_inside(cx, cy, cz)) {
                         smallest = s;
                         best = (int)R.y;
                         bx = cx;

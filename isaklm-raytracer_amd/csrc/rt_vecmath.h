@@ -41,6 +41,21 @@ RT_HD float rt_mod(float x, float m) { return x - m * floorf(x / m); }          
 // origins on a split plane) the plain division runs.  Used for the KD split
 // distance t = (split - o) / d, whose d is one of the ray's 3 components.
 // tests/test_host.py::test_division_matches_ieee checks it against '/'.
+// The barycentric range test of intersect_triangle (rt/trace_ray.cuh:97-110):
+// every coordinate in [0, 1].  On the device as IEEE minimum / maximum
+// (v_minimum3_f32 / v_maximum3_f32): they propagate a NaN, which then fails
+// its compare as a NaN coordinate fails the six; -0 passes both ways.
+RT_HD bool rt_bary_inside(float cx, float cy, float cz)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    const float lo = __builtin_elementwise_minimum(__builtin_elementwise_minimum(cx, cy), cz);
+    const float hi = __builtin_elementwise_maximum(__builtin_elementwise_maximum(cx, cy), cz);
+    return lo >= 0.0f && hi <= 1.0f;
+#else
+    return cx >= 0.0f && cx <= 1.0f && cy >= 0.0f && cy <= 1.0f && cz >= 0.0f && cz <= 1.0f;
+#endif
+}
+
 RT_HD float rt_recip_guard(float d)
 {
     const float a = fabsf(d);

@@ -868,7 +868,7 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_trace_dyn(RtDevScene sc, WfState 
                     const float cy = (D.w * d20 - C.w * d21) * rd;
                     const float cz = (B.w * d21 - C.w * d20) * rd;
                     const float cx = 1.0f - cy - cz;
-                    if (cx >= 0.0f && cx <= 1.0f && cy >= 0.0f && cy <= 1.0f && cz >= 0.0f && cz <= 1.0f) {
+                    if (rt_bary_inside(cx, cy, cz)) {
                         smallest = s;
                         best = (int)R.y;
                         bx = cx;
