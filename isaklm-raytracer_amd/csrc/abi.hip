@@ -111,9 +111,11 @@ int upload_prepared(const rt_host::PreparedHost &h, int ntris, int nindices, rt_
     const int *lights = nullptr;
     const RtF4 *a = nullptr, *sh = nullptr;
     const RtIsectBary *bary = nullptr;
+    const uint32_t *itri = nullptr;
     const RtDevMaterial *mats = nullptr;
     if ((rc = upload_vec(*s, h.nodes, &nodes)) || (rc = upload_vec(*s, h.isect_a, &a)) ||
-        (rc = upload_vec(*s, h.isect_bary, &bary)) || (rc = upload_vec(*s, h.shade, &sh)) ||
+        (rc = upload_vec(*s, h.isect_bary, &bary)) || (rc = upload_vec(*s, h.isect_tri, &itri)) ||
+        (rc = upload_vec(*s, h.shade, &sh)) ||
         (rc = upload_vec(*s, h.materials, &mats)) || (rc = upload_vec(*s, h.lights, &lights))) {
         release(s);
         return rc;
@@ -148,6 +150,7 @@ int upload_prepared(const rt_host::PreparedHost &h, int ntris, int nindices, rt_
     dv.nodes = nodes;
     dv.isect_a = a;
     dv.isect_bary = bary;
+    dv.isect_tri = itri;
     dv.shade = sh;
     dv.materials = mats;
     dv.lights = lights;

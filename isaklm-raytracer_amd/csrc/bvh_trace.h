@@ -95,6 +95,45 @@ __device__ __forceinline__ int leaf_scan(const RtF4 *plane, const RtIsectBary *b
     return best;
 }
 
+// The s_min query's leaf scan (step 2): as leaf_scan, and it also keeps which
+// slot's test set the smallest s (tk; -1: none yet).  A second passing test at
+// exactly that s — another triangle: a triangle has one BVH slot — makes it
+// RT_TK_TIE.  (A test at s == best0, the root's exit, before any pass is no
+// pass: the reference's tests need s < the leaf's exit <= the root's.)
+#define RT_TK_TIE (-2)
+template <bool COUNT>
+__device__ __forceinline__ void leaf_scan_min(const RtF4 *plane, const RtIsectBary *bary, uint32_t e0, uint32_t e1,
+                                              Vec3D o, Vec3D d, float &smallest, int &tk, Cnt &c)
+{
+    for (uint32_t e = e0; e < e1; e += 4) {
+        float s[4];
+        bool p[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const bool in = e + k < e1;
+            const RtF4 A = ldc4(plane + (in ? e + k : e));
+            p[k] = rt_tri_plane(A, o, d, INFINITY, s[k]) && s[k] <= smallest && in;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (!p[k] || !(s[k] <= smallest)) continue;
+            const bool lt = s[k] < smallest;
+            if (!lt && tk < 0) continue; // (at best0, or a tie already)
+            if (COUNT) c.v[RT_CNT_B_BARY]++;
+            float cx, cy, cz;
+            if (rt_tri_bary(ldc4(&bary[e + k].b), ldc4(&bary[e + k].c), ldc4(&bary[e + k].d),
+                            ldc_f(&bary[e + k].rd), o, d, s[k], cx, cy, cz)) {
+                if (lt) {
+                    smallest = s[k];
+                    tk = (int)(e + k);
+                } else {
+                    tk = RT_TK_TIE;
+                }
+            }
+        }
+    }
+}
+
 // s_min of step 2: the smallest s < best of any passing test (best if none)
 template <bool COUNT, typename STACK>
 __device__ __forceinline__ float bvh_bound(const RtDevScene &sc, Vec3D o, Vec3D d, float best, STACK &stk, Cnt &cn)
@@ -168,6 +207,7 @@ struct BvhPark {
     uint32_t cur;
     int sp;
     float best;
+    int tk; // the slot whose test set best (leaf_scan_min)
 };
 
 // One node step of the 4-wide query: node `cur`'s children whose grown box
@@ -226,10 +266,12 @@ __device__ __forceinline__ bool bvh4_query(const RtDevScene &sc, Vec3D o, Vec3D 
     int sp = 0;
     uint32_t cur = 0; // the root (always an inner node)
     float best = best0;
+    int tk = -1;
     if (PARK && resume) {
         sp = pk.sp;
         cur = pk.cur;
         best = pk.best;
+        tk = pk.tk;
     }
     int steps = 0;
     auto pop = [&]() -> uint32_t {
@@ -249,6 +291,7 @@ __device__ __forceinline__ bool bvh4_query(const RtDevScene &sc, Vec3D o, Vec3D 
                     pk.cur = cur;
                     pk.sp = sp;
                     pk.best = best;
+                    pk.tk = tk;
                     return false;
                 }
                 ++steps;
@@ -260,20 +303,23 @@ __device__ __forceinline__ bool bvh4_query(const RtDevScene &sc, Vec3D o, Vec3D 
         if (cur == RT_BVH_EMPTY) break;
         const uint32_t first = (cur & ~RT_BVH_LEAF) >> 3, end = first + (cur & 7u) + 1u;
         if (COUNT) cn.v[RT_CNT_B_BVH_TRI] += end - first;
-        float bx, by, bz;
-        (void)leaf_scan<COUNT>(sc.bvh_a, sc.bvh_bary, first, end, o, d, best, bx, by, bz, cn);
+        leaf_scan_min<COUNT>(sc.bvh_a, sc.bvh_bary, first, end, o, d, best, tk, cn);
         cur = pop();
         if (cur == RT_BVH_EMPTY) break;
     }
     pk.best = best;
+    pk.tk = tk;
     return true;
 }
 
+// (tstar: the triangle whose test alone set s_min — kd_bounded's fast leaf —, else -1)
 template <bool COUNT, typename STACK>
-__device__ __forceinline__ float bvh4_bound(const RtDevScene &sc, Vec3D o, Vec3D d, float best, STACK &stk, Cnt &cn)
+__device__ __forceinline__ float bvh4_bound(const RtDevScene &sc, Vec3D o, Vec3D d, float best, STACK &stk, Cnt &cn,
+                                            int &tstar)
 {
     BvhPark pk;
     (void)bvh4_query<COUNT, false>(sc, o, d, best, stk, cn, 0, false, pk);
+    tstar = pk.tk >= 0 ? (int)sc.bvh_bary[pk.tk].tri : -1;
     return pk.best;
 }
 
@@ -281,8 +327,8 @@ __device__ __forceinline__ float bvh4_bound(const RtDevScene &sc, Vec3D o, Vec3D
 // plain traversal), from the scene box's [entry, root_exit]
 template <bool COUNT, typename STACK>
 __device__ __forceinline__ int kd_bounded(const RtDevScene &sc, const Vec3D o, const Vec3D d, float entry,
-                                          const float root_exit, const float s_min, float &hbx, float &hby, float &hbz,
-                                          STACK &stk, Cnt &c)
+                                          const float root_exit, const float s_min, const int tstar, float &hbx,
+                                          float &hby, float &hbz, STACK &stk, Cnt &c)
 {
     float exit_ = root_exit;
     const float yx = rt_recip_guard(d.x), yy = rt_recip_guard(d.y), yz = rt_recip_guard(d.z);
@@ -324,8 +370,37 @@ __device__ __forceinline__ int kd_bounded(const RtDevScene &sc, const Vec3D o, c
             // trace_leaf_node (:115-172): closest starts at the leaf's exit
             float smallest = exit_;
             float bx = 0.0f, by = 0.0f, bz = 0.0f;
-            if (COUNT) c.v[RT_CNT_TRI] += count;
-            const int be = leaf_scan<COUNT>(sc.isect_a, sc.isect_bary, nd.x, nd.x + count, o, d, smallest, bx, by, bz, c);
+            int be = -1;
+            const uint32_t e0 = nd.x, e1 = nd.x + count;
+            uint32_t lo = e0, hi = e1;
+            if (tstar >= 0) {
+                // s_min is the smallest s of every passing test and T*'s test alone has it (tstar,
+                // leaf_scan_min): where this leaf lists T*, T*'s test is the leaf's result — it passes
+                // (s_min < exit), nothing passes below s_min, nothing else at it — and the reference's
+                // scan returns exactly that entry (its first listing; its arithmetic on the same record)
+                uint32_t at = e1;
+                for (uint32_t e = e0; e < e1 && at == e1; e += 4) {
+                    uint32_t id[4];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) id[k] = *(const RT_CONST uint32_t *)(sc.isect_tri + (e + k < e1 ? e + k : e));
+#pragma unroll
+                    for (int k = 3; k >= 0; --k)
+                        if (e + k < e1 && id[k] == (uint32_t)tstar) at = e + k;
+                }
+                if (at != e1) {
+                    lo = at;
+                    hi = at + 1;
+                }
+            }
+            // (one scan site: T*'s entry, else the whole leaf — and the whole leaf after a T* entry
+            // that did not pass, which the argument above excludes)
+            while (true) {
+                if (COUNT) c.v[RT_CNT_TRI] += hi - lo;
+                be = leaf_scan<COUNT>(sc.isect_a, sc.isect_bary, lo, hi, o, d, smallest, bx, by, bz, c);
+                if (be >= 0 || (lo == e0 && hi == e1)) break;
+                lo = e0;
+                hi = e1;
+            }
             const int best = be >= 0 ? (int)ldc_u2(&sc.isect_bary[be].rd).y : -1;
             if (best >= 0) {
                 if (COUNT) c.v[RT_CNT_HIT]++;
@@ -358,11 +433,12 @@ __device__ __forceinline__ int trace_bvh(const RtDevScene &sc, const Vec3D o, co
     if (!bbox_hit(sc, o, d, entry, exit_)) return -1;
     const float root_exit = exit_;
     float s_min = -INFINITY; // (the plain KD traversal)
+    int tstar = -1;
     if (rt_bounded_ray(o, d, sc.split_vals, sc.split_off)) {
-        s_min = RT_BVH4 ? bvh4_bound<COUNT>(sc, o, d, exit_, stk, c) : bvh_bound<COUNT>(sc, o, d, exit_, stk, c);
+        s_min = RT_BVH4 ? bvh4_bound<COUNT>(sc, o, d, exit_, stk, c, tstar) : bvh_bound<COUNT>(sc, o, d, exit_, stk, c);
         if (!(s_min < root_exit)) return -1;
     }
-    return kd_bounded<COUNT>(sc, o, d, entry, root_exit, s_min, hbx, hby, hbz, stk, c);
+    return kd_bounded<COUNT>(sc, o, d, entry, root_exit, s_min, tstar, hbx, hby, hbz, stk, c);
 }
 
 // trace_bvh with the s_min query parked after `cap` node steps (bvh4_query):
@@ -379,12 +455,14 @@ __device__ __forceinline__ bool trace_bvh_park(const RtDevScene &sc, const Vec3D
     if (!bbox_hit(sc, o, d, entry, exit_)) return true;
     const float root_exit = exit_;
     float s_min = -INFINITY; // (the plain KD traversal)
+    int tstar = -1;
     if (rt_bounded_ray(o, d, sc.split_vals, sc.split_off)) {
         if (!bvh4_query<COUNT, true>(sc, o, d, exit_, stk, c, cap, resume, pk)) return false;
         s_min = pk.best;
         if (!(s_min < root_exit)) return true;
+        if (pk.tk >= 0) tstar = (int)sc.bvh_bary[pk.tk].tri;
     }
-    hit = kd_bounded<COUNT>(sc, o, d, entry, root_exit, s_min, hbx, hby, hbz, stk, c);
+    hit = kd_bounded<COUNT>(sc, o, d, entry, root_exit, s_min, tstar, hbx, hby, hbz, stk, c);
     return true;
 }
 

@@ -251,6 +251,7 @@ int build_bvh(const Triangle *tris, int ntris, const RtF4 *plane, const RtIsectB
     }
     std::vector<uint32_t> keep;
     keep.reserve((size_t)ntris);
+    std::vector<char> always_tri((size_t)ntris, 0);
     for (int i = 0; i < ntris; ++i) {
         const RtIsectBary &r = bary[i];
         const Vec3D p1 = rt_v3(r.b.x, r.b.y, r.b.z), v0 = rt_v3(r.c.x, r.c.y, r.c.z), v1 = rt_v3(r.d.x, r.d.y, r.d.z);
@@ -263,6 +264,7 @@ int build_bvh(const Triangle *tris, int ntris, const RtF4 *plane, const RtIsectB
         Box b;
         if (isinf(m) || !isfinite(t.p1.x + t.p1.y + t.p1.z + t.p2.x + t.p2.y + t.p2.z + t.p3.x + t.p3.y + t.p3.z)) {
             b = all;
+            always_tri[(size_t)i] = 1;
             ++out.always;
         } else {
             b.empty();
@@ -303,6 +305,28 @@ int build_bvh(const Triangle *tris, int ntris, const RtF4 *plane, const RtIsectB
     B.build(0, (int)keep.size(), 0);
     out.depth = B.max_depth;
     out.order = B.prim;
+    // An always-tested triangle (no usable margin) may pass a test with its hit point anywhere on
+    // the ray — even before the ray enters the scene box (the adversarial scene's slivers: a pass
+    // at s = 1.91 for a box entry of 2.62) —, so the boxes of its leaf and of every ancestor are
+    // unbounded (tn = -inf for every ray): visited whatever the query's best, they keep s_min a
+    // lower bound of every passing test.  (The splits were chosen on the finite scene box above.)
+    if (out.always > 0) {
+        std::vector<char> inf(B.nodes.size(), 0);
+        for (size_t id = B.nodes.size(); id-- > 0;) { // children are created after their parent
+            const TNode &t = B.nodes[id];
+            if (t.left < 0) {
+                for (int k = t.first; k < t.first + t.count; ++k) inf[id] |= always_tri[(size_t)B.prim[(size_t)k]];
+            } else {
+                inf[id] = inf[(size_t)t.left] | inf[(size_t)t.right];
+            }
+            if (inf[id]) {
+                for (int a = 0; a < 3; ++a) {
+                    B.nodes[id].box.lo[a] = -INFINITY;
+                    B.nodes[id].box.hi[a] = INFINITY;
+                }
+            }
+        }
+    }
 
     // flatten: every temporary inner node becomes one dual-box node (pre-order)
     std::vector<int> flat((size_t)B.nodes.size(), -1);

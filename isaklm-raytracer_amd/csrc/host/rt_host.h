@@ -50,6 +50,7 @@ struct PreparedHost {
     std::vector<uint32_t> nodes;
     std::vector<RtF4> isect_a;          // leaf-entry order
     std::vector<RtIsectBary> isect_bary; // leaf-entry order
+    std::vector<uint32_t> isect_tri;      // leaf-entry order: the entry's triangle (= isect_bary[e].tri)
     std::vector<RtF4> shade;
     std::vector<RtDevMaterial> materials;
     std::vector<int> lights; // light_count + 1

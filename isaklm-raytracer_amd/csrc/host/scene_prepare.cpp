@@ -259,11 +259,13 @@ int prepare_host(const Triangle *tris, int ntris, const KD_Tree_Node *nodes, int
     const size_t ne = (size_t)(nindices > 0 ? nindices : 0);
     out.isect_a.resize(ne);
     out.isect_bary.resize(ne);
+    out.isect_tri.resize(ne);
 #pragma omp parallel for schedule(static)
     for (long long e = 0; e < (long long)ne; ++e) {
         const int t = indices[e];
         out.isect_a[e] = ta[t];
         out.isect_bary[e] = tbary[t];
+        out.isect_tri[e] = tbary[t].tri;
     }
 
     // --- the conservative BVH (bvh_build.h), records in its leaf order ----

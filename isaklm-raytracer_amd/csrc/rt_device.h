@@ -97,6 +97,7 @@ struct RtDevScene {
     const uint32_t *nodes;      // 2 words per node
     const RtF4 *isect_a;        // per leaf entry: plane
     const RtIsectBary *isect_bary; // per leaf entry: barycentric-test record
+    const uint32_t *isect_tri;  // per leaf entry: its triangle (isect_bary[e].tri, 16 to a line: bvh_trace.h's T* scan)
     const RtF4 *shade;          // 7 per triangle
     const RtDevMaterial *materials;
     const int *lights;          // light_count + 1 entries (SURVEY H4 padding)

@@ -1432,6 +1432,7 @@ __global__ void __launch_bounds__(WF_BLOCK, WAVES) wf_finish_bvh(RtDevScene sc, 
     __shared__ uint32_t s_pk_cur[WF_BLOCK];
     __shared__ int s_pk_sp[WF_BLOCK];
     __shared__ float s_pk_best[WF_BLOCK];
+    __shared__ int s_pk_tk[WF_BLOCK];
     bool parked = false;
 #endif
     while (true) {
@@ -1677,14 +1678,15 @@ __global__ void __launch_bounds__(WF_BLOCK, WAVES) wf_finish_bvh(RtDevScene sc, 
             float bx = 0.0f, by = 0.0f, bz = 0.0f;
 #if WF_BVH_PARK
             int hit;
-            BvhPark pk{0u, 0, 0.0f};
-            if (parked) pk = BvhPark{s_pk_cur[tid], s_pk_sp[tid], s_pk_best[tid]};
+            BvhPark pk{0u, 0, 0.0f, -1};
+            if (parked) pk = BvhPark{s_pk_cur[tid], s_pk_sp[tid], s_pk_best[tid], s_pk_tk[tid]};
             const bool done = trace_bvh_park<COUNT>(sc, p.ro, p.rd, hit, bx, by, bz, stk, c, WF_BVH_PARK, parked, pk);
             parked = !done;
             if (parked) {
                 s_pk_cur[tid] = pk.cur;
                 s_pk_sp[tid] = pk.sp;
                 s_pk_best[tid] = pk.best;
+                s_pk_tk[tid] = pk.tk;
             }
 #else
             const int hit = trace_bvh<COUNT>(sc, p.ro, p.rd, bx, by, bz, stk, c);

@@ -140,6 +140,16 @@ DEGENERATE_OBJ = ("\nusemtl white\nv 0.2 1.2 0.3\nv 0.2 1.2 0.3\nv -0.1 0.9 0.2\
                   "v 0.1 0.2 -0.3\nv 0.1 1.6 -0.3\nv 0.1 1.6 -0.3\nf -3 -2 -1\n")
 
 
+# The same two triangles twice, red then green, facing the camera: every hit on
+# the quad has two passing tests at exactly the same s (identical records), the
+# reference keeps the first listed in its leaf (strict <), and the bounded
+# traversal's T* leaf shortcut must step aside (bvh_trace.h leaf_scan_min: a
+# tie) — the colour says which copy won.
+DUPLICATE_OBJ = ("\nusemtl red\nv -0.45 0.35 0.25\nv 0.45 0.35 0.25\nv 0.45 1.25 0.25\nv -0.45 1.25 0.25\n"
+                 "f -4 -3 -2\nf -4 -2 -1\n"
+                 "usemtl green\nv -0.45 0.35 0.25\nv 0.45 0.35 0.25\nv 0.45 1.25 0.25\nv -0.45 1.25 0.25\n"
+                 "f -4 -3 -2\nf -4 -2 -1\n")
+
 def _mt(n):
     import oracle
 

@@ -72,8 +72,11 @@ bool test(const RtF4 *A, const RtIsectBary *R, uint32_t e, Vec3D o, Vec3D d, flo
 
 // the KD traversal with s_min = -inf is trace_ray itself; with the bound it
 // is bvh_trace.h's step 3
+long long g_fast = 0, g_ties = 0; // T* leaves taken / rays whose s_min two tests share
+
+// tstar >= 0 (bvh_trace.h kd_bounded): a leaf that lists T* tests T*'s entry only
 Hit kd_trace(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, float entry, float exit_, float s_min, Work &w,
-             const Resume *from = nullptr)
+             const Resume *from = nullptr, int tstar = -1)
 {
     Hit hit;
     E stk[64];
@@ -122,7 +125,18 @@ Hit kd_trace(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, float entry, floa
         if (count > 0 && exit_ > s_min) {
             ++w.leaves;
             float smallest = exit_;
-            for (uint32_t e = nx; e < nx + count; ++e) {
+            uint32_t lo = nx, hi = nx + count;
+            if (tstar >= 0) {
+                for (uint32_t e = nx; e < nx + count; ++e)
+                    if (h.isect_tri[e] == (uint32_t)tstar) {
+                        lo = e;
+                        hi = e + 1;
+#pragma omp atomic
+                        ++g_fast;
+                        break;
+                    }
+            }
+            for (uint32_t e = lo; e < hi; ++e) {
                 float s, b[3];
                 ++w.tests;
                 if (test(h.isect_a.data(), h.isect_bary.data(), e, o, d, smallest, s, b)) {
@@ -132,6 +146,10 @@ Hit kd_trace(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, float entry, floa
                 }
             }
             if (hit.tri >= 0) return hit;
+            if (hi - lo != count) {
+                fprintf(stderr, "T* entry of a leaf did not pass\n");
+                exit(3);
+            }
         }
         if (sp == 0) return hit;
         --sp;
@@ -199,8 +217,10 @@ long long g_bvh4_mism = 0;
 
 // the product's s_min query on the 4-wide collapse (bvh_trace.h bvh4_bound):
 // nearest-first, the other hit children pushed farthest-first
-float bvh4_bound(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, float best, Work &w)
+// tstar: the triangle whose test alone set the smallest s (bvh_trace.h leaf_scan_min), else -1
+float bvh4_bound(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, float best, Work &w, int &tstar)
 {
+    int tk = -1; // the slot of the smallest passing test, -2: two tests share it
     const float m = rt_ray_margin(o.x, o.y, o.z, h.bvh_scale);
     const RtSlab sl = rt_slab(o, d, m);
     struct E { uint32_t ref; float tn; };
@@ -234,16 +254,32 @@ float bvh4_bound(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, float best, W
                 if (c[k].ref != RT_BVH_EMPTY) stk.push_back(c[k]);
             cur = c[0].ref != RT_BVH_EMPTY ? c[0].ref : pop();
         }
-        if (cur == RT_BVH_EMPTY) return best;
+        if (cur == RT_BVH_EMPTY) break;
         const uint32_t first = (cur & ~RT_BVH_LEAF) >> 3, end = first + (cur & 7u) + 1u;
         for (uint32_t e = first; e < end; ++e) {
             float s, b[3];
             ++w.bvh_tests;
-            if (test(h.bvh_a.data(), h.bvh_bary.data(), e, o, d, best, s, b)) best = s;
+            if (!rt_tri_plane(h.bvh_a[e], o, d, INFINITY, s) || !(s <= best)) continue;
+            const bool lt = s < best;
+            if (!lt && tk < 0) continue;
+            const RtIsectBary &R = h.bvh_bary[e];
+            if (!rt_tri_bary(R.b, R.c, R.d, bitsf(R.rd), o, d, s, b[0], b[1], b[2])) continue;
+            if (lt) {
+                best = s;
+                tk = (int)e;
+            } else {
+                tk = -2;
+            }
         }
         cur = pop();
-        if (cur == RT_BVH_EMPTY) return best;
+        if (cur == RT_BVH_EMPTY) break;
     }
+    if (tk == -2) {
+#pragma omp atomic
+        ++g_ties;
+    }
+    tstar = tk >= 0 ? (int)h.bvh_bary[tk].tri : -1;
+    return best;
 }
 
 // restatement of coop_trace.h kd_origin_frontier's replay: the descent along
@@ -295,13 +331,14 @@ Hit bounded_trace(const rt_host::PreparedHost &h, Vec3D o, Vec3D d, Work &w)
     if (!rt_bounded_ray(o, d, h.split_vals.data(), h.split_off)) return kd_trace(h, o, d, t1, t2, -INFINITY, w);
     Work w2;
     const float s_bin = bvh_bound(h, o, d, t2, w2);
-    const float s_min = bvh4_bound(h, o, d, t2, w); // the product's query
+    int tstar = -1;
+    const float s_min = bvh4_bound(h, o, d, t2, w, tstar); // the product's query
     if (memcmp(&s_bin, &s_min, 4) != 0) {
 #pragma omp atomic
         ++g_bvh4_mism;
     }
     if (!(s_min < t2)) return Hit{};
-    return kd_trace(h, o, d, t1, t2, s_min, w);
+    return kd_trace(h, o, d, t1, t2, s_min, w, nullptr, tstar);
 }
 
 // the plain traversal entered at the KD node of the grid cell holding the
@@ -367,6 +404,29 @@ int main(int argc, char **argv)
         fprintf(stderr, "prepare failed\n");
         return 2;
     }
+    if (argc > 3 && strcmp(argv[2], "file") == 0) { // a ray file: float32 (n, 6) o, d (tools/dump_rays.py)
+        FILE *f = fopen(argv[3], "rb");
+        if (!f) return 2;
+        std::vector<float> v;
+        float buf[6];
+        while (fread(buf, sizeof buf, 1, f) == 1) v.insert(v.end(), buf, buf + 6);
+        fclose(f);
+        const long long nr = (long long)(v.size() / 6);
+        long long bad = 0;
+        Work wb, wp;
+        for (long long i = 0; i < nr; ++i) {
+            const Vec3D o = rt_v3(v[6 * i], v[6 * i + 1], v[6 * i + 2]), d = rt_v3(v[6 * i + 3], v[6 * i + 4], v[6 * i + 5]);
+            const Hit a = plain_trace(h, o, d, wp), b = bounded_trace(h, o, d, wb);
+            if (a.tri != b.tri || memcmp(a.b, b.b, sizeof a.b) != 0) {
+                if (bad < 5)
+                    printf("mismatch ray %a %a %a %a %a %a: kd %d bounded %d\n", o.x, o.y, o.z, d.x, d.y, d.z, a.tri,
+                           b.tri);
+                ++bad;
+            }
+        }
+        printf("rays %lld mismatches %lld; T* leaves %lld, ties %lld\n", nr, bad, g_fast, g_ties);
+        return bad == 0 ? 0 : 1;
+    }
     if (argc > 3 && strcmp(argv[2], "ray") == 0) { // debug one ray: "ox oy oz dx dy dz" (hex floats)
         Vec3D o, d;
         if (sscanf(argv[3], "%a %a %a %a %a %a", &o.x, &o.y, &o.z, &d.x, &d.y, &d.z) != 6) return 2;
@@ -381,6 +441,11 @@ int main(int argc, char **argv)
         const Hit b = bounded_trace(h, o, d, w);
         g_debug = false;
         printf("box %d [%a, %a] s_min %a kd %d bounded %d\n", in, t1, t2, s_min, a.tri, b.tri);
+        if (in) {
+            int ts = -1;
+            const float s4 = bvh4_bound(h, o, d, t2, w, ts);
+            printf("4-wide query: s_min %a, T* %d\n", s4, ts);
+        }
         for (int e = 0; e < (int)h.isect_a.size(); ++e) { // every passing test (KD entry order)
             float s, bb[3];
             if (test(h.isect_a.data(), h.isect_bary.data(), (uint32_t)e, o, d, INFINITY, s, bb))
@@ -525,5 +590,6 @@ int main(int argc, char **argv)
     printf("origin-cell entry: %lld resumed, mismatches vs the plain traversal %lld\n", g_origin_resumed, g_origin_mism);
     printf("4-wide s_min query: %zu nodes, deepest stack %d, s_min differing from the binary query %lld\n",
            h.bvh4.size() / 8, h.bvh4_stack, g_bvh4_mism);
+    printf("T* leaves: %lld tested by T*'s entry alone; rays whose s_min two tests share: %lld\n", g_fast, g_ties);
     return mism == 0 && g_origin_mism == 0 && g_bvh4_mism == 0 ? 0 : 1;
 }

@@ -17,6 +17,7 @@ tests/test_gpu_traversal.py.
 import os
 import subprocess
 
+import numpy as np
 import pytest
 
 import hazards
@@ -78,6 +79,8 @@ def _run_trace_check(exe, scene, rays=1_000_000, seed=7, cam=None, env=None):
 def test_bounded_equals_kd_host(trace_check, name):
     out = _run_trace_check(trace_check, helpers.scene_path(name))
     assert "mismatches 0" in out, out
+    # the unique-minimum shortcut of the KD phase (bvh_trace.h kd_bounded's T* leaf) is taken
+    assert int(out.split("T* leaves: ")[1].split()[0]) > 100_000, out
     # every triangle of the scene: shipped margin >= the proven bound
     assert "shipped below the proven bound 0, unproven 0" in out, out
 
@@ -88,6 +91,10 @@ def test_bounded_equals_kd_hazard_scenes(trace_check, tmp_path):
     degen = hazards.cornell_variant(str(tmp_path / "d"), "degenerate", yaw_room=0.1, extra_obj=hazards.DEGENERATE_OBJ)
     out = _run_trace_check(trace_check, degen, 500_000)
     assert "mismatches 0" in out and "dropped 0" not in out, out  # the zero-area triangles are left out
+    # two identical copies of a quad: ties at s_min (the T* shortcut steps aside), identical results
+    dup = hazards.cornell_variant(str(tmp_path / "u"), "duplicate", yaw_room=0.1, extra_obj=hazards.DUPLICATE_OBJ)
+    out = _run_trace_check(trace_check, dup, 500_000)
+    assert "mismatches 0" in out and int(out.split("two tests share: ")[1].split()[0]) > 1000, out
     trap = helpers.make_trap_scene(str(tmp_path / "t"))
     assert "mismatches 0" in _run_trace_check(trace_check, trap, 500_000)
     # camera rays from exactly the root split plane
@@ -118,3 +125,38 @@ def test_bounded_equals_kd_adversarial_host(trace_check, tmp_path, variant):
     out = _run_trace_check(trace_check, path, 1_000_000, seed=3)
     assert "rays 1000000" in out and " mismatches 0\n" in out, out
     assert "shipped below the proven bound 0, unproven 0" in out, out
+
+
+# A camera ray of the adversarial "near" scene on which the bounded traversal
+# once returned the wrong triangle: always-tested slivers (no usable margin)
+# pass the reference's test at s = 0.71 and 1.91, before the ray enters the
+# scene box (2.62), and a scene-sized box let the query cull them — s_min then
+# was no lower bound, and the T* leaf returned triangle 107 where the
+# reference returns 44.  (Found by the run-time guard on the GPU,
+# tools/mismatch_ray.py.)
+NEAR_RAY = "-0x1.62103ap-2 0x1.000406p+0 -0x1.caacf8p+1 0x1.64d0bp-7 -0x1.01092ap-2 0x1.ef9396p-1"
+
+
+def test_bounded_equals_kd_real_rays_near_host(trace_check, tmp_path):
+    """The oracle's own rays (camera, bounce and shadow rays of a 160x120
+    frame, oracle or_log_rays) of the adversarial near scene, and the ray
+    above, through the host restatement: bounded == plain KD on every one."""
+    import ctypes
+
+    path = hazards.adversarial_scene(str(tmp_path / "near"), "near")
+    r = subprocess.run([trace_check, path, "ray", NEAR_RAY], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and " kd 44 bounded 44\n" in r.stdout, r.stdout[-2000:]
+    lib = oracle.lib()
+    lib.or_log_rays.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_int] * 2 + [ctypes.c_void_p, ctypes.c_int,
+                                                                            ctypes.c_void_p, ctypes.c_int]
+    osc = oracle.OracleScene(path)
+    W, H = 160, 120
+    pix = np.arange(W * H, dtype=np.int32)
+    rays = np.zeros((len(pix) * 200, 6), np.float32)
+    n = lib.or_log_rays(osc.h, osc.camera.ctypes.data, W, H, pix.ctypes.data, len(pix), rays.ctypes.data,
+                        len(rays))
+    f = str(tmp_path / "rays.f32")
+    rays[:n].tofile(f)
+    r = subprocess.run([trace_check, path, "file", f], capture_output=True, text=True, timeout=600,
+                       env=dict(os.environ, OMP_NUM_THREADS="4"))
+    assert r.returncode == 0 and f"rays {n} mismatches 0;" in r.stdout and n > 30_000, r.stdout

@@ -150,3 +150,16 @@ def test_h7_degenerate_triangles(kernel, tmp_path):
     W, H, P = 40, 32, 3
     haz = _render_both(run, osc, W, H, P, oracle.mt19937(W * H), osc.camera, kernel)
     assert haz["degenerate"] > 1000, haz
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_duplicate_triangles_tie(kernel, tmp_path):
+    """Two identical copies of a quad (hazards.DUPLICATE_OBJ, red then green):
+    their tests tie at exactly the same s on every hit, the reference keeps the
+    copy listed first in the leaf — the BVH query sees the tie and the KD phase
+    scans the leaf in full instead of taking the unique-minimum shortcut."""
+    path = hazards.cornell_variant(str(tmp_path), "duplicate", yaw_room=0.1, extra_obj=hazards.DUPLICATE_OBJ)
+    run = helpers.GpuRun(path)
+    osc = oracle.OracleScene(path)
+    W, H, P = 40, 32, 3
+    _render_both(run, osc, W, H, P, oracle.mt19937(W * H), osc.camera, kernel)
