@@ -372,7 +372,6 @@ __device__ __forceinline__ int kd_bounded(const RtDevScene &sc, const Vec3D o, c
             float bx = 0.0f, by = 0.0f, bz = 0.0f;
             int be = -1;
             const uint32_t e0 = nd.x, e1 = nd.x + count;
-            uint32_t lo = e0, hi = e1;
             if (tstar >= 0) {
                 // s_min is the smallest s of every passing test and T*'s test alone has it (tstar,
                 // leaf_scan_min): where this leaf lists T*, T*'s test is the leaf's result — it passes
@@ -387,19 +386,23 @@ __device__ __forceinline__ int kd_bounded(const RtDevScene &sc, const Vec3D o, c
                     for (int k = 3; k >= 0; --k)
                         if (e + k < e1 && id[k] == (uint32_t)tstar) at = e + k;
                 }
-                if (at != e1) {
-                    lo = at;
-                    hi = at + 1;
+                if (at != e1) { // T*'s entry alone: leaf_scan's test of it, not a 4-wide chunk
+                    float st, cx, cy, cz;
+                    if (COUNT) c.v[RT_CNT_TRI] += 1;
+                    if (rt_tri_plane(ldc4(sc.isect_a + at), o, d, smallest, st) &&
+                        rt_tri_bary(ldc4(&sc.isect_bary[at].b), ldc4(&sc.isect_bary[at].c), ldc4(&sc.isect_bary[at].d),
+                                    ldc_f(&sc.isect_bary[at].rd), o, d, st, cx, cy, cz)) {
+                        smallest = st;
+                        be = (int)at;
+                        bx = cx;
+                        by = cy;
+                        bz = cz;
+                    }
                 }
             }
-            // (one scan site: T*'s entry, else the whole leaf — and the whole leaf after a T* entry
-            // that did not pass, which the argument above excludes)
-            while (true) {
-                if (COUNT) c.v[RT_CNT_TRI] += hi - lo;
-                be = leaf_scan<COUNT>(sc.isect_a, sc.isect_bary, lo, hi, o, d, smallest, bx, by, bz, c);
-                if (be >= 0 || (lo == e0 && hi == e1)) break;
-                lo = e0;
-                hi = e1;
+            if (be < 0) { // the whole leaf (no T*, or a T* entry that did not pass — excluded above)
+                if (COUNT) c.v[RT_CNT_TRI] += count;
+                be = leaf_scan<COUNT>(sc.isect_a, sc.isect_bary, e0, e1, o, d, smallest, bx, by, bz, c);
             }
             const int best = be >= 0 ? (int)ldc_u2(&sc.isect_bary[be].rd).y : -1;
             if (best >= 0) {

@@ -449,8 +449,8 @@ __device__ __forceinline__ int scatter(Vec3D dir, bool &inside, uint32_t &rng, c
     float cos_theta = sqrtf((float)((1.0f - ru) / (ru * (double)(s.roughness * s.roughness - 1.0f) + 1.0f)));
     float sin_theta = sqrtf(1.0f - cos_theta * cos_theta);
     float phi = rng_next(rng) * RT_TAU;
-    float cos_phi = rt_cosf(phi);
-    float sin_phi = rt_sinf(phi);
+    float cos_phi, sin_phi;
+    rt_sincosf(phi, &sin_phi, &cos_phi);
     Vec3D h = s.tangent * sin_theta * cos_phi + s.normal * cos_theta + s.bitangent * sin_theta * sin_phi;
     if (s.extinction > 0.0f) {
         float F = fresnel_conductor(dir, h, s.refractive_index, s.extinction);
@@ -479,8 +479,8 @@ __device__ __forceinline__ int scatter(Vec3D dir, bool &inside, uint32_t &rng, c
     }
     // diffuse_direction (:45-59)
     float dphi = rng_next(rng) * RT_TAU;
-    float ds = rt_sinf(dphi);
-    float dc = rt_cosf(dphi);
+    float ds, dc;
+    rt_sincosf(dphi, &ds, &dc);
     float ru2 = rng_next(rng);
     float sq = sqrtf(ru2);
     out_dir = sq * dc * s.tangent + sqrtf(1.0f - ru2) * s.normal + sq * ds * s.bitangent;
@@ -516,8 +516,10 @@ __device__ __forceinline__ void camera_ray(const RtDevFrame &fr, const RtDevCame
     rd = mat_mul(cam.R, dir);
     float theta = rng_next(rng) * RT_TAU;
     float r = sqrtf(rng_next(rng)) * cam.aperture;
-    float ox = r * rt_cosf(theta);
-    float oy = r * rt_sinf(theta);
+    float st, ct;
+    rt_sincosf(theta, &st, &ct);
+    float ox = r * ct;
+    float oy = r * st;
     ro = rt_v3(cam.pos[0], cam.pos[1], cam.pos[2]) + mat_mul(cam.R, rt_v3(ox, 0.0f, 0.0f)) +
          mat_mul(cam.R, rt_v3(0.0f, oy, 0.0f));
 }

@@ -100,6 +100,27 @@ RT_LIBM_FN double rt_cos_d(double x)
 RT_LIBM_FN float rt_sinf(float x) { return (float)rt_sin_d((double)x); }
 RT_LIBM_FN float rt_cosf(float x) { return (float)rt_cos_d((double)x); }
 
+/* rt_sinf(x) and rt_cosf(x) from one reduction (the same r and quadrant, the
+ * same kernels, the same signs: bit for bit the two calls' results).  The
+ * shading code wants both of one angle; on the GPU a wave whose lanes fall
+ * in different quadrants runs both kernels for each call anyway. */
+RT_LIBM_FN void rt_sincosf(float xf, float *sf, float *cf)
+{
+    const double x = (double)xf;
+    int q;
+    const double r = rt_reduce_pio2(x, &q);
+    const double s = rt_ksin(r), c = rt_kcos(r);
+    double sv, cv;
+    switch (q & 3) {
+    case 0: sv = s; cv = c; break;
+    case 1: sv = c; cv = -s; break;
+    case 2: sv = -s; cv = -c; break;
+    default: sv = -c; cv = s; break;
+    }
+    *sf = x == 0.0 ? xf : (float)sv; /* (rt_sin_d keeps the sign of zero) */
+    *cf = (float)cv;
+}
+
 RT_LIBM_FN float rt_tanf(float xf)
 {
     if (xf == 0.0f) return xf;

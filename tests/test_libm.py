@@ -46,3 +46,21 @@ def test_powf_gamma_domain():
     got = _eval(3, x)
     ref = np.power(x.astype(np.float64), np.float64(np.float32(1 / 2.4))).astype(np.float32)
     assert np.count_nonzero(got != ref) == 0
+
+
+def test_sincos_equals_sin_and_cos(tmp_path):
+    """rt_sincosf (one reduction for both, the shading code's form) gives
+    rt_sinf's and rt_cosf's bits: every 3rd float of [-8, 8], every 4096th
+    float up to 1e6 (tests/native/sincos_check.c; the full [-8, 8] sweep, 2.2
+    billion floats, was run too: 0 mismatches)."""
+    import os
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = str(tmp_path / "sincos_check")
+    subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-fopenmp", "-I",
+                    os.path.join(root, "isaklm-raytracer_amd", "csrc"),
+                    os.path.join(root, "tests", "native", "sincos_check.c"), "-o", exe, "-lm"], check=True)
+    r = subprocess.run([exe, "3"], capture_output=True, text=True, timeout=600,
+                       env=dict(os.environ, OMP_NUM_THREADS="8"))
+    assert r.returncode == 0 and " mismatches 0" in r.stdout and int(r.stdout.split()[1]) > 300_000_000, r.stdout
