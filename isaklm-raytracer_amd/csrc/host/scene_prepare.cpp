@@ -253,7 +253,11 @@ int prepare_host(const Triangle *tris, int ntris, const KD_Tree_Node *nodes, int
         s[3] = f4(t.n1.x, t.n1.y, t.n1.z, t.uv2.x);
         s[4] = f4(t.n2.x, t.n2.y, t.n2.z, t.uv2.y);
         s[5] = f4(t.n3.x, t.n3.y, t.n3.z, t.uv3.x);
-        s[6] = f4(t.uv3.y, 0.0f, 0.0f, 0.0f);
+        // .y: the triangle's area as sample_direct_light computes it for a light (rt/path_tracing.cuh:251-261:
+        // 0.5 * |cross(p2 - p1, p3 - p1)| in double, the magnitude a float sqrtf) — the same operations as
+        // the device's, once per triangle instead of per shadow hit (rt_kernels.h light_contribution)
+        const float area = (float)(0.5 * (double)rt_magnitude(rt_cross(t.p2 - t.p1, t.p3 - t.p1)));
+        s[6] = f4(t.uv3.y, area, 0.0f, 0.0f);
     }
     // ... gathered into leaf-entry order (a leaf's tests read consecutive memory)
     const size_t ne = (size_t)(nindices > 0 ? nindices : 0);

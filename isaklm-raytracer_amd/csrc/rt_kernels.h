@@ -378,9 +378,10 @@ __device__ __forceinline__ void shade(const RtDevScene &sc, int tri, float bx, f
     if (rt_dot(dir, s.normal) > 0) s.normal = -s.normal;
 }
 
-// the part of the hit Sample sample_direct_light uses (normal, emittance)
+// the part of the hit Sample sample_direct_light uses (normal, emittance), and the
+// light's area (precomputed in the record, host/scene_prepare.cpp)
 __device__ __forceinline__ void shade_light(const RtDevScene &sc, int tri, float bx, float by, float bz, Vec3D dir,
-                                            Vec3D &normal, Vec3D &emittance)
+                                            Vec3D &normal, Vec3D &emittance, float &area)
 {
     const RtF4 *r = sc.shade + 7 * (size_t)tri;
     const RtF4 s0 = ldf4(r), s1 = ldf4(r + 1), s2 = ldf4(r + 2), s3 = ldf4(r + 3), s4 = ldf4(r + 4),
@@ -390,6 +391,7 @@ __device__ __forceinline__ void shade_light(const RtDevScene &sc, int tri, float
     emittance = sample_texture(m, rt_v3(m.emittance[0], m.emittance[1], m.emittance[2]), uv);
     normal = rt_normalize(bx * ld3(s3) + by * ld3(s4) + bz * ld3(s5));
     if (rt_dot(dir, normal) > 0) normal = -normal;
+    area = s6.y;
 }
 
 // ---- BSDF (rt/path_tracing.cuh:45-219) ----
@@ -543,10 +545,8 @@ __device__ __forceinline__ Vec3D light_contribution(const RtDevScene &sc, int li
                                                    Vec3D ro, Vec3D rd, Vec3D rp, Vec3D surface_normal)
 {
     Vec3D ln, le;
-    shade_light(sc, light, bx, by, bz, rd, ln, le);
-    const RtF4 *lr = sc.shade + 7 * (size_t)light;
-    const Vec3D lp1 = ld3(ldf4(lr)), lp2 = ld3(ldf4(lr + 1)), lp3 = ld3(ldf4(lr + 2));
-    float area = (float)(0.5 * (double)rt_magnitude(rt_cross(lp2 - lp1, lp3 - lp1)));
+    float area; // (float)(0.5 * (double)|cross(p2 - p1, p3 - p1)|), precomputed
+    shade_light(sc, light, bx, by, bz, rd, ln, le, area);
     float d2 = rt_magnitude_squared(rp - ro);
     float c1 = fmaxf(-rt_dot(rd, ln), 0.0f);
     float c2 = fmaxf(rt_dot(rd, surface_normal), 0.0f);
