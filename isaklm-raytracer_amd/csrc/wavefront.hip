@@ -112,7 +112,9 @@ static_assert(WF_BLOCK % WF_TBLOCK == 0 && WF_TBLOCK % 64 == 0, "WF_TBLOCK must 
 #define WF_CHECK_BLOCKS 256 // wf_check's grid (it runs beside the next call's finisher)
 #endif
 #ifndef WF_BVH_PARK
-#define WF_BVH_PARK 8 // wf_finish_bvh: BVH node steps per loop trip before a lane's query parks (0: never)
+#define WF_BVH_PARK 6 // wf_finish_bvh: BVH node steps per loop trip before a lane's query parks (0: never; re-swept
+                      // after round 6's VALU cuts: 4 / 5 / 6 / 7 / 8 / 12 / 16 = 723-727 / 733 / 738-742 / 739-741 /
+                      // 712-731 / 715 / 699-700 Msamples/s, profiles/r06/ab/ ab16-ab17)
 #endif
 #ifndef WF_FIN_BVH_WAVES
 #define WF_FIN_BVH_WAVES 4 // wf_finish_bvh occupancy target: 4 waves/SIMD (128 VGPRs, 29 spilled) run the bench at
