@@ -149,7 +149,9 @@ static_assert(WF_BLOCK % WF_TBLOCK == 0 && WF_TBLOCK % 64 == 0, "WF_TBLOCK must 
 #define WF_FIN_WIDE_MIN_ENTRIES (1 << 18) // finisher: multi-ray wide tracing only for trees with this many leaf entries
 #define WF_MAX_PIPES 6                // concurrent pipelines (RtOptions.wf_pipelines); more than 3 need GPU_MAX_HW_QUEUES > 4
 #define WF_PIPES_DEFAULT 3
+#ifndef WF_LONG_DEPTH_DEFAULT
 #define WF_LONG_DEPTH_DEFAULT 64      // RtOptions.wf_long_depth: paths deeper than this go to wf_long
+#endif
 #define WF_LONG_DEPTH_MIN 16          // ... smaller values are raised to this (profiles/r05/small_calls/long_depth_sweep)
 #define WF_COALESCE_DEFAULT 256       // RtOptions.coalesce_passes: chained calls are coalesced up to this many passes
 #ifndef WF_LONG_BLOCKS
