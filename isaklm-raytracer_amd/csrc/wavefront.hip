@@ -101,9 +101,10 @@ static_assert(WF_BLOCK % WF_TBLOCK == 0 && WF_TBLOCK % 64 == 0, "WF_TBLOCK must 
 #define WF_TRACE_WAVES 6 // wf_trace_coop occupancy target (blocks of 4 waves per CU = waves per SIMD)
 #endif
 #ifndef WF_BVH_LDS
-#define WF_BVH_LDS 8    // wf_finish_bvh / wf_trace_bvh: stack entries in LDS (BVH query and KD descent share the
-                        // stack; deeper entries go to the HBM spill area).  8, not 12: with the NEE state in LDS
-                        // (WF_NEE_LDS) 12 entries left no room for a wf_long block beside 4 finisher blocks (-9 %)
+#define WF_BVH_LDS 10   // wf_finish_bvh / wf_trace_bvh: stack entries in LDS (BVH query and KD descent share the
+                        // stack; deeper entries go to the HBM spill area).  10 (34.8 KB per block: 4 finisher blocks
+                        // and a wf_long block fit a CU's 160 KB) vs 8 / 9: 745-748 vs 735-738 / 735-742 Msamples/s
+                        // (round 6, profiles/r06/ab/ ab19); 12 left no room for the wf_long block (-9 %)
 #endif
 #ifndef WF_BVH_WAVES
 #define WF_BVH_WAVES 6  // wf_trace_bvh occupancy target
