@@ -225,10 +225,11 @@ __device__ __forceinline__ uint32_t bvh4_children(const RtDevScene &sc, uint32_t
     const uint4 rf = ldc_u4(reinterpret_cast<const uint32_t *>(nd + 6));
     float t0, t1, t2, t3;
     uint32_t r0 = rf.x, r1 = rf.y, r2 = rf.z, r3 = rf.w;
-    if (!(rt_bvh_box(lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, sl, best, t0) && r0 != RT_BVH_EMPTY)) t0 = INFINITY;
-    if (!(rt_bvh_box(lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, sl, best, t1) && r1 != RT_BVH_EMPTY)) t1 = INFINITY;
-    if (!(rt_bvh_box(lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, sl, best, t2) && r2 != RT_BVH_EMPTY)) t2 = INFINITY;
-    if (!(rt_bvh_box(lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, sl, best, t3) && r3 != RT_BVH_EMPTY)) t3 = INFINITY;
+    // (an unused slot's box is culled by its own slab test: host/bvh_build.cpp collapse_bvh4)
+    if (!rt_bvh_box(lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, sl, best, t0)) t0 = INFINITY;
+    if (!rt_bvh_box(lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, sl, best, t1)) t1 = INFINITY;
+    if (!rt_bvh_box(lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, sl, best, t2)) t2 = INFINITY;
+    if (!rt_bvh_box(lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, sl, best, t3)) t3 = INFINITY;
     auto cswap = [](float &ta, uint32_t &ra, float &tb, uint32_t &rb) {
         const bool sw = tb < ta;
         const float t = sw ? tb : ta, u = sw ? ta : tb;

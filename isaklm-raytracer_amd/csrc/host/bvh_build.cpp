@@ -434,6 +434,10 @@ void collapse_bvh4(const std::vector<RtF4> &bin, std::vector<RtF4> &out4)
         float *f = reinterpret_cast<float *>(&out4[8 * i]);
         for (int k = 0; k < 4; ++k) {
             uint32_t ref = RT_BVH_EMPTY;
+            // an unused slot's box lies at +FLT_MAX on every axis: every ray's slab test culls it (entry
+            // +inf or huge where an axis's 1/d > 0, exit -inf where every 1/d < 0; |1/d| >= 1 for a unit
+            // direction), so the query needs no reference check (bvh_trace.h bvh4_children)
+            for (int a = 0; a < 6; ++a) f[4 * a + k] = FLT_MAX;
             if ((size_t)k < wide[i].size()) {
                 const Child &x = wide[i][(size_t)k];
                 ref = (x.ref & RT_BVH_LEAF) ? x.ref : (uint32_t)idx[x.ref];
